@@ -1,0 +1,196 @@
+/*
+ * pgmhip.h — C-ABI of the MI355X (gfx950) discrete-factor engine.
+ *
+ * Plain C types only (pointers, sizes, fixed-layout structs); no torch and no
+ * HIP types cross this boundary (streams travel as opaque `void*`).  Every
+ * entry point returns an int status: PGM_OK (0) or a negative PGM_E* code; the
+ * thread-local message of the last failure is read with pgm_last_error().  No
+ * C++ exception crosses the ABI.  The Python binding is ctypes
+ * (pgmpy_amd/_native.py); INTEGRATION.md shows the stub a pgmpy maintainer adds
+ * to pgmpy/utils/compat_fns.py to bind it.
+ *
+ * The reference (pgmpy 1.0.0, /root/reference) is pure Python: every entry
+ * point below replaces a numpy / opt_einsum call site, cited per function.
+ *
+ * Data layout: factor values are fp64 (pgmpy/global_vars.py:38 DTYPE
+ * "float64") addressed through per-dimension element strides, so a C-order
+ * DiscreteFactor (pgmpy/factors/discrete/DiscreteFactor.py:122, last variable
+ * fastest), a broadcast operand (stride 0), a transposed view, and a batch of
+ * evidence rows (one extra loop dimension, "batch-innermost" stride 1) are all
+ * the same descriptor.  Evidence is column-major uint8 state codes
+ * codes[col * ld + row] (code 255 = not observed).
+ */
+#ifndef PGMHIP_H
+#define PGMHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (Python maps them to the exception pgmpy raises for the same misuse) */
+#define PGM_OK 0
+#define PGM_EINVAL (-1)  /* ValueError  */
+#define PGM_EINDEX (-2)  /* IndexError  (state code >= cardinality)      */
+#define PGM_ENOMEM (-3)  /* MemoryError */
+#define PGM_EDEVICE (-4) /* RuntimeError: HIP runtime failure / no device */
+
+#define PGM_MAX_DIMS 32     /* loop dims accepted per side before coalescing */
+#define PGM_EV_MISSING 255  /* evidence code meaning "not observed" */
+
+/* ---------------------------------------------------------------- runtime */
+int pgm_version(void);                         /* ABI version (PGM_OK-free: returns the number) */
+int pgm_last_error(char *buf, size_t len);     /* copies the thread-local message */
+int pgm_device_count(int *n);
+int pgm_set_device(int device);
+int pgm_alloc(void **ptr, size_t bytes);
+int pgm_free(void *ptr);
+int pgm_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
+int pgm_memset(void *dst, int value, size_t bytes, void *stream);
+int pgm_stream_sync(void *stream);
+/* HIP events, for timing a kernel on the stream it runs on (bench.py) */
+int pgm_event_create(void **ev);
+int pgm_event_destroy(void *ev);
+int pgm_event_record(void *ev, void *stream);
+int pgm_event_elapsed_ms(void *start, void *stop, float *ms);
+
+/* ---------------------------------------------------------------- contract
+ * The one generic kernel behind DiscreteFactor.product / sum / divide /
+ * marginalize / maximize / normalize and every pairwise step of the
+ * sum-product contraction:
+ *
+ *   C[keep] = REDUCE_{red} COMBINE(A[keep, red], B[keep, red])
+ *
+ * keep dims are the output loop (outermost first; C is written at keep_sc
+ * strides), red dims are summed (PGM_RED_SUM) or max-ed (PGM_RED_MAX) away.
+ * Replaces:
+ *   product      np.einsum(A, ia, B, ib, union)    DiscreteFactor.py:771-777
+ *   marginalize  np.einsum(A, range(n), keep)      DiscreteFactor.py:408
+ *   maximize     np.max(A, axis)                   DiscreteFactor.py:480 (compat_fns.py:53-60)
+ *   sum          A + B (broadcast)                 DiscreteFactor.py:712
+ *   divide       A / B, NaN -> 0                   DiscreteFactor.py:859-863
+ *   normalize    A / A.sum()                       DiscreteFactor.py:530 (two calls: SUM, then DIV_RAW)
+ *   one pairwise tensordot/einsum step of opt_einsum.contract(..., "greedy")
+ *                                                  ExactInference.py:404-406, factors/base.py:106
+ */
+enum pgm_combine {
+  PGM_COMBINE_MUL = 0,     /* A*B                                   */
+  PGM_COMBINE_ADD = 1,     /* A+B                                   */
+  PGM_COMBINE_DIV = 2,     /* A/B with NaN -> 0 (factor division)   */
+  PGM_COMBINE_COPY = 3,    /* A (B unused)                          */
+  PGM_COMBINE_DIV_RAW = 4  /* A/B, IEEE (0/0 = NaN, as normalize)   */
+};
+enum pgm_reduce { PGM_RED_NONE = 0, PGM_RED_SUM = 1, PGM_RED_MAX = 2 };
+
+typedef struct {
+  int32_t combine; /* enum pgm_combine */
+  int32_t reduce;  /* enum pgm_reduce  */
+  int32_t n_keep;
+  int32_t n_red;
+  int64_t keep_card[PGM_MAX_DIMS];
+  int64_t keep_sa[PGM_MAX_DIMS];
+  int64_t keep_sb[PGM_MAX_DIMS];
+  int64_t keep_sc[PGM_MAX_DIMS];
+  int64_t red_card[PGM_MAX_DIMS];
+  int64_t red_sa[PGM_MAX_DIMS];
+  int64_t red_sb[PGM_MAX_DIMS];
+} pgm_contract_desc;
+
+/* bytes of device workspace pgm_contract needs for this descriptor (0 = none) */
+int pgm_contract_workspace(const pgm_contract_desc *d, size_t *bytes);
+int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, double *C,
+                 void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------- evidence gather
+ * Batched DiscreteFactor.reduce: one evidence row per value of the batch
+ * loop dim; the reduced variables' states come from the per-row codes.
+ *   C[keep] = A[keep_sa . keep + sum_j codes[ev_col[j]*ld + row] * ev_stride[j]]
+ * Replaces basic indexing values[tuple(slice_)] (DiscreteFactor.py:614;
+ * the greedy path's per-factor slice ExactInference.py:352-365,385).
+ * A code >= ev_card[j] sets *err_flag (-> IndexError, test_Factor.py:555-565);
+ * PGM_EV_MISSING is rejected the same way (the plan must not gather it).
+ */
+typedef struct {
+  int32_t n_keep;
+  int32_t n_ev;
+  int32_t batch_dim; /* index into keep dims that enumerates rows (-1: row 0 only) */
+  int32_t _pad;
+  int64_t ld;        /* leading dimension of codes (rows per column) */
+  int64_t row0;      /* first row of this call (sharding offset) */
+  int64_t keep_card[PGM_MAX_DIMS];
+  int64_t keep_sa[PGM_MAX_DIMS];
+  int64_t keep_sc[PGM_MAX_DIMS];
+  int64_t ev_col[PGM_MAX_DIMS];
+  int64_t ev_stride[PGM_MAX_DIMS];
+  int64_t ev_card[PGM_MAX_DIMS];
+} pgm_gather_desc;
+
+int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
+               int32_t *err_flag, void *stream);
+
+/* 0/1 evidence indicator (BP findings):
+ * out[k*s_state + r*s_row] = (codes[r] == k) or 1 when codes[r] == PGM_EV_MISSING */
+int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *out, int64_t s_state,
+                  int64_t s_row, int32_t *err_flag, void *stream);
+
+/* ---------------------------------------------------------------- argmax
+ * First-flat-index argmax per row (np.argmax semantics incl. NaN-first):
+ * replaces compat_fns.argmax (compat_fns.py:70-74) in map_query
+ * (ExactInference.py:616).  out_idx[r] = argmax_i X[r*s_row + i*s_elem]. */
+int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem,
+               int64_t *out_idx, void *stream);
+
+/* ---------------------------------------------------------------- fused row plan
+ * The batched-evidence hot path (DiscreteBayesianNetwork.predict /
+ * predict_probability, DiscreteBayesianNetwork.py:731-989): per evidence row,
+ * the whole reduce -> sum-product -> normalize -> marginalize/argmax chain of
+ * one evidence pattern in ONE kernel, one lane per row, CPT slices staged in
+ * LDS, no HBM intermediates.  Loop space = query dims (first n_query) then
+ * hidden dims (summed).  Factor f's value for a loop point is
+ *   values[fac_base[f] + sum_j code_j(row) * ev_stride_j + sum_k digit_k * fac_stride[f][k]].
+ */
+#define PGM_ROWS_MAX_LOOP 12
+#define PGM_ROWS_MAX_FAC 16
+#define PGM_ROWS_MAX_EV 48
+#define PGM_ROWS_MAX_ACC 192
+
+enum pgm_rows_mode {
+  PGM_ROWS_MARGINALS = 1, /* per query var normalized marginal (predict_probability) */
+  PGM_ROWS_JOINT = 2,     /* normalized joint over the query dims (query joint=True) */
+  PGM_ROWS_MAP = 4,       /* first-index argmax of the joint (map_query / predict)  */
+  PGM_ROWS_MAPGAP = 8     /* also (best - second best) / best, for tie screening      */
+};
+
+typedef struct {
+  int32_t n_loop;
+  int32_t n_query;
+  int32_t n_fac;
+  int32_t n_ev;
+  int32_t n_values; /* packed CPT values (doubles) */
+  int32_t _pad[3];
+  int32_t loop_card[PGM_ROWS_MAX_LOOP];
+  int32_t fac_base[PGM_ROWS_MAX_FAC];
+  int32_t fac_stride[PGM_ROWS_MAX_FAC][PGM_ROWS_MAX_LOOP];
+  int32_t fac_ev_begin[PGM_ROWS_MAX_FAC]; /* evidence terms of factor f: [begin, end) */
+  int32_t fac_ev_end[PGM_ROWS_MAX_FAC];
+  int32_t ev_col[PGM_ROWS_MAX_EV];
+  int32_t ev_stride[PGM_ROWS_MAX_EV];
+  int32_t ev_card[PGM_ROWS_MAX_EV];
+} pgm_rows_plan;
+
+int pgm_rows_plan_create(const pgm_rows_plan *plan, const double *host_values, void **handle);
+int pgm_rows_plan_destroy(void *handle);
+/* outputs are column-major with leading dim ld_out (>= n_rows), any may be NULL unless its mode bit is set:
+ *   marg  [sum_q card_q][ld_out]   joint [prod_q card_q][ld_out]   map [n_rows] int32   gap [n_rows] */
+int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
+                      int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map,
+                      double *gap, int32_t *err_flag, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGMHIP_H */

@@ -1,0 +1,203 @@
+"""ctypes binding of the C-ABI in include/pgmhip.h (libpgmhip.so, gfx950).
+
+This is the seam where pgmpy's numpy/torch dispatch (pgmpy/utils/compat_fns.py:
+einsum L63-67, max L53-60, argmax L70-74) is replaced by hand-written HIP
+kernels.  There is no CPU fallback: every compute entry point raises
+``NativeUnavailable`` when the library or a GPU is missing, so a silent numpy
+path can never stand in for the device path.
+
+Device buffers are torch tensors (PyTorch is plumbing here: allocator, streams,
+torch.distributed); only raw pointers and the HIP stream handle cross the ABI.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpgmhip.so")
+
+PGM_OK = 0
+PGM_EINVAL = -1
+PGM_EINDEX = -2
+PGM_ENOMEM = -3
+PGM_EDEVICE = -4
+PGM_MAX_DIMS = 32
+PGM_EV_MISSING = 255
+
+COMBINE_MUL, COMBINE_ADD, COMBINE_DIV, COMBINE_COPY, COMBINE_DIV_RAW = 0, 1, 2, 3, 4
+RED_NONE, RED_SUM, RED_MAX = 0, 1, 2
+
+ROWS_MAX_LOOP = 12
+ROWS_MAX_FAC = 16
+ROWS_MAX_EV = 48
+ROWS_MAX_ACC = 192
+ROWS_MARGINALS, ROWS_JOINT, ROWS_MAP, ROWS_MAPGAP = 1, 2, 4, 8
+
+
+class NativeUnavailable(RuntimeError):
+    """The gfx950 HIP library (or a GPU) is not available: there is no CPU fallback."""
+
+
+_I64 = ctypes.c_int64 * PGM_MAX_DIMS
+
+
+class ContractDesc(ctypes.Structure):
+    _fields_ = [
+        ("combine", ctypes.c_int32),
+        ("reduce", ctypes.c_int32),
+        ("n_keep", ctypes.c_int32),
+        ("n_red", ctypes.c_int32),
+        ("keep_card", _I64),
+        ("keep_sa", _I64),
+        ("keep_sb", _I64),
+        ("keep_sc", _I64),
+        ("red_card", _I64),
+        ("red_sa", _I64),
+        ("red_sb", _I64),
+    ]
+
+
+class GatherDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_keep", ctypes.c_int32),
+        ("n_ev", ctypes.c_int32),
+        ("batch_dim", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
+        ("ld", ctypes.c_int64),
+        ("row0", ctypes.c_int64),
+        ("keep_card", _I64),
+        ("keep_sa", _I64),
+        ("keep_sc", _I64),
+        ("ev_col", _I64),
+        ("ev_stride", _I64),
+        ("ev_card", _I64),
+    ]
+
+
+class RowsPlan(ctypes.Structure):
+    _fields_ = [
+        ("n_loop", ctypes.c_int32),
+        ("n_query", ctypes.c_int32),
+        ("n_fac", ctypes.c_int32),
+        ("n_ev", ctypes.c_int32),
+        ("n_values", ctypes.c_int32),
+        ("_pad", ctypes.c_int32 * 3),
+        ("loop_card", ctypes.c_int32 * ROWS_MAX_LOOP),
+        ("fac_base", ctypes.c_int32 * ROWS_MAX_FAC),
+        ("fac_stride", (ctypes.c_int32 * ROWS_MAX_LOOP) * ROWS_MAX_FAC),
+        ("fac_ev_begin", ctypes.c_int32 * ROWS_MAX_FAC),
+        ("fac_ev_end", ctypes.c_int32 * ROWS_MAX_FAC),
+        ("ev_col", ctypes.c_int32 * ROWS_MAX_EV),
+        ("ev_stride", ctypes.c_int32 * ROWS_MAX_EV),
+        ("ev_card", ctypes.c_int32 * ROWS_MAX_EV),
+    ]
+
+
+_P = ctypes.c_void_p
+_SIGS = {
+    "pgm_version": ([], ctypes.c_int),
+    "pgm_last_error": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "pgm_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "pgm_set_device": ([ctypes.c_int], ctypes.c_int),
+    "pgm_alloc": ([ctypes.POINTER(_P), ctypes.c_size_t], ctypes.c_int),
+    "pgm_free": ([_P], ctypes.c_int),
+    "pgm_memcpy_h2d": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_memcpy_d2h": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_memcpy_d2d": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_memset": ([_P, ctypes.c_int, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_stream_sync": ([_P], ctypes.c_int),
+    "pgm_event_create": ([ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_event_destroy": ([_P], ctypes.c_int),
+    "pgm_event_record": ([_P, _P], ctypes.c_int),
+    "pgm_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "pgm_contract_workspace": ([ctypes.POINTER(ContractDesc), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_gather": ([ctypes.POINTER(GatherDesc), _P, _P, _P, _P, _P], ctypes.c_int),
+    "pgm_indicator": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P],
+                      ctypes.c_int),
+    "pgm_argmax": ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P], ctypes.c_int),
+    "pgm_rows_plan_create": ([ctypes.POINTER(RowsPlan), _P, ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_rows_plan_destroy": ([_P], ctypes.c_int),
+    "pgm_rows_plan_run": ([_P, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P,
+                           ctypes.c_int64, _P, _P, _P, _P], ctypes.c_int),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lock = threading.Lock()
+_lib = None
+_device_ok = None
+
+
+def load_library():
+    """Load libpgmhip.so (no GPU needed). Raises NativeUnavailable if it was not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"{LIB_PATH} is missing: build it with `python -m pgmpy_amd.build` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = lib
+        return lib
+
+
+def last_error():
+    lib = load_library()
+    buf = ctypes.create_string_buffer(1024)
+    lib.pgm_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc == PGM_OK:
+        return
+    msg = f"{what}: {last_error()}" if what else last_error()
+    if rc == PGM_EINVAL:
+        raise ValueError(msg)
+    if rc == PGM_EINDEX:
+        raise IndexError(msg)
+    if rc == PGM_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def lib():
+    """The library, for compute: additionally requires a visible GPU (no CPU fallback)."""
+    global _device_ok
+    L = load_library()
+    if _device_ok is None:
+        import torch
+
+        _device_ok = bool(torch.cuda.is_available())
+    if not _device_ok:
+        raise NativeUnavailable("no HIP device visible: the gfx950 kernels need an MI355X (no CPU fallback)")
+    return L
+
+
+def stream_handle(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Raw device pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def i64arr(vals):
+    a = _I64()
+    for i, v in enumerate(vals):
+        a[i] = int(v)
+    return a

@@ -1,0 +1,887 @@
+// pgmhip.hip — gfx950 (MI355X / CDNA4) kernels + C-ABI of the discrete-factor engine.
+//
+// Built for gfx950 only:  hipcc --offload-arch=gfx950 -O3 -fPIC -shared
+// (pgmpy_amd/build.py).  Declarations and the reference call site each entry
+// point replaces: include/pgmhip.h.  Design, data layout and the roofline of
+// every kernel: DESIGN.md.
+//
+// Kernels
+//   k_contract / k_contract_final  generic strided broadcast-combine + axis reduce (HBM-bound)
+//   k_gather                       batched evidence reduce (gather by per-row state codes)
+//   k_indicator                    0/1 evidence indicators (BP findings)
+//   k_argmax                       first-index argmax per row
+//   k_rows                         fused per-row plan: reduce -> sum-product -> normalize ->
+//                                  marginals / joint / MAP, one lane per evidence row
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "pgmhip.h"
+
+#define PGM_ABI_VERSION 1
+
+// ----------------------------------------------------------------------------- errors
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      (void)hipGetLastError();                                                           \
+      return fail(e_ == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "%s: %s", #expr, \
+                  hipGetErrorString(e_));                                                \
+    }                                                                                    \
+  } while (0)
+
+static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ----------------------------------------------------------------------------- fast division
+// n / d for n < 2^31 with one mul-hi and one shift (Granlund-Montgomery round-up method).
+struct FDiv {
+  uint32_t d, m, s;
+};
+
+static FDiv make_fdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FDiv{d, (uint32_t)m, l};
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FDiv &f) {
+  uint32_t t = __umulhi(n, f.m);
+  return (t + n) >> f.s;
+}
+
+__device__ __forceinline__ double max_nan(double a, double b) {
+  // np.max semantics: NaN propagates
+  return (a > b || a != a) ? a : b;
+}
+
+// ----------------------------------------------------------------------------- contract
+#define KMAX 12
+
+struct ContractK {
+  int32_t nk, nr, g_log2, n_split;
+  uint32_t n_out, n_red, red_chunk, _pad;
+  FDiv kdiv[KMAX];
+  int64_t ksa[KMAX], ksb[KMAX], ksc[KMAX];
+  FDiv rdiv[KMAX];
+  int64_t rsa[KMAX], rsb[KMAX];
+};
+
+template <int CMB>
+__device__ __forceinline__ double combine(double a, double b) {
+  if constexpr (CMB == PGM_COMBINE_MUL) return a * b;
+  if constexpr (CMB == PGM_COMBINE_ADD) return a + b;
+  if constexpr (CMB == PGM_COMBINE_DIV) {
+    double r = a / b;
+    return (r != r) ? 0.0 : r;  // DiscreteFactor.py:863 values[isnan] = 0
+  }
+  if constexpr (CMB == PGM_COMBINE_DIV_RAW) return a / b;
+  return a;  // COPY
+}
+
+template <int RED>
+__device__ __forceinline__ double red_init() {
+  if constexpr (RED == PGM_RED_MAX) return -__builtin_inf();
+  return 0.0;
+}
+
+template <int RED>
+__device__ __forceinline__ double red_op(double acc, double v) {
+  if constexpr (RED == PGM_RED_SUM) return acc + v;
+  if constexpr (RED == PGM_RED_MAX) return max_nan(acc, v);
+  return v;
+}
+
+template <int CMB, int RED>
+__global__ __launch_bounds__(256) void k_contract(const ContractK p, const double *__restrict__ A,
+                                                  const double *__restrict__ B, double *__restrict__ C,
+                                                  double *__restrict__ ws) {
+  const uint32_t G = 1u << p.g_log2;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane_g = (uint32_t)tid & (G - 1);
+  const uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) >> p.g_log2;
+  const uint32_t split = blockIdx.y;
+  const uint32_t e0 = split * p.red_chunk;
+  const uint32_t e1 = min(p.n_red, e0 + p.red_chunk);
+  for (uint64_t out = tid >> p.g_log2; out < p.n_out; out += ngroups) {
+    int64_t oa = 0, ob = 0, oc = 0;
+    uint32_t idx = (uint32_t)out;
+    for (int k = p.nk - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      if constexpr (CMB != PGM_COMBINE_COPY) ob += (int64_t)dg * p.ksb[k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    double acc = red_init<RED>();
+    for (uint32_t e = e0 + lane_g; e < e1; e += G) {
+      int64_t ra = oa, rb = ob;
+      uint32_t r = e;
+      for (int k = p.nr - 1; k >= 0; --k) {
+        const uint32_t q = fdiv(r, p.rdiv[k]);
+        const uint32_t dg = r - q * p.rdiv[k].d;
+        ra += (int64_t)dg * p.rsa[k];
+        if constexpr (CMB != PGM_COMBINE_COPY) rb += (int64_t)dg * p.rsb[k];
+        r = q;
+      }
+      double v;
+      if constexpr (CMB == PGM_COMBINE_COPY)
+        v = A[ra];
+      else
+        v = combine<CMB>(A[ra], B[rb]);
+      acc = red_op<RED>(acc, v);
+    }
+    if constexpr (RED != PGM_RED_NONE) {
+      for (uint32_t off = G >> 1; off > 0; off >>= 1) acc = red_op<RED>(acc, __shfl_xor(acc, (int)off, 64));
+    }
+    if (lane_g == 0) {
+      if (p.n_split == 1)
+        C[oc] = acc;
+      else
+        ws[(uint64_t)split * p.n_out + out] = acc;
+    }
+  }
+}
+
+template <int RED>
+__global__ __launch_bounds__(256) void k_contract_final(const ContractK p, const double *__restrict__ ws,
+                                                        double *__restrict__ C) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t out = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; out < p.n_out; out += stride) {
+    int64_t oc = 0;
+    uint32_t idx = (uint32_t)out;
+    for (int k = p.nk - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      oc += (int64_t)(idx - q * p.kdiv[k].d) * p.ksc[k];
+      idx = q;
+    }
+    double acc = ws[out];
+    for (int s = 1; s < p.n_split; ++s) acc = red_op<RED>(acc, ws[(uint64_t)s * p.n_out + out]);
+    C[oc] = acc;
+  }
+}
+
+// host: drop card-1 dims, merge dims that are contiguous for every operand
+struct Dims {
+  int n = 0;
+  int64_t card[PGM_MAX_DIMS];
+  int64_t s[3][PGM_MAX_DIMS];
+};
+
+static void coalesce(Dims &d, int nops) {
+  Dims o;
+  for (int i = 0; i < d.n; ++i) {
+    if (d.card[i] == 1) continue;
+    if (o.n > 0) {
+      bool ok = true;
+      const int j = o.n - 1;
+      for (int t = 0; t < nops; ++t)
+        if (o.s[t][j] != d.card[i] * d.s[t][i]) ok = false;
+      if (ok) {
+        o.card[j] *= d.card[i];
+        for (int t = 0; t < nops; ++t) o.s[t][j] = d.s[t][i];
+        continue;
+      }
+    }
+    o.card[o.n] = d.card[i];
+    for (int t = 0; t < nops; ++t) o.s[t][o.n] = d.s[t][i];
+    ++o.n;
+  }
+  d = o;
+}
+
+static const uint64_t kTargetThreads = 256ull * 2048;  // 256 CUs x 32 waves x 64 lanes
+
+struct ContractLaunch {
+  ContractK k;
+  dim3 grid;
+  uint64_t ws_doubles;
+  bool empty;
+};
+
+static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
+  if (!d) return fail(PGM_EINVAL, "contract: null descriptor");
+  if (d->n_keep < 0 || d->n_keep > PGM_MAX_DIMS || d->n_red < 0 || d->n_red > PGM_MAX_DIMS)
+    return fail(PGM_EINVAL, "contract: n_keep/n_red out of range (%d, %d)", d->n_keep, d->n_red);
+  if (d->combine < 0 || d->combine > 4 || d->reduce < 0 || d->reduce > 2)
+    return fail(PGM_EINVAL, "contract: bad combine/reduce (%d, %d)", d->combine, d->reduce);
+  if (d->reduce == PGM_RED_NONE && d->n_red > 0)
+    return fail(PGM_EINVAL, "contract: reduction dims given with PGM_RED_NONE");
+  Dims kd, rd;
+  kd.n = d->n_keep;
+  uint64_t n_out = 1, n_red = 1;
+  for (int i = 0; i < d->n_keep; ++i) {
+    if (d->keep_card[i] <= 0) return fail(PGM_EINVAL, "contract: keep_card[%d] = %lld", i, (long long)d->keep_card[i]);
+    kd.card[i] = d->keep_card[i];
+    kd.s[0][i] = d->keep_sa[i];
+    kd.s[1][i] = d->keep_sb[i];
+    kd.s[2][i] = d->keep_sc[i];
+    n_out *= (uint64_t)d->keep_card[i];
+  }
+  rd.n = d->n_red;
+  for (int i = 0; i < d->n_red; ++i) {
+    if (d->red_card[i] <= 0) return fail(PGM_EINVAL, "contract: red_card[%d] = %lld", i, (long long)d->red_card[i]);
+    rd.card[i] = d->red_card[i];
+    rd.s[0][i] = d->red_sa[i];
+    rd.s[1][i] = d->red_sb[i];
+    n_red *= (uint64_t)d->red_card[i];
+  }
+  if (n_out >= (1ull << 31) || n_red >= (1ull << 31))
+    return fail(PGM_EINVAL, "contract: index space too large (%llu x %llu; limit 2^31 each)",
+                (unsigned long long)n_out, (unsigned long long)n_red);
+  coalesce(kd, 3);
+  coalesce(rd, 2);
+  if (kd.n > KMAX || rd.n > KMAX)
+    return fail(PGM_EINVAL, "contract: %d keep / %d reduce dims after coalescing (limit %d)", kd.n, rd.n, KMAX);
+  ContractK &k = L.k;
+  memset(&k, 0, sizeof k);
+  k.nk = kd.n;
+  k.nr = rd.n;
+  for (int i = 0; i < kd.n; ++i) {
+    k.kdiv[i] = make_fdiv((uint32_t)kd.card[i]);
+    k.ksa[i] = kd.s[0][i];
+    k.ksb[i] = kd.s[1][i];
+    k.ksc[i] = kd.s[2][i];
+  }
+  for (int i = 0; i < rd.n; ++i) {
+    k.rdiv[i] = make_fdiv((uint32_t)rd.card[i]);
+    k.rsa[i] = rd.s[0][i];
+    k.rsb[i] = rd.s[1][i];
+  }
+  k.n_out = (uint32_t)n_out;
+  k.n_red = (uint32_t)n_red;
+  L.empty = (n_out == 0);
+  // work decomposition: G lanes cooperate on one output, S splits of the reduction over blocks
+  int g_log2 = 0;
+  uint32_t n_split = 1;
+  if (d->reduce != PGM_RED_NONE && n_red > 1) {
+    const bool red_contig = rd.n > 0 && rd.s[0][rd.n - 1] == 1;
+    const bool keep_contig = kd.n > 0 && kd.s[0][kd.n - 1] == 1;
+    if (!(keep_contig && !red_contig)) {
+      // lanes stride the reduction (coalesced when the reduced axis is innermost)
+      while (g_log2 < 6 && (n_out << g_log2) < kTargetThreads && (1ull << (g_log2 + 1)) <= n_red) ++g_log2;
+    }
+    const uint64_t par = n_out << g_log2;
+    if (par < kTargetThreads / 4) {
+      uint64_t want = (kTargetThreads / 4 + par - 1) / par;
+      uint64_t max_split = std::max<uint64_t>(1, n_red / ((1ull << g_log2) * 16));
+      n_split = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(want, max_split), 1024);
+      if (n_split < 1) n_split = 1;
+    }
+  }
+  k.g_log2 = g_log2;
+  k.n_split = (int32_t)n_split;
+  k.red_chunk = (uint32_t)((n_red + n_split - 1) / n_split);
+  const uint64_t threads = n_out << g_log2;
+  uint64_t blocks = (threads + 255) / 256;
+  blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 65535);
+  L.grid = dim3((unsigned)blocks, n_split, 1);
+  L.ws_doubles = n_split > 1 ? (uint64_t)n_split * n_out : 0;
+  return PGM_OK;
+}
+
+template <int CMB, int RED>
+static void launch_contract_t(const ContractLaunch &L, const double *A, const double *B, double *C, double *ws,
+                              hipStream_t s) {
+  hipLaunchKernelGGL((k_contract<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
+  if (L.k.n_split > 1) {
+    uint64_t blocks = std::min<uint64_t>((L.k.n_out + 255) / 256, 65535);
+    hipLaunchKernelGGL((k_contract_final<RED>), dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s,
+                       L.k, (const double *)ws, C);
+  }
+}
+
+template <int CMB>
+static void launch_contract_c(int red, const ContractLaunch &L, const double *A, const double *B, double *C,
+                              double *ws, hipStream_t s) {
+  switch (red) {
+    case PGM_RED_NONE: launch_contract_t<CMB, PGM_RED_NONE>(L, A, B, C, ws, s); break;
+    case PGM_RED_SUM: launch_contract_t<CMB, PGM_RED_SUM>(L, A, B, C, ws, s); break;
+    default: launch_contract_t<CMB, PGM_RED_MAX>(L, A, B, C, ws, s); break;
+  }
+}
+
+// ----------------------------------------------------------------------------- gather
+struct GatherK {
+  int32_t nk, n_ev, batch_dim, _pad;
+  uint32_t n_out, _pad2;
+  int64_t ld, row0;
+  FDiv kdiv[KMAX];
+  int64_t ksa[KMAX], ksc[KMAX];
+  int64_t ev_col[PGM_MAX_DIMS], ev_stride[PGM_MAX_DIMS];
+  int32_t ev_card[PGM_MAX_DIMS];
+};
+
+__global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *__restrict__ A,
+                                                const uint8_t *__restrict__ codes, double *__restrict__ C,
+                                                int32_t *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t out = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; out < p.n_out; out += stride) {
+    int64_t oa = 0, oc = 0, row = 0;
+    uint32_t idx = (uint32_t)out;
+    for (int k = p.nk - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      oc += (int64_t)dg * p.ksc[k];
+      if (k == p.batch_dim) row = dg;
+      idx = q;
+    }
+    for (int j = 0; j < p.n_ev; ++j) {
+      uint32_t c = codes[p.ev_col[j] * p.ld + p.row0 + row];
+      if (c >= (uint32_t)p.ev_card[j]) {
+        if (err) atomicOr(err, 1);
+        c = 0;
+      }
+      oa += (int64_t)c * p.ev_stride[j];
+    }
+    C[oc] = A[oa];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_indicator(const uint8_t *__restrict__ codes, int64_t n_rows, int64_t card,
+                                                   double *__restrict__ out, int64_t s_state, int64_t s_row,
+                                                   int32_t *__restrict__ err) {
+  const int64_t n = n_rows * card;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t r = i % n_rows, k = i / n_rows;
+    const uint32_t c = codes[r];
+    double v;
+    if (c == PGM_EV_MISSING)
+      v = 1.0;
+    else {
+      if (c >= (uint64_t)card && err) atomicOr(err, 1);
+      v = (c == (uint64_t)k) ? 1.0 : 0.0;
+    }
+    out[k * s_state + r * s_row] = v;
+  }
+}
+
+// ----------------------------------------------------------------------------- argmax
+__device__ __forceinline__ bool am_better(double v, uint32_t i, double bv, uint32_t bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn) return !bn || i < bi;  // np.argmax: first NaN wins
+  if (bn) return false;
+  return v > bv || (v == bv && i < bi);
+}
+
+__global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, uint64_t n_rows, uint32_t row_len,
+                                                int64_t s_row, int64_t s_elem, int g_log2,
+                                                int64_t *__restrict__ out) {
+  const uint32_t G = 1u << g_log2;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane_g = (uint32_t)tid & (G - 1);
+  const uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) >> g_log2;
+  for (uint64_t r = tid >> g_log2; r < n_rows; r += ngroups) {
+    double bv = -__builtin_inf();
+    uint32_t bi = 0xffffffffu;
+    for (uint32_t i = lane_g; i < row_len; i += G) {
+      const double v = X[(int64_t)r * s_row + (int64_t)i * s_elem];
+      if (am_better(v, i, bv, bi)) {
+        bv = v;
+        bi = i;
+      }
+    }
+    for (uint32_t off = G >> 1; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(bv, (int)off, 64);
+      const uint32_t oi = (uint32_t)__shfl_xor((int)bi, (int)off, 64);
+      if (am_better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane_g == 0) out[r] = (bi == 0xffffffffu) ? 0 : (int64_t)bi;
+  }
+}
+
+// ----------------------------------------------------------------------------- fused row plan
+struct RowsK {
+  int32_t n_loop, n_query, n_fac, n_ev;
+  int32_t n_values, n_acc, vals_lds, acc_lds;
+  uint32_t P, H;  // query space, hidden space sizes
+  int32_t loop_card[PGM_ROWS_MAX_LOOP];
+  int32_t fac_base[PGM_ROWS_MAX_FAC];
+  int32_t inc[PGM_ROWS_MAX_LOOP][PGM_ROWS_MAX_FAC];  // offset increment when loop dim k advances
+  int32_t fac_ev_begin[PGM_ROWS_MAX_FAC], fac_ev_end[PGM_ROWS_MAX_FAC];
+  int32_t ev_col[PGM_ROWS_MAX_EV], ev_stride[PGM_ROWS_MAX_EV], ev_card[PGM_ROWS_MAX_EV];
+  int32_t acc_off[PGM_ROWS_MAX_LOOP];
+  int32_t hspan[PGM_ROWS_MAX_FAC];  // sum over hidden dims of (card-1)*stride: undone on a full hidden wrap
+};
+
+struct RowsHandle {
+  RowsK k;
+  double *d_values;
+  int device;
+};
+
+template <int MAXF>
+__global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__restrict__ gvals,
+                                              const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0,
+                                              int64_t n_rows, int32_t mode, double *__restrict__ marg,
+                                              double *__restrict__ joint, int64_t ld_out,
+                                              int32_t *__restrict__ map, double *__restrict__ gap,
+                                              int32_t *__restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double *svals = lds;                                   // [n_values] when vals_lds
+  double *sacc = lds + (p.vals_lds ? ((p.n_values + 1) & ~1) : 0);  // [n_acc][blockDim] when acc_lds
+  if (p.vals_lds) {
+    for (int i = threadIdx.x; i < p.n_values; i += blockDim.x) svals[i] = gvals[i];
+    __syncthreads();
+  }
+  const double *V = p.vals_lds ? svals : gvals;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int nb = blockDim.x;
+  const int lane = threadIdx.x;
+
+  // evidence part of every factor's offset (per row)
+  int32_t base[MAXF];
+#pragma unroll
+  for (int f = 0; f < MAXF; ++f) {
+    base[f] = 0;
+    if (f < p.n_fac) {
+      int32_t b = p.fac_base[f];
+      for (int j = p.fac_ev_begin[f]; j < p.fac_ev_end[f]; ++j) {
+        uint32_t c = codes[(int64_t)p.ev_col[j] * ld_codes + row0 + r];
+        if (c >= (uint32_t)p.ev_card[j]) {
+          if (err) atomicOr(err, 1);
+          c = 0;
+        }
+        b += (int32_t)c * p.ev_stride[j];
+      }
+      base[f] = b;
+    }
+  }
+  const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
+  const bool do_joint = (mode & PGM_ROWS_JOINT) != 0;
+  const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
+  double *acc_row = p.acc_lds ? (sacc + lane) : (marg + r);
+  const int64_t acc_stride = p.acc_lds ? nb : ld_out;
+  if (do_marg)
+    for (int a = 0; a < p.n_acc; ++a) acc_row[a * acc_stride] = 0.0;
+
+  // uniform odometer state (identical across lanes -> scalar registers); all array indices are
+  // compile-time constants after unrolling so nothing spills to scratch
+  int32_t off[MAXF];
+#pragma unroll
+  for (int f = 0; f < MAXF; ++f) off[f] = 0;
+  int32_t dig[PGM_ROWS_MAX_LOOP];
+#pragma unroll
+  for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k) dig[k] = 0;
+
+  double z = 0.0, best = -1.0, second = -1.0;
+  uint32_t best_i = 0;
+  const int nq = p.n_query, nl = p.n_loop;
+  for (uint32_t qi = 0; qi < p.P; ++qi) {
+    double v = 0.0;
+    for (uint32_t hi = 0; hi < p.H; ++hi) {
+      double prod = 1.0;
+#pragma unroll
+      for (int f = 0; f < MAXF; ++f)
+        if (f < p.n_fac) prod *= V[base[f] + off[f]];
+      v += prod;
+      // advance the hidden odometer (dims nq .. nl-1, innermost last)
+      bool carry = true;
+#pragma unroll
+      for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
+        if (carry && k >= nq && k < nl) {
+          if (++dig[k] < p.loop_card[k]) {
+#pragma unroll
+            for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
+            carry = false;
+          } else {
+            dig[k] = 0;
+          }
+        }
+      }
+      if (carry) {  // full wrap of the hidden space: digits are back to 0, drop their offsets
+#pragma unroll
+        for (int f = 0; f < MAXF; ++f) off[f] -= p.hspan[f];
+      }
+    }
+    z += v;
+    if (do_marg) {
+#pragma unroll
+      for (int i = 0; i < PGM_ROWS_MAX_LOOP; ++i)
+        if (i < nq) acc_row[(p.acc_off[i] + dig[i]) * acc_stride] += v;
+    }
+    if (do_joint) joint[(int64_t)qi * ld_out + r] = v;
+    if (do_map) {
+      if (v > best) {
+        second = best;
+        best = v;
+        best_i = qi;
+      } else if (v > second) {
+        second = v;
+      }
+    }
+    // advance the query odometer (dims 0 .. nq-1)
+    bool carry = true;
+#pragma unroll
+    for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
+      if (carry && k < nq) {
+        if (++dig[k] < p.loop_card[k]) {
+#pragma unroll
+          for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
+          carry = false;
+        } else {
+          dig[k] = 0;
+        }
+      }
+    }
+  }
+  if (do_marg) {
+    for (int a = 0; a < p.n_acc; ++a) {
+      const double m = acc_row[a * acc_stride] / z;  // 0/0 = NaN on impossible evidence, as normalize
+      marg[(int64_t)a * ld_out + r] = m;
+    }
+  }
+  if (do_joint)
+    for (uint32_t qi = 0; qi < p.P; ++qi) joint[(int64_t)qi * ld_out + r] /= z;
+  if (do_map) {
+    if (map) map[r] = (int32_t)best_i;
+    if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0;
+  }
+}
+
+// ============================================================================= C-ABI
+extern "C" {
+
+int pgm_version(void) { return PGM_ABI_VERSION; }
+
+int pgm_last_error(char *buf, size_t len) {
+  if (!buf || len == 0) return PGM_EINVAL;
+  size_t n = std::min(len - 1, g_err.size());
+  memcpy(buf, g_err.data(), n);
+  buf[n] = 0;
+  return PGM_OK;
+}
+
+int pgm_device_count(int *n) {
+  if (!n) return fail(PGM_EINVAL, "null pointer");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *n = 0;
+    return fail(PGM_EDEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *n = c;
+  return PGM_OK;
+}
+
+int pgm_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return PGM_OK;
+}
+
+int pgm_alloc(void **ptr, size_t bytes) {
+  if (!ptr) return fail(PGM_EINVAL, "null pointer");
+  *ptr = nullptr;
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMalloc(ptr, bytes));
+  return PGM_OK;
+}
+
+int pgm_free(void *ptr) {
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return PGM_OK;
+}
+
+int pgm_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
+  return PGM_OK;
+}
+
+int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)));
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  return PGM_OK;
+}
+
+int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+  return PGM_OK;
+}
+
+int pgm_memset(void *dst, int value, size_t bytes, void *stream) {
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMemsetAsync(dst, value, bytes, S(stream)));
+  return PGM_OK;
+}
+
+int pgm_stream_sync(void *stream) {
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  return PGM_OK;
+}
+
+int pgm_event_create(void **ev) {
+  if (!ev) return fail(PGM_EINVAL, "null pointer");
+  hipEvent_t e;
+  HIP_TRY(hipEventCreate(&e));
+  *ev = (void *)e;
+  return PGM_OK;
+}
+
+int pgm_event_destroy(void *ev) {
+  if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
+  return PGM_OK;
+}
+
+int pgm_event_record(void *ev, void *stream) {
+  HIP_TRY(hipEventRecord((hipEvent_t)ev, S(stream)));
+  return PGM_OK;
+}
+
+int pgm_event_elapsed_ms(void *start, void *stop, float *ms) {
+  HIP_TRY(hipEventSynchronize((hipEvent_t)stop));
+  HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  return PGM_OK;
+}
+
+int pgm_contract_workspace(const pgm_contract_desc *d, size_t *bytes) {
+  if (!bytes) return fail(PGM_EINVAL, "null pointer");
+  ContractLaunch L;
+  int rc = plan_contract(d, L);
+  if (rc) return rc;
+  *bytes = L.ws_doubles * sizeof(double);
+  return PGM_OK;
+}
+
+int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, double *C, void *workspace,
+                 size_t workspace_bytes, void *stream) {
+  ContractLaunch L;
+  int rc = plan_contract(d, L);
+  if (rc) return rc;
+  if (L.empty) return PGM_OK;
+  if (!A || !C) return fail(PGM_EINVAL, "contract: null A or C");
+  if (d->combine != PGM_COMBINE_COPY && !B) return fail(PGM_EINVAL, "contract: null B for a binary combine");
+  if (L.ws_doubles * sizeof(double) > workspace_bytes || (L.ws_doubles && !workspace))
+    return fail(PGM_EINVAL, "contract: workspace of %zu bytes needed, %zu given",
+                (size_t)(L.ws_doubles * sizeof(double)), workspace_bytes);
+  double *ws = (double *)workspace;
+  hipStream_t s = S(stream);
+  switch (d->combine) {
+    case PGM_COMBINE_MUL: launch_contract_c<PGM_COMBINE_MUL>(d->reduce, L, A, B, C, ws, s); break;
+    case PGM_COMBINE_ADD: launch_contract_c<PGM_COMBINE_ADD>(d->reduce, L, A, B, C, ws, s); break;
+    case PGM_COMBINE_DIV: launch_contract_c<PGM_COMBINE_DIV>(d->reduce, L, A, B, C, ws, s); break;
+    case PGM_COMBINE_DIV_RAW: launch_contract_c<PGM_COMBINE_DIV_RAW>(d->reduce, L, A, B, C, ws, s); break;
+    default: launch_contract_c<PGM_COMBINE_COPY>(d->reduce, L, A, B, C, ws, s); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C, int32_t *err_flag,
+               void *stream) {
+  if (!d || !A || !C) return fail(PGM_EINVAL, "gather: null argument");
+  if (d->n_keep < 0 || d->n_keep > KMAX || d->n_ev < 0 || d->n_ev > PGM_MAX_DIMS)
+    return fail(PGM_EINVAL, "gather: n_keep %d (limit %d) / n_ev %d", d->n_keep, KMAX, d->n_ev);
+  if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "gather: null codes");
+  if (d->batch_dim >= d->n_keep) return fail(PGM_EINVAL, "gather: batch_dim out of range");
+  GatherK k;
+  memset(&k, 0, sizeof k);
+  k.nk = d->n_keep;
+  k.n_ev = d->n_ev;
+  k.batch_dim = d->batch_dim;
+  k.ld = d->ld;
+  k.row0 = d->row0;
+  uint64_t n_out = 1;
+  for (int i = 0; i < d->n_keep; ++i) {
+    if (d->keep_card[i] <= 0) return fail(PGM_EINVAL, "gather: keep_card[%d] <= 0", i);
+    n_out *= (uint64_t)d->keep_card[i];
+    k.kdiv[i] = make_fdiv((uint32_t)d->keep_card[i]);
+    k.ksa[i] = d->keep_sa[i];
+    k.ksc[i] = d->keep_sc[i];
+  }
+  if (n_out >= (1ull << 31)) return fail(PGM_EINVAL, "gather: output too large");
+  for (int j = 0; j < d->n_ev; ++j) {
+    k.ev_col[j] = d->ev_col[j];
+    k.ev_stride[j] = d->ev_stride[j];
+    k.ev_card[j] = (int32_t)d->ev_card[j];
+  }
+  k.n_out = (uint32_t)n_out;
+  if (n_out == 0) return PGM_OK;
+  uint64_t blocks = std::min<uint64_t>((n_out + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(256), 0, S(stream), k, A, codes, C, err_flag);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *out, int64_t s_state, int64_t s_row,
+                  int32_t *err_flag, void *stream) {
+  if (!codes || !out) return fail(PGM_EINVAL, "indicator: null argument");
+  if (n_rows <= 0 || card <= 0) return PGM_OK;
+  uint64_t blocks = std::min<uint64_t>((uint64_t)(n_rows * card + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_indicator, dim3((unsigned)blocks), dim3(256), 0, S(stream), codes, n_rows, card, out, s_state,
+                     s_row, err_flag);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem, int64_t *out_idx,
+               void *stream) {
+  if (!X || !out_idx) return fail(PGM_EINVAL, "argmax: null argument");
+  if (n_rows <= 0) return PGM_OK;
+  if (row_len <= 0) return fail(PGM_EINVAL, "argmax: empty rows (np.argmax of an empty sequence)");
+  if (row_len >= (1ll << 31)) return fail(PGM_EINVAL, "argmax: row too long");
+  int g = 0;
+  while (g < 6 && ((uint64_t)n_rows << g) < kTargetThreads && (1ll << (g + 1)) <= row_len) ++g;
+  uint64_t threads = (uint64_t)n_rows << g;
+  uint64_t blocks = std::min<uint64_t>((threads + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_argmax, dim3((unsigned)blocks), dim3(256), 0, S(stream), X, (uint64_t)n_rows,
+                     (uint32_t)row_len, s_row, s_elem, g, out_idx);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, void **handle) {
+  if (!pl || !handle || (!host_values && pl->n_values > 0)) return fail(PGM_EINVAL, "rows_plan_create: null argument");
+  *handle = nullptr;
+  if (pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP || pl->n_query < 0 || pl->n_query > pl->n_loop ||
+      pl->n_fac < 0 || pl->n_fac > PGM_ROWS_MAX_FAC || pl->n_ev < 0 || pl->n_ev > PGM_ROWS_MAX_EV ||
+      pl->n_values < 0)
+    return fail(PGM_EINVAL, "rows_plan_create: plan out of range (loop %d query %d fac %d ev %d)", pl->n_loop,
+                pl->n_query, pl->n_fac, pl->n_ev);
+  RowsK k;
+  memset(&k, 0, sizeof k);
+  k.n_loop = pl->n_loop;
+  k.n_query = pl->n_query;
+  k.n_fac = pl->n_fac;
+  k.n_ev = pl->n_ev;
+  k.n_values = pl->n_values;
+  uint64_t P = 1, H = 1;
+  int n_acc = 0;
+  for (int i = 0; i < pl->n_loop; ++i) {
+    if (pl->loop_card[i] <= 0) return fail(PGM_EINVAL, "rows_plan_create: loop_card[%d] <= 0", i);
+    k.loop_card[i] = pl->loop_card[i];
+    if (i < pl->n_query) {
+      P *= pl->loop_card[i];
+      k.acc_off[i] = n_acc;
+      n_acc += pl->loop_card[i];
+    } else {
+      H *= pl->loop_card[i];
+    }
+  }
+  if (P * H >= (1ull << 31)) return fail(PGM_EINVAL, "rows_plan_create: loop space too large");
+  if (n_acc > PGM_ROWS_MAX_ACC) return fail(PGM_EINVAL, "rows_plan_create: %d marginal entries (limit %d)", n_acc,
+                                            PGM_ROWS_MAX_ACC);
+  k.P = (uint32_t)P;
+  k.H = (uint32_t)H;
+  k.n_acc = n_acc;
+  for (int f = 0; f < pl->n_fac; ++f) {
+    k.fac_base[f] = pl->fac_base[f];
+    k.fac_ev_begin[f] = pl->fac_ev_begin[f];
+    k.fac_ev_end[f] = pl->fac_ev_end[f];
+    if (pl->fac_ev_begin[f] < 0 || pl->fac_ev_end[f] > pl->n_ev || pl->fac_ev_begin[f] > pl->fac_ev_end[f])
+      return fail(PGM_EINVAL, "rows_plan_create: factor %d evidence range", f);
+    // odometer increments: advancing dim k resets every deeper dim of the SAME odometer
+    // (query dims [0,nq) and hidden dims [nq,nl) are two separate odometers)
+    for (int kk = 0; kk < pl->n_loop; ++kk) {
+      const int end = kk < pl->n_query ? pl->n_query : pl->n_loop;
+      int64_t inc = pl->fac_stride[f][kk];
+      for (int k2 = kk + 1; k2 < end; ++k2) inc -= (int64_t)(pl->loop_card[k2] - 1) * pl->fac_stride[f][k2];
+      k.inc[kk][f] = (int32_t)inc;
+    }
+    int64_t hs = 0;
+    for (int kk = pl->n_query; kk < pl->n_loop; ++kk) hs += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
+    k.hspan[f] = (int32_t)hs;
+    // bounds: max offset must stay inside values
+    int64_t mx = pl->fac_base[f];
+    for (int kk = 0; kk < pl->n_loop; ++kk) mx += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
+    for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) mx += (int64_t)(pl->ev_card[j] - 1) * pl->ev_stride[j];
+    if (mx >= pl->n_values || pl->fac_base[f] < 0) return fail(PGM_EINVAL, "rows_plan_create: factor %d reads past values", f);
+  }
+  for (int j = 0; j < pl->n_ev; ++j) {
+    k.ev_col[j] = pl->ev_col[j];
+    k.ev_stride[j] = pl->ev_stride[j];
+    k.ev_card[j] = pl->ev_card[j];
+  }
+  RowsHandle *h = new (std::nothrow) RowsHandle;
+  if (!h) return fail(PGM_ENOMEM, "rows_plan_create: host allocation");
+  h->k = k;
+  h->d_values = nullptr;
+  hipGetDevice(&h->device);
+  if (pl->n_values > 0) {
+    hipError_t e = hipMalloc((void **)&h->d_values, sizeof(double) * pl->n_values);
+    if (e == hipSuccess) e = hipMemcpy(h->d_values, host_values, sizeof(double) * pl->n_values, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      if (h->d_values) hipFree(h->d_values);
+      delete h;
+      return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_plan_create: %s", hipGetErrorString(e));
+    }
+  }
+  *handle = h;
+  return PGM_OK;
+}
+
+int pgm_rows_plan_destroy(void *handle) {
+  RowsHandle *h = (RowsHandle *)handle;
+  if (!h) return PGM_OK;
+  if (h->d_values) hipFree(h->d_values);
+  delete h;
+  return PGM_OK;
+}
+
+int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
+                      double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap, int32_t *err_flag,
+                      void *stream) {
+  RowsHandle *h = (RowsHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "rows_plan_run: null handle");
+  if (n_rows <= 0) return PGM_OK;
+  if (h->k.n_ev > 0 && !codes) return fail(PGM_EINVAL, "rows_plan_run: null codes");
+  if ((mode & PGM_ROWS_MARGINALS) && !marg) return fail(PGM_EINVAL, "rows_plan_run: marginals requested, marg is null");
+  if ((mode & PGM_ROWS_JOINT) && !joint) return fail(PGM_EINVAL, "rows_plan_run: joint requested, joint is null");
+  if ((mode & PGM_ROWS_MAP) && !map) return fail(PGM_EINVAL, "rows_plan_run: MAP requested, map is null");
+  if ((mode & PGM_ROWS_MAPGAP) && !gap) return fail(PGM_EINVAL, "rows_plan_run: MAP gap requested, gap is null");
+  if ((mode & (PGM_ROWS_MARGINALS | PGM_ROWS_JOINT)) && ld_out < n_rows)
+    return fail(PGM_EINVAL, "rows_plan_run: ld_out %lld < n_rows %lld", (long long)ld_out, (long long)n_rows);
+  RowsK k = h->k;
+  // LDS budget: CPT values (if they fit) + per-lane marginal accumulators
+  const size_t kLds = 64 * 1024;
+  size_t vals_bytes = (size_t)((k.n_values + 1) & ~1) * sizeof(double);
+  k.vals_lds = vals_bytes <= 48 * 1024 ? 1 : 0;
+  if (!k.vals_lds) vals_bytes = 0;
+  int block = 256;
+  k.acc_lds = 0;
+  if (mode & PGM_ROWS_MARGINALS) {
+    while (block > 64 && vals_bytes + (size_t)k.n_acc * block * sizeof(double) > kLds) block >>= 1;
+    k.acc_lds = vals_bytes + (size_t)k.n_acc * block * sizeof(double) <= kLds ? 1 : 0;
+    if (!k.acc_lds) block = 256;
+  }
+  size_t lds = vals_bytes + (k.acc_lds ? (size_t)k.n_acc * block * sizeof(double) : 0);
+  uint64_t blocks = ((uint64_t)n_rows + block - 1) / block;
+  if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
+  hipLaunchKernelGGL((k_rows<PGM_ROWS_MAX_FAC>), dim3((unsigned)blocks), dim3(block), lds, S(stream), k,
+                     (const double *)h->d_values, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap,
+                     err_flag);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,235 @@
+"""Label-based device operations over fp64 torch tensors, dispatched to libpgmhip.
+
+Every factor operation of the hot path is one ``contract`` call: operands are
+device tensors whose axes carry variable labels; the kernel walks the output
+labels (keep loop) and the labels that appear only in the inputs (reduce loop)
+using each operand's element strides, so broadcasting (absent label -> stride 0),
+transposition and batching over evidence rows (a ``ROW`` label) need no copies.
+
+This module replaces the reference's numpy calls (pgmpy/utils/compat_fns.py:
+einsum L63-67, max L53-60, argmax L70-74) with the C-ABI of include/pgmhip.h.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+ROW = "__row__"  # label of the evidence-row (batch) axis
+
+_REDUCE = {None: N.RED_NONE, "sum": N.RED_SUM, "max": N.RED_MAX}
+_COMBINE = {"mul": N.COMBINE_MUL, "add": N.COMBINE_ADD, "div": N.COMBINE_DIV, "copy": N.COMBINE_COPY,
+            "div_raw": N.COMBINE_DIV_RAW}
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def device():
+    torch = _torch()
+    N.lib()  # raises NativeUnavailable without a GPU / library
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def to_device(arr):
+    """Host numpy (any dtype castable to fp64) -> contiguous fp64 device tensor.
+
+    The H2D copy goes through the library (pgm_memcpy_h2d) on the current stream."""
+    torch = _torch()
+    L = N.lib()
+    a = np.ascontiguousarray(arr, dtype=np.float64)
+    t = torch.empty(a.shape, dtype=torch.float64, device=device())
+    if a.size:
+        N.check(L.pgm_memcpy_h2d(N.ptr(t), a.ctypes.data_as(ctypes.c_void_p), a.nbytes, N.stream_handle()),
+                "memcpy_h2d")
+    return t
+
+
+def to_host(t):
+    """Device tensor -> numpy (C-order copy of its logical contents)."""
+    L = N.lib()
+    if not t.is_contiguous():
+        t = copy(t)
+    out = np.empty(tuple(t.shape), dtype=np.float64)
+    if out.size:
+        N.check(L.pgm_memcpy_d2h(out.ctypes.data_as(ctypes.c_void_p), N.ptr(t), out.nbytes, N.stream_handle()),
+                "memcpy_d2h")
+    return out
+
+
+def empty(shape):
+    torch = _torch()
+    return torch.empty(tuple(int(s) for s in shape), dtype=torch.float64, device=device())
+
+
+def scalar(x):
+    return to_device(np.array(x, dtype=np.float64))
+
+
+def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
+    """C[out_labels] = REDUCE_{labels not in out} COMBINE(A[la], B[lb]).
+
+    A/B: device fp64 tensors (any strides), la/lb: one label per axis (B may be
+    None for combine="copy").  Labels absent from an operand broadcast.  Returns
+    the output tensor (C-order over out_labels unless `out` is given)."""
+    L = N.lib()
+    la = list(la)
+    lb = list(lb) if B is not None else []
+    out_labels = list(out_labels)
+    if len(la) != A.dim() or (B is not None and len(lb) != B.dim()):
+        raise ValueError("label count does not match tensor rank")
+    card = {}
+    for t, ls in ((A, la), (B, lb)):
+        if t is None:
+            continue
+        for d, l in enumerate(ls):
+            c = int(t.shape[d])
+            if card.setdefault(l, c) != c:
+                raise ValueError(f"cardinality mismatch for {l!r}: {card[l]} vs {c}")
+    for l in out_labels:
+        if l not in card:
+            raise ValueError(f"output label {l!r} not in any operand")
+    red = [l for l in dict.fromkeys(la + lb) if l not in out_labels]
+    if red and reduce is None:
+        raise ValueError(f"labels {red} would be reduced but reduce=None")
+    if len(out_labels) > N.PGM_MAX_DIMS or len(red) > N.PGM_MAX_DIMS:
+        raise ValueError(f"too many dimensions ({len(out_labels)} kept, {len(red)} reduced; limit {N.PGM_MAX_DIMS})")
+    if out is None:
+        out = empty([card[l] for l in out_labels])
+    elif tuple(out.shape) != tuple(card[l] for l in out_labels):
+        raise ValueError("out has the wrong shape")
+
+    def st(t, ls, l):
+        if t is None or l not in ls:
+            return 0
+        return int(t.stride(ls.index(l)))
+
+    d = N.ContractDesc()
+    d.combine = _COMBINE[combine]
+    d.reduce = _REDUCE[reduce] if red else N.RED_NONE
+    d.n_keep = len(out_labels)
+    d.n_red = len(red)
+    for i, l in enumerate(out_labels):
+        d.keep_card[i] = card[l]
+        d.keep_sa[i] = st(A, la, l)
+        d.keep_sb[i] = st(B, lb, l)
+        d.keep_sc[i] = int(out.stride(i))
+    for i, l in enumerate(red):
+        d.red_card[i] = card[l]
+        d.red_sa[i] = st(A, la, l)
+        d.red_sb[i] = st(B, lb, l)
+    ws_bytes = ctypes.c_size_t(0)
+    N.check(L.pgm_contract_workspace(ctypes.byref(d), ctypes.byref(ws_bytes)), "contract")
+    ws = None
+    if ws_bytes.value:
+        ws = empty([ws_bytes.value // 8])
+    N.check(L.pgm_contract(ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), ws_bytes.value,
+                           N.stream_handle()), "contract")
+    # ws may be freed here: torch's caching allocator is stream-ordered, so its memory is only
+    # handed to work queued after these kernels on the same stream.
+    return out
+
+
+def copy(A, la=None, out_labels=None):
+    la = list(range(A.dim())) if la is None else la
+    out_labels = la if out_labels is None else out_labels
+    return contract(A, la, None, None, out_labels, combine="copy")
+
+
+def total(A):
+    """Sum of all entries -> 0-d device tensor."""
+    return contract(A, list(range(A.dim())), None, None, [], reduce="sum", combine="copy")
+
+
+def normalize_(A):
+    """A /= A.sum() in place (0/0 -> NaN as DiscreteFactor.normalize, DiscreteFactor.py:530)."""
+    s = total(A)
+    labels = list(range(A.dim()))
+    contract(A, labels, s, [], labels, combine="div_raw", out=A)
+    return A
+
+
+def normalize_rows_(A, la, row_label=ROW):
+    """Per-row normalize of a batched tensor: every label except row_label is summed."""
+    s = contract(A, la, None, None, [row_label], reduce="sum", combine="copy")
+    contract(A, la, s, [row_label], la, combine="div_raw", out=A)
+    return A
+
+
+def argmax_rows(A, la, row_label=None):
+    """First-flat-index argmax over all labels but row_label (C-order of la minus row)."""
+    torch = _torch()
+    L = N.lib()
+    if row_label is None:
+        X = A if A.is_contiguous() else copy(A)
+        out = torch.empty(1, dtype=torch.int64, device=X.device)
+        n = X.numel()
+        N.check(L.pgm_argmax(N.ptr(X), 1, n, n, 1, N.ptr(out), N.stream_handle()), "argmax")
+        return out
+    other = [l for l in la if l != row_label]
+    X = contract(A, la, None, None, [row_label] + other, combine="copy")
+    n_rows = X.shape[0]
+    row_len = int(np.prod(X.shape[1:])) if X.dim() > 1 else 1
+    out = torch.empty(n_rows, dtype=torch.int64, device=X.device)
+    N.check(L.pgm_argmax(N.ptr(X), n_rows, row_len, row_len, 1, N.ptr(out), N.stream_handle()), "argmax")
+    return out
+
+
+def gather(A, la, evidence, out_labels, codes=None, ld=0, row0=0, n_rows=None, err=None):
+    """Evidence reduce.
+
+    evidence: {label: state} (static) or {label: column} with `codes` (uint8
+    device tensor [n_cols, ld]) giving per-row states; per-row gathers need
+    ROW in out_labels.  Labels of A that are in `evidence` are dropped."""
+    L = N.lib()
+    torch = _torch()
+    la = list(la)
+    static = {l: s for l, s in evidence.items() if codes is None or not isinstance(s, tuple)}
+    dynamic = {l: s[1] for l, s in evidence.items() if codes is not None and isinstance(s, tuple)}
+    card = {l: int(A.shape[i]) for i, l in enumerate(la)}
+    base = 0
+    for l, s in static.items():
+        if not (0 <= int(s) < card[l]):
+            raise IndexError(f"index {s} is out of bounds for axis with size {card[l]}")
+        base += int(s) * int(A.stride(la.index(l)))
+    keep_shape = []
+    for l in out_labels:
+        if l == ROW:
+            keep_shape.append(int(n_rows))
+        else:
+            keep_shape.append(card[l])
+    out = empty(keep_shape)
+    d = N.GatherDesc()
+    d.n_keep = len(out_labels)
+    d.n_ev = len(dynamic)
+    d.batch_dim = out_labels.index(ROW) if ROW in out_labels else -1
+    d.ld = int(ld)
+    d.row0 = int(row0)
+    for i, l in enumerate(out_labels):
+        d.keep_card[i] = keep_shape[i]
+        d.keep_sa[i] = 0 if l == ROW else int(A.stride(la.index(l)))
+        d.keep_sc[i] = int(out.stride(i))
+    for j, (l, col) in enumerate(dynamic.items()):
+        d.ev_col[j] = int(col)
+        d.ev_stride[j] = int(A.stride(la.index(l)))
+        d.ev_card[j] = card[l]
+    own_err = err is None and d.n_ev > 0
+    if own_err:
+        err = torch.zeros(1, dtype=torch.int32, device=A.device)
+    Aptr = ctypes.c_void_p(A.data_ptr() + 8 * base)
+    N.check(L.pgm_gather(ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err), N.stream_handle()), "gather")
+    if own_err and int(err.item()) != 0:
+        raise IndexError("evidence state code out of range for its variable")
+    return out
+
+
+def indicator(codes_col, card, n_rows, err=None):
+    """[card, n_rows] 0/1 evidence indicator from a uint8 code column (255 = unobserved)."""
+    L = N.lib()
+    out = empty([card, n_rows])
+    N.check(L.pgm_indicator(N.ptr(codes_col), int(n_rows), int(card), N.ptr(out), int(out.stride(0)),
+                            int(out.stride(1)), N.ptr(err), N.stream_handle()), "indicator")
+    return out

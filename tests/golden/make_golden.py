@@ -1,0 +1,582 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+This script is the only place that imports the read-only reference
+(/root/reference, pgmpy 1.0.0).  It runs in the build container only; the
+fixtures it writes (inputs + expected outputs, plain JSON / npz) are what the
+tests and the oracle are pinned against on the GPU box, where the reference
+does not exist.
+
+    PYTHONHASHSEED=0 PYTHONDONTWRITEBYTECODE=1 \
+        python tests/golden/make_golden.py [--only NAME ...] [--jobs 8]
+
+Three offline shims under tests/golden/shims/ stand in for packages the image
+lacks (scikit-base, statsmodels, opt_einsum).  opt_einsum's
+greedy path is restated there; contraction values do not depend on the path
+beyond floating-point rounding.
+
+Fixture inventory (SURVEY.md §8(c) "Golden vectors"):
+  networks/<net>_cpts.npz      CPT export of alarm / munin / pathfinder (parser pin)
+  factor_ops.json              DiscreteFactor op results on seeded small factors
+  unit_cases.json              hand-sized unit expectations of the reference tests
+  alarm_queries.json           C1: HISTORY|CVP=LOW + 50 seeded query patterns (+ MAP)
+  alarm_predict.json           predict / predict_probability on alarm rows (with NaN)
+  alarm_bp.npz / .json         BP calibration on a min-fill JT of alarm (full beliefs)
+  munin_predict.npz            C3 template rows, MAP codes and marginals
+  munin_c2_query.json          C2: 100 leaf findings -> 1 root posterior
+  pathfinder_bp.npz / .json    C4: min-fill JT + beliefs (checksums) + marginals
+"""
+import argparse
+import gzip
+import json
+import os
+import random
+import sys
+import time
+from multiprocessing import Pool
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+
+def _setup():
+    if os.environ.get("PYTHONHASHSEED") != "0":
+        raise SystemExit("run with PYTHONHASHSEED=0 (product() orders variables by set hash)")
+    for p in (REF, os.path.join(HERE, "shims")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    # the shims must shadow nothing real; put them after the reference
+    sys.path.remove(os.path.join(HERE, "shims"))
+    sys.path.insert(1, os.path.join(HERE, "shims"))
+    import logging
+
+    logging.getLogger("pgmpy").setLevel(logging.ERROR)
+    from pgmpy import config
+
+    config.set_show_progress(False) if hasattr(config, "set_show_progress") else None
+    config.SHOW_PROGRESS = False
+
+
+def _dump(name, obj):
+    path = os.path.join(HERE, name)
+    with open(path, "w") as f:
+        json.dump(obj, f, indent=None, separators=(",", ":"))
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+def _model(name):
+    from pgmpy.utils import get_example_model
+
+    return get_example_model(name)
+
+
+def _states(model):
+    return {v: [str(s) for s in model.get_cpds(v).state_names[v]] for v in model.nodes()}
+
+
+# ----------------------------------------------------------------------------- networks
+def gen_networks():
+    os.makedirs(os.path.join(HERE, "networks"), exist_ok=True)
+    for net in ("alarm", "munin", "pathfinder"):
+        m = _model(net)
+        meta = {"nodes": [], "states": {}, "parents": {}}
+        arrays = {}
+        for i, v in enumerate(sorted(m.nodes())):
+            cpd = m.get_cpds(v)
+            meta["nodes"].append(v)
+            meta["states"][v] = [str(s) for s in cpd.state_names[v]]
+            meta["parents"][v] = list(cpd.variables[1:])
+            meta.setdefault("parent_states", {})[v] = {
+                p: [str(s) for s in cpd.state_names[p]] for p in cpd.variables[1:]
+            }
+            arrays[f"v{i}"] = np.asarray(cpd.values, dtype=np.float64).ravel()
+        path = os.path.join(HERE, "networks", f"{net}_cpts.npz")
+        np.savez_compressed(path, meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8), **arrays)
+        print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+# ----------------------------------------------------------------------------- factor ops
+def _fac_json(phi):
+    return {
+        "variables": list(phi.variables),
+        "cardinality": [int(c) for c in phi.cardinality],
+        "values": [float(x) for x in np.asarray(phi.values, dtype=np.float64).ravel()],
+    }
+
+
+def gen_factor_ops():
+    """DiscreteFactor.{product,marginalize,maximize,reduce,normalize,divide,sum} on seeded factors.
+
+    pgmpy/factors/discrete/DiscreteFactor.py:360-866."""
+    from pgmpy.factors import factor_divide, factor_product
+    from pgmpy.factors.discrete import DiscreteFactor
+
+    rng = np.random.default_rng(20251017)
+    names = [f"x{i}" for i in range(8)]
+    cards = {n: int(c) for n, c in zip(names, rng.integers(2, 5, size=8))}
+    cases = []
+
+    def rand_factor(nv, zeros=False):
+        vs = list(rng.choice(names, size=nv, replace=False))
+        card = [cards[v] for v in vs]
+        vals = rng.random(int(np.prod(card)))
+        if zeros:
+            vals[rng.random(vals.size) < 0.3] = 0.0
+        return DiscreteFactor(vs, card, vals)
+
+    for t in range(40):
+        a = rand_factor(int(rng.integers(1, 4)), zeros=(t % 5 == 0))
+        b = rand_factor(int(rng.integers(1, 4)), zeros=(t % 7 == 0))
+        case = {"a": _fac_json(a), "b": _fac_json(b)}
+        case["product"] = _fac_json(a.product(b, inplace=False))
+        case["sum"] = _fac_json(a.sum(b, inplace=False))
+        k = int(rng.integers(1, len(a.variables) + 1))
+        mv = list(rng.choice(a.variables, size=k, replace=False))
+        case["marg_vars"] = mv
+        case["marginalize"] = _fac_json(a.marginalize(mv, inplace=False))
+        case["maximize"] = _fac_json(a.maximize(mv, inplace=False))
+        case["normalize"] = _fac_json(a.normalize(inplace=False))
+        rv = list(rng.choice(a.variables, size=int(rng.integers(1, len(a.variables) + 1)), replace=False))
+        red = [(v, int(rng.integers(0, cards[v]))) for v in rv]
+        case["reduce_vals"] = red
+        case["reduce"] = _fac_json(a.reduce(red, inplace=False))
+        # divide needs scope(b) subset of scope(a): divide a by a marginal of a (with zeros)
+        dsub = list(rng.choice(a.variables, size=int(rng.integers(1, len(a.variables) + 1)), replace=False))
+        den = DiscreteFactor(dsub, [cards[v] for v in dsub], rng.random(int(np.prod([cards[v] for v in dsub]))))
+        if t % 3 == 0:
+            dv = den.values.ravel()
+            dv[rng.random(dv.size) < 0.4] = 0.0
+            den = DiscreteFactor(dsub, [cards[v] for v in dsub], dv)
+        case["den"] = _fac_json(den)
+        case["divide"] = _fac_json(a.divide(den, inplace=False))
+        c = rand_factor(int(rng.integers(1, 3)))
+        case["c"] = _fac_json(c)
+        case["factor_product3"] = _fac_json(factor_product(a, b, c))
+        case["argmax"] = int(np.argmax(a.values))
+        cases.append(case)
+    _dump("factor_ops.json", {"cards": cards, "cases": cases})
+
+
+def gen_unit_cases():
+    """Numbers the reference's own unit tests pin (test_Factor.py, test_ExactInference.py).
+
+    Computed by running the reference on the same inputs as those tests."""
+    from pgmpy.factors.discrete import DiscreteFactor, TabularCPD
+    from pgmpy.inference import BeliefPropagation, VariableElimination
+    from pgmpy.models import DiscreteBayesianNetwork, JunctionTree
+
+    out = {}
+    # test_Factor.py:390-450 marginalize; docstring examples DiscreteFactor.py:381-388
+    phi = DiscreteFactor(["x1", "x2", "x3"], [2, 3, 2], range(12))
+    out["marg_x1_x3"] = _fac_json(phi.marginalize(["x1", "x3"], inplace=False))
+    phi1 = DiscreteFactor(["x1", "x2", "x3"], [2, 3, 2], range(12))
+    phi2 = DiscreteFactor(["x3", "x4", "x1"], [2, 2, 2], range(8))
+    out["product_doc"] = _fac_json(phi1.product(phi2, inplace=False))
+    out["sum_doc"] = _fac_json(phi1.sum(phi2, inplace=False))
+    d2 = DiscreteFactor(["x3", "x1"], [2, 2], range(1, 5))
+    out["divide_doc"] = _fac_json(phi1.divide(d2, inplace=False))
+    # divide with zeros: 0/0 -> 0, x/0 -> inf (test_Factor.py:674-723)
+    num = DiscreteFactor(["x1", "x2"], [2, 2], [0.0, 1.0, 2.0, 0.0])
+    den = DiscreteFactor(["x1"], [2], [0.0, 2.0])
+    r = num.divide(den, inplace=False)
+    out["divide_zero"] = {
+        "variables": r.variables,
+        "cardinality": [int(c) for c in r.cardinality],
+        "values": [("inf" if np.isinf(x) else float(x)) for x in r.values.ravel()],
+    }
+    mx = DiscreteFactor(["x1", "x2", "x3"], [3, 2, 2],
+                        [0.25, 0.35, 0.08, 0.16, 0.05, 0.07, 0.00, 0.00, 0.15, 0.21, 0.09, 0.18])
+    out["maximize_doc"] = _fac_json(mx.maximize(["x2"], inplace=False))
+    # TabularCPD normalize / marginalize / reduce docstring cases (CPD.py:449-567)
+    cpd = TabularCPD("grade", 2, [[0.7, 0.2, 0.6, 0.2], [0.4, 0.4, 0.4, 0.8]], ["intel", "diff"], [2, 2])
+    out["cpd_normalize"] = [list(map(float, r)) for r in cpd.normalize(inplace=False).get_values()]
+    cpd2 = TabularCPD("grade", 2, [[0.7, 0.6, 0.6, 0.2], [0.3, 0.4, 0.4, 0.8]], ["intel", "diff"], [2, 2])
+    out["cpd_marginalize_diff"] = [list(map(float, r)) for r in cpd2.marginalize(["diff"], inplace=False).get_values()]
+    out["cpd_reduce_diff0"] = [list(map(float, r)) for r in cpd2.reduce([("diff", 0)], inplace=False).get_values()]
+
+    # 6-node BN of test_ExactInference.py:22-60 (SAMIAM-pinned)
+    bn = DiscreteBayesianNetwork([("A", "J"), ("R", "J"), ("J", "Q"), ("J", "L"), ("G", "L")])
+    cpds = [
+        TabularCPD("A", 2, [[0.2], [0.8]]),
+        TabularCPD("R", 2, [[0.4], [0.6]]),
+        TabularCPD("J", 2, [[0.9, 0.6, 0.7, 0.1], [0.1, 0.4, 0.3, 0.9]], ["R", "A"], [2, 2]),
+        TabularCPD("Q", 2, [[0.9, 0.2], [0.1, 0.8]], ["J"], [2]),
+        TabularCPD("L", 2, [[0.9, 0.45, 0.8, 0.1], [0.1, 0.55, 0.2, 0.9]], ["G", "J"], [2, 2]),
+        TabularCPD("G", 2, [[0.6], [0.4]]),
+    ]
+    bn.add_cpds(*cpds)
+    out["bn6"] = {
+        "edges": [list(e) for e in bn.edges()],
+        "cpds": [{"variable": c.variable, "card": int(c.variable_card),
+                  "values": [list(map(float, r)) for r in c.get_values()],
+                  "evidence": list(c.variables[1:]), "evidence_card": [int(x) for x in c.cardinality[1:]]}
+                 for c in cpds],
+    }
+    ve = VariableElimination(bn)
+    q = {}
+    for order in ("greedy", "MinFill", "MinNeighbors", "MinWeight", "WeightedMinFill"):
+        r1 = ve.query(["J"], show_progress=False, elimination_order=order)
+        r2 = ve.query(["J", "Q"], evidence={"A": 0, "R": 0, "G": 0, "L": 1}, show_progress=False,
+                      elimination_order=order)
+        r3 = ve.query(["Q", "J"], evidence={"A": 1}, joint=False, show_progress=False, elimination_order=order)
+        q[order] = {"J": _fac_json(r1), "JQ|ARGL": _fac_json(r2),
+                    "Q,J|A=1 sep": {k: _fac_json(v) for k, v in r3.items()}}
+    out["bn6_queries"] = q
+    out["bn6_map_J"] = ve.map_query(["J"], show_progress=False)
+    out["bn6_map_JQ"] = ve.map_query(["J", "Q"], evidence={"A": 0, "R": 0, "G": 0, "L": 1}, show_progress=False)
+    out["bn6_max_marginal"] = float(ve.max_marginal(["J", "Q"], evidence={"A": 0, "R": 0, "G": 0, "L": 1}))
+    bp = BeliefPropagation(bn)
+    out["bn6_bp_query"] = _fac_json(bp.query(["J", "Q"], evidence={"A": 0, "R": 0, "G": 0, "L": 1}, show_progress=False))
+    out["bn6_bp_map"] = bp.map_query(["J", "Q"], evidence={"A": 0, "R": 0, "G": 0, "L": 1}, show_progress=False)
+
+    # BP on a given 3-clique junction tree (test_ExactInference.py:891-1033)
+    jt = JunctionTree()
+    jt.add_edges_from([(("A", "B"), ("B", "C")), (("B", "C"), ("C", "D"))])
+    phi1 = DiscreteFactor(["A", "B"], [2, 3], range(6))
+    phi2 = DiscreteFactor(["B", "C"], [3, 2], range(6))
+    phi3 = DiscreteFactor(["C", "D"], [2, 2], range(4))
+    jt.add_factors(phi1, phi2, phi3)
+    bpj = BeliefPropagation(jt)
+    bpj.calibrate()
+    out["jt3"] = {
+        "cliques": [list(c) for c in jt.nodes()],
+        "edges": [[list(a), list(b)] for a, b in jt.edges()],
+        "factors": [_fac_json(f) for f in (phi1, phi2, phi3)],
+        "clique_beliefs": [[list(c), _fac_json(v)] for c, v in bpj.get_clique_beliefs().items()],
+        "sepset_beliefs": [[sorted(map(list, k)), _fac_json(v)] for k, v in bpj.get_sepset_beliefs().items()],
+    }
+    bpj2 = BeliefPropagation(jt)
+    bpj2.max_calibrate()
+    out["jt3_max"] = {
+        "clique_beliefs": [[list(c), _fac_json(v)] for c, v in bpj2.get_clique_beliefs().items()],
+    }
+    _dump("unit_cases.json", out)
+
+
+# ----------------------------------------------------------------------------- alarm
+def gen_alarm():
+    """C1: HISTORY|CVP=LOW plus 50 patterns from random.Random(1)."""
+    from pgmpy.inference import VariableElimination
+    from pgmpy.sampling import BayesianModelSampling
+
+    m = _model("alarm")
+    ve = VariableElimination(m)
+    res = {"history_cvp_low": _fac_json(ve.query(["HISTORY"], {"CVP": "LOW"}, show_progress=False))}
+    samples = BayesianModelSampling(m).forward_sample(size=50, seed=1, show_progress=False)
+    rng = random.Random(1)
+    nodes = sorted(m.nodes())
+    pats = []
+    for i in range(50):
+        picks = rng.sample(nodes, 8)
+        qv, ev = picks[:3], picks[3:]
+        evidence = {v: str(samples.iloc[i][v]) for v in ev}
+        r = ve.query(qv, evidence, joint=False, show_progress=False)
+        rj = ve.query(qv, evidence, joint=True, show_progress=False)
+        rm = ve.query(qv, evidence, joint=True, show_progress=False, elimination_order="MinFill")
+        mp = ve.map_query(qv, evidence, show_progress=False)
+        jv = np.asarray(rj.values).ravel()
+        srt = np.sort(jv)[::-1]
+        pats.append({
+            "variables": qv, "evidence": evidence,
+            "marginals": {k: _fac_json(v) for k, v in r.items()},
+            "joint": _fac_json(rj), "joint_minfill": _fac_json(rm),
+            "map": {k: str(v) for k, v in mp.items()},
+            "map_gap": float(srt[0] - srt[1]) if srt.size > 1 else 1.0,
+        })
+    res["patterns"] = pats
+    _dump("alarm_queries.json", res)
+
+
+def gen_alarm_predict():
+    """predict / predict_probability (DiscreteBayesianNetwork.py:731-989) on alarm rows."""
+    import pandas as pd
+    from pgmpy.sampling import BayesianModelSampling
+
+    m = _model("alarm")
+    df = BayesianModelSampling(m).forward_sample(size=300, seed=3, show_progress=False)
+    rng = np.random.default_rng(3)
+    missing = ["LVFAILURE", "HYPOVOLEMIA", "STROKEVOLUME"]
+    data = df.drop(columns=missing).astype(object)
+    # sprinkle NaNs into 30 rows (these rows predict extra variables)
+    nan_rows = rng.choice(len(data), size=30, replace=False)
+    nan_col_choices = ["HISTORY", "CVP", "PCWP"]
+    for r in nan_rows:
+        data.iat[r, data.columns.get_loc(nan_col_choices[r % 3])] = np.nan
+    pred = m.predict(data, n_jobs=1)
+    clean = data.drop(index=data.index[nan_rows])
+    prob = m.predict_probability(clean)
+    _dump("alarm_predict.json", {
+        "columns": list(data.columns),
+        "rows": [[None if (isinstance(x, float) and np.isnan(x)) else str(x) for x in row] for row in data.values],
+        "missing": missing,
+        "predict_columns": list(pred.columns),
+        "predict": [[None if (isinstance(x, float) and np.isnan(x)) else str(x) for x in row] for row in pred.values],
+        "prob_index": [int(i) for i in clean.index],
+        "prob_columns": list(prob.columns),
+        "prob": prob.values.tolist(),
+    })
+
+
+# ----------------------------------------------------------------------------- junction trees
+def minfill_junction_tree(model):
+    """Min-fill JT used as the BP oracle input (SURVEY.md §8(c) "BP oracle caveat")."""
+    import networkx as nx
+    from networkx.algorithms.approximation import treewidth_min_fill_in
+    from pgmpy.factors.discrete import DiscreteFactor
+    from pgmpy.models import JunctionTree
+    from pgmpy.factors import factor_product
+
+    moral = model.moralize()
+    g = nx.Graph(moral.edges())
+    g.add_nodes_from(model.nodes())
+    tw, decomp = treewidth_min_fill_in(g)
+    bags = [tuple(sorted(b)) for b in decomp.nodes()]
+    jt = JunctionTree()
+    if len(bags) == 1:
+        jt.add_node(bags[0])
+    for a, b in decomp.edges():
+        jt.add_edge(tuple(sorted(a)), tuple(sorted(b)))
+    assigned = {b: [] for b in bags}
+    for node in sorted(model.nodes()):
+        cpd = model.get_cpds(node)
+        scope = set(cpd.scope())
+        for b in bags:
+            if scope <= set(b):
+                assigned[b].append(cpd.to_factor())
+                break
+        else:
+            raise RuntimeError(f"no bag covers {node}")
+    card = model.get_cardinality()
+    factors = []
+    for b in bags:
+        ones = DiscreteFactor(list(b), [card[v] for v in b], np.ones(int(np.prod([card[v] for v in b]))),
+                              state_names={v: model.get_cpds(v).state_names[v] for v in b})
+        pot = factor_product(ones, *assigned[b]) if assigned[b] else ones
+        pot = DiscreteFactor(list(b), [card[v] for v in b],
+                             pot.values.transpose([pot.variables.index(v) for v in b]).ravel(),
+                             state_names={v: model.get_cpds(v).state_names[v] for v in b})
+        factors.append(pot)
+    jt.add_factors(*factors)
+    return jt, bags, [(tuple(sorted(a)), tuple(sorted(b))) for a, b in decomp.edges()], assigned
+
+
+def _aligned(phi, order):
+    return np.asarray(phi.values).transpose([phi.variables.index(v) for v in order])
+
+
+def _bp_case(model, jt, bags, evidence):
+    """Calibrate with evidence applied as 0/1 indicators into the first clique holding each var."""
+    import copy
+
+    from pgmpy.factors.discrete import DiscreteFactor
+    from pgmpy.inference import BeliefPropagation
+
+    jt = copy.deepcopy(jt)
+    card = model.get_cardinality()
+    states = _states(model)
+    for var, st in evidence.items():
+        for b in bags:
+            if var in b:
+                f = jt.get_factors(b)
+                ind = np.zeros(card[var])
+                ind[states[var].index(st)] = 1.0
+                f2 = f.product(DiscreteFactor([var], [card[var]], ind,
+                                              state_names={var: model.get_cpds(var).state_names[var]}),
+                               inplace=False)
+                f2 = DiscreteFactor(list(b), [card[v] for v in b], _aligned(f2, b).ravel(), state_names=f.state_names)
+                jt.remove_factors(f)
+                jt.add_factors(f2)
+                break
+    bp = BeliefPropagation(jt)
+    bp.calibrate()
+    cb = bp.get_clique_beliefs()
+    sb = bp.get_sepset_beliefs()
+    beliefs = {b: _aligned(cb[b], b).ravel() for b in bags}
+    seps = {}
+    for k, v in sb.items():
+        a, b = sorted(tuple(x) for x in k)
+        sep = tuple(sorted(set(a) & set(b)))
+        seps[(a, b)] = _aligned(v, sep).ravel()
+    # variable marginals from the first clique holding each variable
+    marg = {}
+    for var in sorted(model.nodes()):
+        for b in bags:
+            if var in b:
+                arr = beliefs[b].reshape([card[v] for v in b])
+                axes = tuple(i for i, v in enumerate(b) if v != var)
+                m = arr.sum(axis=axes)
+                marg[var] = (m / m.sum()).tolist()
+                break
+    return beliefs, seps, marg
+
+
+def gen_alarm_bp():
+    m = _model("alarm")
+    jt, bags, edges, _ = minfill_junction_tree(m)
+    from pgmpy.sampling import BayesianModelSampling
+
+    s = BayesianModelSampling(m).forward_sample(size=4, seed=7, show_progress=False)
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    rng = random.Random(7)
+    cases = [{}]
+    for i in range(3):
+        ev = rng.sample(leaves, 4)
+        cases.append({v: str(s.iloc[i][v]) for v in ev})
+    arrays, meta = {}, {"bags": [list(b) for b in bags], "edges": [[list(a), list(b)] for a, b in edges],
+                        "cases": []}
+    for ci, ev in enumerate(cases):
+        beliefs, seps, marg = _bp_case(m, jt, bags, ev)
+        for bi, b in enumerate(bags):
+            arrays[f"c{ci}_b{bi}"] = beliefs[b]
+        sep_keys = []
+        for si, (k, v) in enumerate(sorted(seps.items())):
+            arrays[f"c{ci}_s{si}"] = v
+            sep_keys.append([list(k[0]), list(k[1])])
+        meta["cases"].append({"evidence": ev, "sep_keys": sep_keys, "marginals": marg})
+    np.savez_compressed(os.path.join(HERE, "alarm_bp.npz"), **arrays)
+    _dump("alarm_bp.json", meta)
+
+
+def gen_pathfinder_bp():
+    """C4: min-fill JT, 0 and 4-finding calibrations, checksums + marginals."""
+    m = _model("pathfinder")
+    jt, bags, edges, _ = minfill_junction_tree(m)
+    from pgmpy.sampling import BayesianModelSampling
+
+    s = BayesianModelSampling(m).forward_sample(size=4, seed=7, show_progress=False)
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    rng = random.Random(7)
+    cases = [{}]
+    for i in range(2):
+        ev = rng.sample(leaves, 4)
+        cases.append({v: str(s.iloc[i][v]) for v in ev})
+    wrng = np.random.default_rng(123)
+    arrays = {}
+    meta = {"bags": [list(b) for b in bags], "edges": [[list(a), list(b)] for a, b in edges], "cases": []}
+    sizes = [len(_aligned_size(m, b)) if False else None for b in bags]
+    card = m.get_cardinality()
+    bag_sizes = [int(np.prod([card[v] for v in b])) for b in bags]
+    small = sorted(range(len(bags)), key=lambda i: bag_sizes[i])[:12]
+    for ci, ev in enumerate(cases):
+        t0 = time.time()
+        beliefs, seps, marg = _bp_case(m, jt, bags, ev)
+        cs = []
+        for bi, b in enumerate(bags):
+            x = beliefs[b]
+            w = np.random.default_rng(1000 + bi).random(x.size)
+            cs.append([float(x.sum()), float((w * x).sum())])
+        arrays[f"c{ci}_checksums"] = np.array(cs)
+        for bi in small:
+            arrays[f"c{ci}_b{bi}"] = beliefs[bags[bi]]
+        meta["cases"].append({"evidence": ev, "marginals": marg, "seconds": time.time() - t0})
+    meta["small_bags"] = small
+    np.savez_compressed(os.path.join(HERE, "pathfinder_bp.npz"), **arrays)
+    _dump("pathfinder_bp.json", meta)
+
+
+def _aligned_size(m, b):
+    return b
+
+
+# ----------------------------------------------------------------------------- munin
+MUNIN_MISSING = None
+
+
+def _munin_rows(n, seed=42):
+    from pgmpy.sampling import BayesianModelSampling
+
+    m = _model("munin")
+    return m, BayesianModelSampling(m).forward_sample(size=n, seed=seed, show_progress=False)
+
+
+def _munin_worker(args):
+    _setup()
+    lo, hi, rows_json, missing = args
+    import pandas as pd
+
+    m = _model("munin")
+    df = pd.DataFrame(rows_json)
+    df = df.iloc[lo:hi]
+    t0 = time.time()
+    pred = m.predict(df, n_jobs=1)
+    t1 = time.time()
+    prob = m.predict_probability(df)
+    t2 = time.time()
+    return lo, pred[missing].values.tolist(), list(prob.columns), prob.values.tolist(), t1 - t0, t2 - t1
+
+
+def gen_munin_predict(n_rows=1000, jobs=8):
+    """C3 template: missing = random.Random(0).sample(sorted(nodes), 3)."""
+    m, samples = _munin_rows(n_rows, seed=42)
+    nodes = sorted(m.nodes())
+    missing = random.Random(0).sample(nodes, 3)
+    print("munin missing:", missing)
+    df = samples.drop(columns=missing).astype(str)
+    rows_json = df.to_dict(orient="list")
+    chunks = []
+    step = (n_rows + jobs - 1) // jobs
+    for lo in range(0, n_rows, step):
+        chunks.append((lo, min(n_rows, lo + step), rows_json, missing))
+    with Pool(jobs) as pool:
+        res = pool.map(_munin_worker, chunks)
+    res.sort()
+    states = _states(m)
+    pred_codes = np.array([[states[v].index(str(x)) for v, x in zip(missing, r)] for _, p, _, _, _, _ in res for r in p],
+                          dtype=np.uint8)
+    prob_cols = res[0][2]
+    prob = np.array([r for _, _, _, p, _, _ in res for r in p], dtype=np.float64)
+    cols = list(df.columns)
+    codes = np.array([[states[c].index(str(x)) for x in df[c]] for c in cols], dtype=np.uint8)  # [V][N]
+    meta = {"missing": missing, "columns": cols, "prob_columns": prob_cols,
+            "predict_s_per_row": sum(r[4] for r in res) / n_rows,
+            "predict_probability_s_per_row": sum(r[5] for r in res) / n_rows}
+    np.savez_compressed(os.path.join(HERE, "munin_predict.npz"), codes=codes, map_codes=pred_codes, prob=prob,
+                        meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8))
+    print("wrote munin_predict.npz", meta["predict_s_per_row"], meta["predict_probability_s_per_row"])
+
+
+def gen_munin_c2():
+    """C2: 100 leaf findings -> 1 root, VariableElimination.query greedy path."""
+    from pgmpy.inference import VariableElimination
+
+    m, samples = _munin_rows(20, seed=0)
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    roots = sorted(n for n in m.nodes() if m.in_degree(n) == 0)
+    rng = random.Random(100000)
+    E = rng.sample(leaves, 100)
+    q = [rng.choice(roots)]
+    evidence = {v: str(samples.iloc[0][v]) for v in E}
+    t0 = time.time()
+    r = VariableElimination(m).query(q, evidence, show_progress=False)
+    dt = time.time() - t0
+    _dump("munin_c2_query.json", {"variables": q, "evidence": evidence, "result": _fac_json(r), "seconds": dt})
+
+
+GENS = {
+    "networks": gen_networks,
+    "factor_ops": gen_factor_ops,
+    "unit_cases": gen_unit_cases,
+    "alarm": gen_alarm,
+    "alarm_predict": gen_alarm_predict,
+    "alarm_bp": gen_alarm_bp,
+    "pathfinder_bp": gen_pathfinder_bp,
+    "munin_predict": gen_munin_predict,
+    "munin_c2": gen_munin_c2,
+}
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--munin-rows", type=int, default=1000)
+    a = ap.parse_args()
+    _setup()
+    for name in (a.only or list(GENS)):
+        t0 = time.time()
+        if name == "munin_predict":
+            gen_munin_predict(a.munin_rows, a.jobs)
+        else:
+            GENS[name]()
+        print(f"[{name}] {time.time() - t0:.1f}s")

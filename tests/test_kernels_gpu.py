@@ -1,0 +1,158 @@
+"""Primitive-kernel parity on the GPU: pgm_contract / pgm_gather / pgm_argmax / pgm_rows_*.
+
+Each kernel is checked against the numpy arithmetic the reference itself runs
+(np.einsum / np.max / np.argmax / basic indexing: DiscreteFactor.py:408,480,614,
+771-777; compat_fns.py:53-74).  Tolerance: 1e-12 relative for sums (fp64,
+different summation order), exact for copies, max and argmax.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _e():
+    from pgmpy_amd import engine
+
+    return engine
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_contract_random_einsum(gpu, seed):
+    E = _e()
+    rng = np.random.default_rng(seed)
+    labels = list("abcdefg")
+    card = {l: int(rng.integers(1, 6)) for l in labels}
+    la = list(rng.choice(labels, size=int(rng.integers(1, 5)), replace=False))
+    lb = list(rng.choice(labels, size=int(rng.integers(1, 5)), replace=False))
+    a = rng.random([card[l] for l in la])
+    b = rng.random([card[l] for l in lb])
+    union = list(dict.fromkeys(la + lb))
+    keep = [l for l in union if rng.random() < 0.6]
+    rng.shuffle(keep)
+    A, B = E.to_device(a), E.to_device(b)
+    ref = np.einsum(a, [labels.index(l) for l in la], b, [labels.index(l) for l in lb],
+                    [labels.index(l) for l in keep])
+    got = E.to_host(E.contract(A, la, B, lb, keep, reduce="sum", combine="mul"))
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0)
+    # max-product
+    full = np.einsum(a, [labels.index(l) for l in la], b, [labels.index(l) for l in lb],
+                     [labels.index(l) for l in union])
+    red = tuple(i for i, l in enumerate(union) if l not in keep)
+    refm = np.max(full, axis=red) if red else full
+    refm = np.transpose(refm, [[l for l in union if l in keep].index(l) for l in keep]) if keep else refm
+    gotm = E.to_host(E.contract(A, la, B, lb, keep, reduce="max", combine="mul"))
+    np.testing.assert_array_equal(gotm, refm)
+
+
+def test_contract_large_reduction_split(gpu):
+    """Tiny output, huge reduction -> split-K path with the finalize kernel."""
+    E = _e()
+    rng = np.random.default_rng(1)
+    a = rng.random((3, 1 << 20))
+    A = E.to_device(a)
+    got = E.to_host(E.contract(A, ["x", "y"], None, None, ["x"], reduce="sum", combine="copy"))
+    np.testing.assert_allclose(got, a.sum(axis=1), rtol=1e-12)
+    got0 = E.to_host(E.contract(A, ["x", "y"], None, None, ["y"], reduce="sum", combine="copy"))
+    np.testing.assert_allclose(got0, a.sum(axis=0), rtol=1e-12)
+    tot = E.to_host(E.total(A))
+    np.testing.assert_allclose(tot, a.sum(), rtol=1e-12)
+    mx = E.to_host(E.contract(A, ["x", "y"], None, None, ["x"], reduce="max", combine="copy"))
+    np.testing.assert_array_equal(mx, a.max(axis=1))
+
+
+def test_divide_and_normalize_semantics(gpu):
+    E = _e()
+    a = np.array([[0.0, 1.0], [2.0, 0.0]])
+    b = np.array([0.0, 2.0])
+    A, B = E.to_device(a), E.to_device(b)
+    got = E.to_host(E.contract(A, ["x1", "x2"], B, ["x1"], ["x1", "x2"], combine="div"))
+    # DiscreteFactor.py:859-863: 0/0 -> 0, x/0 -> inf
+    np.testing.assert_array_equal(got, np.array([[0.0, np.inf], [1.0, 0.0]]))
+    z = E.to_device(np.zeros(4))
+    E.normalize_(z)
+    assert np.isnan(E.to_host(z)).all()
+
+
+def test_argmax_first_index_and_nan(gpu):
+    E = _e()
+    x = np.array([[1.0, 3.0, 3.0, 2.0], [0.0, 0.0, 0.0, 0.0], [1.0, np.nan, 5.0, np.nan]])
+    X = E.to_device(x)
+    got = E.to_host(E.argmax_rows(X, ["r", "i"], row_label="r").double()).astype(int)
+    assert list(got) == [int(np.argmax(r)) for r in x]
+
+
+def test_gather_per_row(gpu):
+    import torch
+
+    E = _e()
+    rng = np.random.default_rng(5)
+    a = rng.random((3, 4, 5))
+    n = 1000
+    codes = np.stack([rng.integers(0, 4, n), rng.integers(0, 5, n)]).astype(np.uint8)
+    C = torch.from_numpy(codes).to(gpu)
+    A = E.to_device(a)
+    out = E.gather(A, ["x", "y", "z"], {"y": (None, 0), "z": (None, 1)}, ["x", E.ROW], codes=C, ld=n, n_rows=n)
+    got = E.to_host(out)
+    ref = np.stack([a[:, codes[0, r], codes[1, r]] for r in range(n)], axis=1)
+    np.testing.assert_array_equal(got, ref)
+    bad = torch.from_numpy(np.full((2, n), 7, dtype=np.uint8)).to(gpu)
+    with pytest.raises(IndexError):
+        E.gather(A, ["x", "y", "z"], {"y": (None, 0), "z": (None, 1)}, ["x", E.ROW], codes=bad, ld=n, n_rows=n)
+
+
+def test_rows_plan_matches_numpy(gpu):
+    """Hand-built fused plan: 2 query dims, 1 hidden dim, 3 factors with evidence."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as N
+
+    rng = np.random.default_rng(11)
+    cq0, cq1, ch, ce0, ce1 = 3, 4, 2, 5, 3
+    f0 = rng.random((cq0, ce0))            # (q0, e0)
+    f1 = rng.random((cq1, cq0, ch))        # (q1, q0, h)
+    f2 = rng.random((ch, ce1, cq1))        # (h, e1, q1)
+    vals = np.concatenate([f0.ravel(), f1.ravel(), f2.ravel()])
+    P = N.RowsPlan()
+    P.n_loop, P.n_query, P.n_fac, P.n_ev, P.n_values = 3, 2, 3, 2, vals.size
+    for i, c in enumerate([cq0, cq1, ch]):
+        P.loop_card[i] = c
+    P.fac_base[0], P.fac_base[1], P.fac_base[2] = 0, f0.size, f0.size + f1.size
+    s0, s1, s2 = [x // 8 for x in f0.strides], [x // 8 for x in f1.strides], [x // 8 for x in f2.strides]
+    # loop dims: 0=q0, 1=q1, 2=h
+    P.fac_stride[0][0] = s0[0]
+    P.fac_stride[1][1], P.fac_stride[1][0], P.fac_stride[1][2] = s1[0], s1[1], s1[2]
+    P.fac_stride[2][2], P.fac_stride[2][1] = s2[0], s2[2]
+    P.fac_ev_begin[0], P.fac_ev_end[0] = 0, 1
+    P.fac_ev_begin[1], P.fac_ev_end[1] = 1, 1
+    P.fac_ev_begin[2], P.fac_ev_end[2] = 1, 2
+    P.ev_col[0], P.ev_stride[0], P.ev_card[0] = 0, s0[1], ce0
+    P.ev_col[1], P.ev_stride[1], P.ev_card[1] = 1, s2[1], ce1
+    L = N.lib()
+    h = ctypes.c_void_p()
+    N.check(L.pgm_rows_plan_create(ctypes.byref(P), vals.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)))
+    n = 777
+    codes = np.stack([rng.integers(0, ce0, n), rng.integers(0, ce1, n)]).astype(np.uint8)
+    C = torch.from_numpy(codes).to(gpu)
+    marg = torch.empty((cq0 + cq1, n), dtype=torch.float64, device=gpu)
+    joint = torch.empty((cq0 * cq1, n), dtype=torch.float64, device=gpu)
+    mp = torch.empty(n, dtype=torch.int32, device=gpu)
+    gap = torch.empty(n, dtype=torch.float64, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    mode = N.ROWS_MARGINALS | N.ROWS_JOINT | N.ROWS_MAP | N.ROWS_MAPGAP
+    N.check(L.pgm_rows_plan_run(h, mode, N.ptr(C), n, 0, n, N.ptr(marg), N.ptr(joint), n, N.ptr(mp), N.ptr(gap),
+                                N.ptr(err), N.stream_handle()))
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    joint_h, marg_h, mp_h = joint.cpu().numpy(), marg.cpu().numpy(), mp.cpu().numpy()
+    for r in range(n):
+        e0, e1 = codes[0, r], codes[1, r]
+        j = np.einsum("a,bah,hb->ab", f0[:, e0], f1, f2[:, e1, :])
+        z = j.sum()
+        np.testing.assert_allclose(joint_h[:, r], (j / z).ravel(), rtol=1e-12)
+        np.testing.assert_allclose(marg_h[:cq0, r], j.sum(1) / z, rtol=1e-12)
+        np.testing.assert_allclose(marg_h[cq0:, r], j.sum(0) / z, rtol=1e-12)
+        assert int(mp_h[r]) == int(np.argmax(j))
+    N.check(L.pgm_rows_plan_destroy(h))
