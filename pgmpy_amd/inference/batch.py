@@ -1,0 +1,211 @@
+"""Batched-evidence front end: DataFrame <-> uint8 codes, pattern grouping, result frames.
+
+Replaces the per-row Python loops of DiscreteBayesianNetwork.predict (joblib
+threads over map_query per unique row, DiscreteBayesianNetwork.py:866-910) and
+predict_probability (iterrows + query, L962-989).  Rows are encoded once into
+column-major uint8 state codes (255 = NaN / unobserved),
+grouped by evidence pattern, and each pattern runs as one compiled device plan
+(pgmpy_amd.inference.plan.PatternPlan).
+"""
+import ctypes
+
+import numpy as np
+
+from .. import _native as N
+from .. import engine as E
+from .plan import PatternPlan
+
+MISSING = N.PGM_EV_MISSING
+
+
+def encode_frame(model, data, columns=None):
+    """[n_cols, n_rows] uint8 codes of `data` (state names -> state numbers, NaN -> 255)."""
+    import pandas as pd
+
+    columns = list(data.columns) if columns is None else list(columns)
+    states = model.states
+    n = len(data)
+    codes = np.empty((len(columns), n), dtype=np.uint8)
+    for j, col in enumerate(columns):
+        st = list(states[col])
+        if len(st) >= MISSING:
+            raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
+        v = data[col]
+        isna = v.isna().to_numpy()
+        cat = pd.Categorical(v, categories=st)
+        c = np.asarray(cat.codes, dtype=np.int64)
+        bad = (c < 0) & ~isna
+        if bad.any():
+            # retry through str(): numeric frames against string state names (and vice versa)
+            sm = {str(s): i for i, s in enumerate(st)}
+            vals = v.to_numpy(object)
+            for i in np.nonzero(bad)[0]:
+                k = sm.get(str(vals[i]))
+                if k is None:
+                    raise KeyError(f"state: {vals[i]} is an unknown for variable: {col}. It must be one of {st}")
+                c[i] = k
+        c[isna] = MISSING
+        codes[j] = c.astype(np.uint8)
+    return codes
+
+
+def upload_codes(codes):
+    """Host uint8 [n_cols, n] -> device (through pgm_memcpy_h2d)."""
+    import torch
+
+    L = N.lib()
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    t = torch.empty(codes.shape, dtype=torch.uint8, device=E.device())
+    if codes.size:
+        N.check(L.pgm_memcpy_h2d(N.ptr(t), codes.ctypes.data_as(ctypes.c_void_p), codes.nbytes, N.stream_handle()),
+                "memcpy_h2d")
+    return t
+
+
+def download(t):
+    """Device tensor -> numpy through pgm_memcpy_d2h."""
+    import torch
+
+    L = N.lib()
+    dt = {torch.float64: np.float64, torch.int32: np.int32, torch.int64: np.int64, torch.uint8: np.uint8}[t.dtype]
+    if not t.is_contiguous():
+        raise ValueError("download needs a contiguous tensor")
+    out = np.empty(tuple(t.shape), dtype=dt)
+    if out.size:
+        N.check(L.pgm_memcpy_d2h(out.ctypes.data_as(ctypes.c_void_p), N.ptr(t), out.nbytes, N.stream_handle()),
+                "memcpy_d2h")
+    return out
+
+
+def group_patterns(codes):
+    """Rows grouped by which columns are observed: list of (observed column mask, row indices)."""
+    miss = codes == MISSING  # [n_cols, n]
+    if not miss.any():
+        return [(np.ones(codes.shape[0], dtype=bool), np.arange(codes.shape[1]))]
+    packed = np.packbits(miss.T, axis=1)
+    uniq, inv = np.unique(packed, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    groups = []
+    for g in range(len(uniq)):
+        rows = np.nonzero(inv == g)[0]
+        groups.append((~miss[:, rows[0]], rows))
+    return groups
+
+
+_PLAN_CACHE_ATTR = "_pgmpy_amd_plan_cache"
+
+
+def get_plan(model, variables, evidence_vars, col_of):
+    cache = getattr(model, _PLAN_CACHE_ATTR, None)
+    if cache is None:
+        cache = {}
+        setattr(model, _PLAN_CACHE_ATTR, cache)
+    key = (tuple(variables), tuple(evidence_vars), tuple(sorted((k, v) for k, v in col_of.items()
+                                                                if k in set(evidence_vars))))
+    plan = cache.get(key)
+    if plan is None:
+        plan = PatternPlan(model, variables, evidence_vars, col_of)
+        cache[key] = plan
+    return plan
+
+
+def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars):
+    """Yield (plan, rows, outputs-on-host) per evidence pattern."""
+    columns = list(data.columns)
+    col_of = {c: i for i, c in enumerate(columns)}
+    codes = encode_frame(model, data, columns)
+    for mask, rows in group_patterns(codes):
+        observed = [columns[j] for j in range(len(columns)) if mask[j]]
+        nan_cols = [columns[j] for j in range(len(columns)) if not mask[j]]
+        variables = list(base_vars) + ([c for c in nan_cols if c not in base_vars] if extra_nan_vars else [])
+        plan = get_plan(model, variables, observed, col_of)
+        sub = codes if len(rows) == codes.shape[1] else codes[:, rows]
+        dcodes = upload_codes(sub)
+        n = len(rows)
+        out = plan.alloc_outputs(n, marginals=want_marg, map_=want_map)
+        err = None
+        import torch
+
+        err = torch.zeros(1, dtype=torch.int32, device=dcodes.device)
+        plan.run(dcodes, n, 0, n, out, err=err)
+        if int(download(err)[0]) != 0:
+            raise IndexError("evidence state code out of range")
+        host = {k: download(v) for k, v in out.items()}
+        yield plan, rows, host
+
+
+def predict_probability_frame(model, data):
+    """DiscreteBayesianNetwork.predict_probability (DiscreteBayesianNetwork.py:912-989)."""
+    import pandas as pd
+
+    missing_variables = set(model.nodes()) - set(data.columns)
+    order = list(missing_variables)  # the reference's set iteration order (column order of its output)
+    n = len(data)
+    cols = {}
+    for var in order:
+        for s in model.get_cpds(var).state_names[var]:
+            cols[var + "_" + str(s)] = np.empty(n)
+    for plan, rows, host in _run_groups(model, data, order, True, False, False):
+        for i, var in enumerate(plan.variables[:len(order)]):
+            a = plan.acc_off[i]
+            for k, s in enumerate(plan.states[var]):
+                cols[var + "_" + str(s)][rows] = host["marg"][a + k]
+    return pd.DataFrame(cols, index=data.index)
+
+
+def predict_frame(model, data):
+    """DiscreteBayesianNetwork.predict, MAP (DiscreteBayesianNetwork.py:731-910)."""
+    import pandas as pd
+
+    missing_variables = set(model.nodes()) - set(data.columns)
+    order = list(missing_variables)
+    all_columns = data.columns.tolist() + [col for col in missing_variables]
+    result = data.reindex(columns=all_columns).astype(object)
+    vals = {c: result[c].to_numpy(object).copy() for c in all_columns}
+    for plan, rows, host in _run_groups(model, data, order, False, True, True):
+        idx = host["map"].astype(np.int64)
+        # decode the flat index (C-order over plan.variables, last fastest)
+        for i in reversed(range(len(plan.variables))):
+            var = plan.variables[i]
+            c = plan.cards[i]
+            st = np.array(plan.states[var], dtype=object)
+            vals[var][rows] = st[idx % c]
+            idx = idx // c
+    out = pd.DataFrame(vals, index=data.index, columns=all_columns)
+    return out.sort_index()
+
+
+def query_batch(model, variables, evidence, joint=False):
+    """P(variables | row) for every row of the evidence DataFrame (NaN = unobserved)."""
+    n = len(evidence)
+    res = None
+    cards = [int(model.get_cardinality(v)) for v in variables]
+    if joint:
+        res = np.empty([n] + cards)
+    else:
+        res = {v: np.empty((n, c)) for v, c in zip(variables, cards)}
+    columns = list(evidence.columns)
+    col_of = {c: i for i, c in enumerate(columns)}
+    codes = encode_frame(model, evidence, columns)
+    import torch
+
+    for mask, rows in group_patterns(codes):
+        observed = [columns[j] for j in range(len(columns)) if mask[j]]
+        plan = get_plan(model, list(variables), observed, col_of)
+        sub = codes if len(rows) == codes.shape[1] else codes[:, rows]
+        dcodes = upload_codes(sub)
+        m = len(rows)
+        out = plan.alloc_outputs(m, marginals=not joint, joint=joint)
+        err = torch.zeros(1, dtype=torch.int32, device=dcodes.device)
+        plan.run(dcodes, m, 0, m, out, err=err)
+        if int(download(err)[0]) != 0:
+            raise IndexError("evidence state code out of range")
+        if joint:
+            j = download(out["joint"])  # [P, m]
+            res[rows] = j.T.reshape([m] + cards)
+        else:
+            mg = download(out["marg"])
+            for i, v in enumerate(variables):
+                a = plan.acc_off[i]
+                res[v][rows] = mg[a:a + cards[i]].T
+    return res

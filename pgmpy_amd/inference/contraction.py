@@ -1,0 +1,174 @@
+"""Greedy pairwise sum-product contraction (replaces opt_einsum.contract(..., optimize="greedy")).
+
+Reference call sites: pgmpy/inference/ExactInference.py:404-406 (the default
+VariableElimination.query path) and pgmpy/factors/base.py:106
+(factor_sum_product).  opt_einsum (pyproject.toml:36, ">=3.3", unpinned, not
+vendored) plans a greedy path; its published greedy strategy is restated here:
+
+  1. sum every label that occurs in exactly one operand and not in the output;
+  2. repeatedly contract the pair of operands that share a label and minimise
+     size(result) - size(a) - size(b), keeping a label in the result while any
+     other operand or the output still needs it;
+  3. with no pair sharing a label left, take outer products of the two
+     smallest operands.
+
+Every pairwise step is ONE fused product+marginalize kernel (pgm_contract,
+combine=MUL, reduce=SUM): the broadcast product is never materialised.  A
+``ROW`` label (evidence rows) is just another kept label, so the same planner
+and executor run single queries (C2) and row batches.
+"""
+import heapq
+from itertools import count
+
+import numpy as np
+
+from .. import engine as E
+
+
+def _size(labels, dims):
+    s = 1
+    for l in labels:
+        s *= int(dims[l])
+    return s
+
+
+def greedy_path(operand_labels, out_labels, dims):
+    """Plan the contraction.
+
+    Returns (steps, final_id): steps are ("reduce", i, keep, new_id) or
+    ("pair", i, j, keep, new_id) over operand ids (inputs are 0..n-1)."""
+    out_set = set(out_labels)
+    ops = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    holders = {}
+    for i, ls in ops.items():
+        for l in ls:
+            holders.setdefault(l, set()).add(i)
+    steps = []
+    ids = count(len(operand_labels))
+
+    def kept(labels, exclude):
+        return [l for l in labels if l in out_set or len(holders[l] - exclude) > 0]
+
+    # 1. private labels
+    for i in list(ops):
+        ls = ops[i]
+        keep = kept(ls, {i})
+        if keep != ls:
+            nid = next(ids)
+            steps.append(("reduce", i, keep, nid))
+            for l in ls:
+                holders[l].discard(i)
+            for l in keep:
+                holders[l].add(nid)
+            del ops[i]
+            ops[nid] = keep
+
+    def pair_entry(i, j):
+        li, lj = ops[i], ops[j]
+        union = list(dict.fromkeys(li + lj))
+        keep = kept(union, {i, j})
+        cost = _size(keep, dims) - _size(li, dims) - _size(lj, dims)
+        return (cost, min(i, j), max(i, j), keep)
+
+    heap = []
+    seen = set()
+
+    def push_pairs(i):
+        partners = set()
+        for l in ops[i]:
+            partners |= holders[l]
+        partners.discard(i)
+        for j in partners:
+            key = (min(i, j), max(i, j))
+            if key in seen:
+                continue
+            seen.add(key)
+            c, a, b, keep = pair_entry(i, j)
+            heapq.heappush(heap, (c, a, b, keep))
+
+    for i in list(ops):
+        push_pairs(i)
+    while len(ops) > 1:
+        entry = None
+        while heap:
+            c, a, b, keep = heapq.heappop(heap)
+            if a in ops and b in ops:
+                entry = (a, b, keep)
+                break
+        if entry is None:
+            # disconnected operands: outer product of the two smallest
+            sizes = sorted(ops, key=lambda k: (_size(ops[k], dims), k))
+            a, b = sizes[0], sizes[1]
+            union = list(dict.fromkeys(ops[a] + ops[b]))
+            entry = (a, b, kept(union, {a, b}))
+        a, b, keep = entry
+        nid = next(ids)
+        steps.append(("pair", a, b, keep, nid))
+        for l in ops[a] + ops[b]:
+            holders[l].discard(a)
+            holders[l].discard(b)
+        for l in keep:
+            holders[l].add(nid)
+        del ops[a], ops[b]
+        ops[nid] = keep
+        push_pairs(nid)
+    (final_id,) = ops.keys() if ops else (None,)
+    return steps, final_id
+
+
+def plan_stats(operand_labels, out_labels, dims):
+    """Algorithmic bytes / flops of the planned path (SURVEY.md §8(d) C2 definition):
+    sum over pairwise steps of 8 (|A| + |B| + |C|) bytes and 2 |index space| flops."""
+    steps, _ = greedy_path(operand_labels, out_labels, dims)
+    labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    nbytes = flops = 0
+    max_inter = 0
+    for st in steps:
+        if st[0] == "reduce":
+            _, i, keep, nid = st
+            nbytes += 8 * (_size(labels[i], dims) + _size(keep, dims))
+            flops += _size(labels[i], dims)
+        else:
+            _, i, j, keep, nid = st
+            union = list(dict.fromkeys(labels[i] + labels[j]))
+            nbytes += 8 * (_size(labels[i], dims) + _size(labels[j], dims) + _size(keep, dims))
+            flops += 2 * _size(union, dims)
+        labels[nid] = keep
+        max_inter = max(max_inter, _size(keep, dims))
+    return {"steps": len(steps), "bytes": nbytes, "flops": flops, "max_intermediate": max_inter}
+
+
+def contract_factors(operands, out_labels, reduce="sum"):
+    """sum_{labels not in out} prod operands, on the device.
+
+    operands: list of (device tensor, labels).  Returns a tensor over
+    out_labels (C-order).  reduce="max" gives the max-product variant."""
+    if not operands:
+        raise ValueError("nothing to contract")
+    dims = {}
+    for t, ls in operands:
+        if len(ls) != t.dim():
+            raise ValueError("label count does not match tensor rank")
+        for d, l in enumerate(ls):
+            c = int(t.shape[d])
+            if dims.setdefault(l, c) != c:
+                raise ValueError(f"cardinality mismatch for {l!r}")
+    for l in out_labels:
+        if l not in dims:
+            raise ValueError(f"output label {l!r} not in any operand")
+    steps, final_id = greedy_path([ls for _, ls in operands], out_labels, dims)
+    live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
+    for st in steps:
+        if st[0] == "reduce":
+            _, i, keep, nid = st
+            t, ls = live.pop(i)
+            live[nid] = (E.contract(t, ls, None, None, keep, reduce=reduce, combine="copy"), keep)
+        else:
+            _, i, j, keep, nid = st
+            ti, li = live.pop(i)
+            tj, lj = live.pop(j)
+            live[nid] = (E.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
+    t, ls = live[final_id]
+    if ls != list(out_labels):
+        t = E.contract(t, ls, None, None, list(out_labels), reduce=reduce, combine="copy")
+    return t

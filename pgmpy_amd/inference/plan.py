@@ -1,0 +1,261 @@
+"""Evidence-pattern plan compiler for batched inference.
+
+For one evidence *pattern* — the set of observed variables E and the query
+variables Q — everything that does not depend on the observed *states* is
+done once on the host:
+
+  1. prune the network (d-separation + ancestral graph, pgmpy/inference/base.py:154-212),
+     summing pruned parents out of CPDs on the device (TabularCPD.marginalize);
+  2. drop factors whose scope is all evidence (ExactInference.py:383);
+  3. pick an executor:
+     * FUSED  (pgm_rows_plan_*): when the query+hidden index space is small, one
+       kernel runs reduce -> sum-product -> normalize -> marginals / joint / MAP
+       for every row, one lane per row, CPTs staged in LDS (the munin predict
+       template of SURVEY.md §8(d) C3: 5 CPTs, 7 evidence columns, 180-entry joint);
+     * STEPS: otherwise, per-row evidence gathers (pgm_gather) and a greedy
+       pairwise path of fused product+marginalize kernels over tensors that
+       carry an evidence-row axis (pgmpy_amd.inference.contraction).
+
+Per batch only the uint8 evidence-code columns the plan reads are touched.
+A compiled plan is immutable; run() is re-entrant on distinct outputs.
+"""
+import ctypes
+
+import numpy as np
+
+from .. import _native as N
+from .. import engine as E
+from .base import prune_structure
+from .contraction import contract_factors, plan_stats
+
+FUSED_MAX_SPACE = 4096  # query x hidden index space per row for the fused kernel
+
+
+class PatternPlan:
+    """Compiled plan for (query variables, observed variables) on a DiscreteBayesianNetwork."""
+
+    def __init__(self, model, variables, evidence_vars, col_of, force=None):
+        self.model = model
+        self.variables = list(variables)
+        self.evidence_vars = list(evidence_vars)
+        self.col_of = dict(col_of)
+        overlap = set(self.variables) & set(self.evidence_vars)
+        if overlap:
+            raise ValueError(f"Can't have the same variables in both `variables` and `evidence`. "
+                             f"Found in both: {overlap}")
+        if not self.variables:
+            raise ValueError("The `variables` argument to query() must contain at least one variable.")
+        states = model.states
+        self.states = {v: list(states[v]) for v in self.variables}
+        self.cards = [len(self.states[v]) for v in self.variables]
+        self.n_acc = int(sum(self.cards))
+        self.acc_off = list(np.cumsum([0] + self.cards[:-1]))
+        self.P = int(np.prod(self.cards))
+
+        kept, ev = prune_structure(model, self.variables, self.evidence_vars)
+        kept_set, ev_set = set(kept), set(ev)
+        factors = []  # (vars, host values C-order)
+        for var in kept:
+            cpd = model.get_cpds(var)
+            scope_diff = set(cpd.scope()) - kept_set
+            if scope_diff:
+                cpd = cpd.marginalize(scope_diff, inplace=False)  # device op
+            vars_ = list(cpd.variables)
+            if all(v in ev_set for v in vars_):
+                continue  # ExactInference.py:383
+            factors.append((vars_, cpd))
+        self.factors = factors
+        self.ev_used = sorted({v for vars_, _ in factors for v in vars_ if v in ev_set},
+                              key=lambda v: self.col_of[v])
+        hidden = []
+        for vars_, _ in factors:
+            for v in vars_:
+                if v not in ev_set and v not in self.variables and v not in hidden:
+                    hidden.append(v)
+        self.hidden = hidden
+        card = {v: int(model.get_cardinality(v)) for v in set(self.variables) | set(hidden) | ev_set}
+        self.card = card
+        self.H = int(np.prod([card[v] for v in hidden])) if hidden else 1
+        n_ev_terms = sum(1 for vars_, _ in factors for v in vars_ if v in ev_set)
+        fused_ok = (len(factors) <= N.ROWS_MAX_FAC and len(self.variables) + len(hidden) <= N.ROWS_MAX_LOOP
+                    and n_ev_terms <= N.ROWS_MAX_EV and self.n_acc <= N.ROWS_MAX_ACC
+                    and self.P * self.H <= FUSED_MAX_SPACE)
+        self.kind = force or ("fused" if fused_ok else "steps")
+        if self.kind == "fused" and not fused_ok:
+            raise ValueError("pattern does not fit the fused row kernel")
+        self._handle = None
+        if self.kind == "fused":
+            self._build_fused()
+
+    # ------------------------------------------------------------------ fused
+    def _build_fused(self):
+        loop = self.variables + self.hidden
+        pl = N.RowsPlan()
+        pl.n_loop = len(loop)
+        pl.n_query = len(self.variables)
+        pl.n_fac = len(self.factors)
+        for i, v in enumerate(loop):
+            pl.loop_card[i] = self.card[v]
+        chunks, base, ev_terms = [], 0, []
+        for f, (vars_, cpd) in enumerate(self.factors):
+            vals = np.ascontiguousarray(cpd.values, dtype=np.float64).reshape(-1)
+            cards = [int(c) for c in cpd.cardinality]
+            strides = [int(np.prod(cards[i + 1:])) for i in range(len(cards))]
+            pl.fac_base[f] = base
+            pl.fac_ev_begin[f] = len(ev_terms)
+            for v, s in zip(vars_, strides):
+                if v in loop:
+                    pl.fac_stride[f][loop.index(v)] = s
+                else:
+                    ev_terms.append((self.col_of[v], s, self.card[v]))
+            pl.fac_ev_end[f] = len(ev_terms)
+            chunks.append(vals)
+            base += vals.size
+        pl.n_ev = len(ev_terms)
+        for j, (col, s, c) in enumerate(ev_terms):
+            pl.ev_col[j], pl.ev_stride[j], pl.ev_card[j] = col, s, c
+        values = np.concatenate(chunks) if chunks else np.zeros(1)
+        if values.size >= 2 ** 31:
+            raise ValueError("plan values too large")
+        pl.n_values = int(values.size)
+        self._values = values
+        self._plan = pl
+        L = N.lib()
+        h = ctypes.c_void_p()
+        N.check(L.pgm_rows_plan_create(ctypes.byref(pl), values.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)),
+                "rows_plan_create")
+        self._handle = h
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and h.value:
+            try:
+                N.load_library().pgm_rows_plan_destroy(h)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------ run
+    def alloc_outputs(self, n_rows, marginals=True, joint=False, map_=False, gap=False):
+        import torch
+
+        dev = E.device()
+        out = {}
+        if marginals:
+            out["marg"] = torch.empty((self.n_acc, n_rows), dtype=torch.float64, device=dev)
+        if joint:
+            out["joint"] = torch.empty((self.P, n_rows), dtype=torch.float64, device=dev)
+        if map_ or gap:
+            out["map"] = torch.empty(n_rows, dtype=torch.int32, device=dev)
+        if gap:
+            out["gap"] = torch.empty(n_rows, dtype=torch.float64, device=dev)
+        return out
+
+    def run(self, codes, ld, row0, n_rows, out, err=None):
+        """Run the plan on rows [row0, row0+n_rows) of the column-major uint8 codes [n_cols, ld].
+
+        out: dict from alloc_outputs (marg [n_acc, n], joint [P, n], map [n] int32, gap [n])."""
+        if n_rows <= 0:
+            return out
+        if self.kind == "fused":
+            return self._run_fused(codes, ld, row0, n_rows, out, err)
+        return self._run_steps(codes, ld, row0, n_rows, out, err)
+
+    def _mode(self, out):
+        mode = 0
+        if "marg" in out:
+            mode |= N.ROWS_MARGINALS
+        if "joint" in out:
+            mode |= N.ROWS_JOINT
+        if "map" in out:
+            mode |= N.ROWS_MAP
+        if "gap" in out:
+            mode |= N.ROWS_MAPGAP
+        return mode
+
+    def _run_fused(self, codes, ld, row0, n_rows, out, err):
+        L = N.lib()
+        ld_out = None
+        for k in ("marg", "joint"):
+            if k in out:
+                ld_out = int(out[k].stride(0))
+        N.check(L.pgm_rows_plan_run(self._handle, self._mode(out), N.ptr(codes), int(ld), int(row0), int(n_rows),
+                                    N.ptr(out.get("marg")), N.ptr(out.get("joint")), int(ld_out or n_rows),
+                                    N.ptr(out.get("map")), N.ptr(out.get("gap")), N.ptr(err), N.stream_handle()),
+                "rows_plan_run")
+        return out
+
+    def _dev_factors(self):
+        if not hasattr(self, "_dev_cache"):
+            self._dev_cache = [(cpd._d(), vars_) for vars_, cpd in self.factors]
+        return self._dev_cache
+
+    def max_intermediate_per_row(self):
+        labels, dims = [], dict(self.card)
+        dims[E.ROW] = 1
+        for vars_, _ in self.factors:
+            ls = [v for v in vars_ if v not in self.evidence_vars]
+            if any(v in self.evidence_vars for v in vars_):
+                ls = ls + [E.ROW]
+            labels.append(ls)
+        return max(1, plan_stats(labels, self.variables + [E.ROW], dims)["max_intermediate"])
+
+    def _run_steps(self, codes, ld, row0, n_rows, out, err):
+        """Batched greedy contraction with an evidence-row axis; rows chunked to bound memory."""
+        import torch
+
+        L = N.lib()
+        ev_set = set(self.evidence_vars)
+        per_row = self.max_intermediate_per_row()
+        chunk = max(1, min(n_rows, (1 << 26) // per_row))
+        for c0 in range(0, n_rows, chunk):
+            n = min(chunk, n_rows - c0)
+            ops = []
+            for t, vars_ in self._dev_factors():
+                rem = [v for v in vars_ if v not in ev_set]
+                dyn = {v: (None, self.col_of[v]) for v in vars_ if v in ev_set}
+                if dyn:
+                    g = E.gather(t, vars_, dyn, rem + [E.ROW], codes=codes, ld=ld, row0=row0 + c0, n_rows=n, err=err)
+                    ops.append((g, rem + [E.ROW]))
+                else:
+                    ops.append((t, list(vars_)))
+            outl = self.variables + [E.ROW]
+            if not any(E.ROW in ls for _, ls in ops):
+                # no evidence touches this pattern: broadcast one result over the rows
+                ones = E.to_device(np.ones(n))
+                ops.append((ones, [E.ROW]))
+            R = contract_factors(ops, outl)  # [Q..., ROW] C-order
+            Z = E.contract(R, outl, None, None, [E.ROW], reduce="sum", combine="copy")
+            if "marg" in out:
+                for i, v in enumerate(self.variables):
+                    a = self.acc_off[i]
+                    view = out["marg"][a:a + self.cards[i], c0:c0 + n]
+                    m = E.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
+                    E.contract(m, [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw", out=view)
+            if "map" in out:
+                idx = torch.empty(n, dtype=torch.int64, device=R.device)
+                N.check(L.pgm_argmax(N.ptr(R), n, self.P, 1, n, N.ptr(idx), N.stream_handle()), "argmax")
+                out["map"][c0:c0 + n].copy_(idx.to(torch.int32))
+                if "gap" in out:
+                    out["gap"][c0:c0 + n].fill_(1.0)
+            if "joint" in out:
+                jv = out["joint"][:, c0:c0 + n]
+                E.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw", out=jv)
+        return out
+
+    # ------------------------------------------------------------------ accounting
+    def algorithmic_bytes_per_row(self, marginals=True, map_=False, joint=False):
+        """HBM bytes per row the plan must move: evidence codes read + outputs written
+        (7 B + 136 B marginals or + 3 B MAP codes)."""
+        b = len(self.ev_used)
+        if marginals:
+            b += 8 * self.n_acc
+        if joint:
+            b += 8 * self.P
+        if map_:
+            b += len(self.variables)  # one uint8 state code per MAP variable
+        return b
+
+    def describe(self):
+        return {"kind": self.kind, "factors": [list(v) for v, _ in self.factors], "hidden": self.hidden,
+                "evidence_columns": len(self.ev_used), "query_space": self.P, "hidden_space": self.H,
+                "values": int(sum(int(np.prod(c.cardinality)) for _, c in self.factors))}

@@ -1,0 +1,238 @@
+"""DiscreteBayesianNetwork (the hot path's container and data-parallel caller).
+
+Mirrors the parts of pgmpy/models/DiscreteBayesianNetwork.py and
+pgmpy/base/DAG.py the hot path touches: CPD bookkeeping (add_cpds/get_cpds
+L243-353), check_model (L451-508), moralize (DAG.py:449), d-separation
+(active_trail_nodes DAG.py:864-950, _get_ancestors_of L952-990,
+get_ancestral_graph L1163-1186), to_junction_tree (L539-594) and the
+data-parallel callers predict / predict_probability (L731-989).
+
+predict / predict_probability do not loop over rows in Python: rows are
+grouped by evidence pattern (which columns are observed), each pattern is
+compiled once into a device plan (pgmpy_amd.inference.plan) and every row of
+the pattern runs in one fused kernel launch.
+"""
+import logging
+from collections import defaultdict
+
+import networkx as nx
+import numpy as np
+
+from ..factors.discrete import TabularCPD
+
+logger = logging.getLogger("pgmpy")
+
+
+class DiscreteBayesianNetwork(nx.DiGraph):
+    def __init__(self, ebunch=None, latents=set()):
+        super().__init__()
+        self.cpds = []
+        self._cpd_index = {}
+        self.cardinalities = defaultdict(int)
+        self.latents = set(latents)
+        if ebunch:
+            self.add_edges_from(ebunch)
+
+    # ------------------------------------------------------------------ structure
+    def add_edge(self, u, v, **kwargs):
+        if u == v:
+            raise ValueError("Self loops are not allowed.")
+        if u in self.nodes() and v in self.nodes() and nx.has_path(self, v, u):
+            raise ValueError(f"Loops are not allowed. Adding the edge from ({u}->{v}) forms a loop.")
+        super().add_edge(u, v, **kwargs)
+
+    def add_edges_from(self, ebunch, **kwargs):
+        for e in ebunch:
+            self.add_edge(*e[:2], **kwargs)
+
+    def get_parents(self, node):
+        return list(self.predecessors(node))
+
+    def get_children(self, node):
+        return list(self.successors(node))
+
+    def moralize(self):
+        """Moral graph (DAG.py:449-470): drop directions, marry co-parents."""
+        g = nx.Graph()
+        g.add_nodes_from(self.nodes())
+        g.add_edges_from(self.to_undirected().edges())
+        for node in self.nodes():
+            ps = list(self.predecessors(node))
+            for i in range(len(ps)):
+                for j in range(i + 1, len(ps)):
+                    g.add_edge(ps[i], ps[j])
+        return g
+
+    # ------------------------------------------------------------------ CPDs
+    def add_cpds(self, *cpds):
+        # DiscreteBayesianNetwork.py:243-283
+        for cpd in cpds:
+            if not isinstance(cpd, TabularCPD):
+                raise ValueError("Only TabularCPD can be added.")
+            if set(cpd.scope()) - set(cpd.scope()).intersection(set(self.nodes())):
+                raise ValueError("CPD defined on variable not in the model", cpd)
+            if cpd.variable in self._cpd_index:
+                logger.warning(f"Replacing existing CPD for {cpd.variable}")
+                for i, c in enumerate(self.cpds):
+                    if c.variable == cpd.variable:
+                        self.cpds[i] = cpd
+                        break
+            else:
+                self.cpds.append(cpd)
+            self._cpd_index[cpd.variable] = cpd
+
+    def get_cpds(self, node=None):
+        if node is not None:
+            if node not in self.nodes():
+                raise ValueError("Node not present in the Directed Graph")
+            return self._cpd_index.get(node)
+        return self.cpds
+
+    def remove_cpds(self, *cpds):
+        for cpd in cpds:
+            if isinstance(cpd, (str, int)):
+                cpd = self.get_cpds(cpd)
+            self.cpds.remove(cpd)
+            self._cpd_index.pop(cpd.variable, None)
+
+    def get_cardinality(self, node=None):
+        if node is not None:
+            return self.get_cpds(node).cardinality[0]
+        return defaultdict(int, {cpd.variable: cpd.cardinality[0] for cpd in self.cpds})
+
+    @property
+    def states(self):
+        return {var: self.get_cpds(var).state_names[var] for var in self.nodes()}
+
+    def check_model(self):
+        # DiscreteBayesianNetwork.py:451-508
+        for node in self.nodes():
+            cpd = self.get_cpds(node=node)
+            if cpd is None:
+                raise ValueError(f"No CPD associated with {node}")
+            evidence = cpd.get_evidence()
+            if set(evidence) != set(self.get_parents(node)):
+                raise ValueError(f"CPD associated with {node} doesn't have proper parents associated with it.")
+            if len(set(cpd.variables) - set(cpd.state_names.keys())) > 0:
+                raise ValueError(f"CPD for {node} doesn't have state names defined for all the variables.")
+            if not cpd.is_valid_cpd():
+                raise ValueError(f"Sum or integral of conditional probabilities for node {node} is not equal to 1.")
+        for node in self.nodes():
+            cpd = self.get_cpds(node=node)
+            for index, par in enumerate(cpd.variables[1:]):
+                parent_cpd = self.get_cpds(par)
+                if parent_cpd.cardinality[0] != cpd.cardinality[1 + index]:
+                    raise ValueError(f"The cardinality of {par} doesn't match in it's child nodes.")
+                if parent_cpd.state_names[par] != cpd.state_names[par]:
+                    raise ValueError(f"The state names of {par} doesn't match in it's child nodes.")
+        return True
+
+    def copy(self):
+        m = DiscreteBayesianNetwork(latents=self.latents)
+        m.add_nodes_from(self.nodes())
+        m.add_edges_from(self.edges())
+        if self.cpds:
+            m.add_cpds(*[cpd.copy() for cpd in self.cpds])
+        return m
+
+    # ------------------------------------------------------------------ d-separation (DAG.py)
+    def _get_ancestors_of(self, nodes):
+        if not isinstance(nodes, (list, tuple)):
+            nodes = [nodes]
+        for node in nodes:
+            if node not in self.nodes():
+                raise ValueError(f"Node {node} not in graph")
+        anc = set()
+        for node in nodes:
+            anc.update(nx.ancestors(self, node))
+        anc.update(nodes)
+        return anc
+
+    def active_trail_nodes(self, variables, observed=None, include_latents=False):
+        """Reachable nodes by active trails (Koller & Friedman Alg. 3.1; DAG.py:864-950)."""
+        if observed:
+            if isinstance(observed, set):
+                observed = list(observed)
+            observed_list = observed if isinstance(observed, (list, tuple)) else [observed]
+        else:
+            observed_list = []
+        observed_set = set(observed_list)
+        ancestors_list = self._get_ancestors_of(observed_list)
+        active_trails = {}
+        for start in variables if isinstance(variables, list) else [variables]:
+            visit_list = {(start, "up")}
+            traversed = set()
+            active_nodes = set()
+            while visit_list:
+                node, direction = visit_list.pop()
+                if (node, direction) in traversed:
+                    continue
+                if node not in observed_set:
+                    active_nodes.add(node)
+                traversed.add((node, direction))
+                if direction == "up" and node not in observed_set:
+                    for parent in self.predecessors(node):
+                        visit_list.add((parent, "up"))
+                    for child in self.successors(node):
+                        visit_list.add((child, "down"))
+                elif direction == "down":
+                    if node not in observed_set:
+                        for child in self.successors(node):
+                            visit_list.add((child, "down"))
+                    if node in ancestors_list:
+                        for parent in self.predecessors(node):
+                            visit_list.add((parent, "up"))
+            active_trails[start] = active_nodes if include_latents else active_nodes - self.latents
+        return active_trails
+
+    def get_ancestral_graph(self, nodes):
+        anc = self._get_ancestors_of(list(nodes))
+        g = DiscreteBayesianNetwork()
+        g.add_nodes_from([n for n in self.nodes() if n in anc])
+        g.add_edges_from([(u, v) for u, v in self.edges() if u in anc and v in anc])
+        return g
+
+    # ------------------------------------------------------------------ junction tree
+    def to_junction_tree(self):
+        """Junction tree with clique potentials = product of the CPDs assigned to each clique.
+
+        The reference triangulates with heuristic H6 (DiscreteMarkovNetwork.py:324-518),
+        which builds a 75-variable clique on pathfinder (ValueError) and a 95.5M-state
+        clique on alarm (SURVEY.md headline 4).  This uses a proper min-fill elimination
+        (pgmpy_amd.inference.EliminationOrder.min_fill_cliques); the calibrated marginals
+        are the same distribution (BP is exact on any junction tree)."""
+        from ..inference.EliminationOrder import junction_tree_from_model
+
+        return junction_tree_from_model(self)
+
+    # ------------------------------------------------------------------ data-parallel callers
+    def predict(self, data, algo=None, stochastic=False, n_jobs=-1, seed=None, **kwargs):
+        """MAP of the missing variables per row (DiscreteBayesianNetwork.py:731-910).
+
+        Rows are grouped by evidence pattern; each pattern is one compiled device plan
+        (fused one-lane-per-row kernel).  The output frame matches the reference:
+        columns data.columns + missing variables, rows in index order, state names."""
+        from ..inference.batch import predict_frame
+
+        if set(data.columns) == set(self.nodes()):
+            raise ValueError("No variable missing in data. Nothing to predict")
+        elif set(data.columns) - set(self.nodes()):
+            raise ValueError("Data has variables which are not in the model")
+        if algo is not None:
+            from ..inference import Inference
+
+            if not (isinstance(algo, type) and issubclass(algo, Inference)):
+                raise TypeError(f"Algorithm should be a valid pgmpy inference method. Got {type(algo)} instead.")
+        if stochastic:
+            raise NotImplementedError("stochastic=True (sampling from the posterior) is outside the accelerated path")
+        return predict_frame(self, data)
+
+    def predict_probability(self, data):
+        """Per-row marginals of every missing variable (DiscreteBayesianNetwork.py:912-989)."""
+        from ..inference.batch import predict_probability_frame
+
+        if set(data.columns) == set(self.nodes()):
+            raise ValueError("No variable missing in data. Nothing to predict")
+        elif set(data.columns) - set(self.nodes()):
+            raise ValueError("Data has variables which are not in the model")
+        return predict_probability_frame(self, data)

@@ -1,0 +1,7 @@
+from .DiscreteBayesianNetwork import DiscreteBayesianNetwork
+from .JunctionTree import JunctionTree
+
+# pgmpy < 1.0 name
+BayesianNetwork = DiscreteBayesianNetwork
+
+__all__ = ["DiscreteBayesianNetwork", "BayesianNetwork", "JunctionTree"]

@@ -77,21 +77,61 @@ def contract(*args, optimize="greedy", **kwargs):
         new_ops.append((a, keep))
     ops = new_ops
 
-    while len(ops) > 1:
-        best = None
-        for i in range(len(ops)):
-            for j in range(i + 1, len(ops)):
-                li, lj = ops[i][1], ops[j][1]
-                shared = set(li) & set(lj)
-                union = list(dict.fromkeys(li + lj))
-                keep = [l for l in union if needed_elsewhere(l, {i, j})]
-                cost = _size(keep, dims) - _size(li, dims) - _size(lj, dims)
-                key = (0 if shared else 1, cost)
-                if best is None or key < best[0]:
-                    best = (key, i, j, keep)
-        _, i, j, keep = best
-        res = _einsum_local([ops[i], ops[j]], keep)
-        ops = [op for k, op in enumerate(ops) if k not in (i, j)] + [(res, keep)]
+    # heap of candidate pairs that share a label (lazy deletion of dead operands)
+    import heapq
+
+    live = {i: op for i, op in enumerate(ops)}
+    holders = {}
+    for i, (_, ls) in live.items():
+        for l in ls:
+            holders.setdefault(l, set()).add(i)
+    nxt = len(ops)
+
+    def kept(labels, exclude):
+        return [l for l in labels if l in out_labels or len(holders[l] - exclude) > 0]
+
+    heap, seen = [], set()
+
+    def push(i):
+        partners = set()
+        for l in live[i][1]:
+            partners |= holders[l]
+        partners.discard(i)
+        for j in partners:
+            key = (min(i, j), max(i, j))
+            if key in seen:
+                continue
+            seen.add(key)
+            li, lj = live[key[0]][1], live[key[1]][1]
+            keep = kept(list(dict.fromkeys(li + lj)), set(key))
+            cost = _size(keep, dims) - _size(li, dims) - _size(lj, dims)
+            heapq.heappush(heap, (cost, key[0], key[1], keep))
+
+    for i in list(live):
+        push(i)
+    while len(live) > 1:
+        pick = None
+        while heap:
+            cost, a, b, keep = heapq.heappop(heap)
+            if a in live and b in live:
+                pick = (a, b, keep)
+                break
+        if pick is None:
+            a, b = sorted(live, key=lambda k: (_size(live[k][1], dims), k))[:2]
+            pick = (a, b, kept(list(dict.fromkeys(live[a][1] + live[b][1])), {a, b}))
+        a, b, keep = pick
+        res = _einsum_local([live[a], live[b]], keep)
+        for l in live[a][1] + live[b][1]:
+            holders[l].discard(a)
+            holders[l].discard(b)
+        del live[a], live[b]
+        nid = nxt
+        nxt += 1
+        live[nid] = (res, keep)
+        for l in keep:
+            holders[l].add(nid)
+        push(nid)
+    ops = list(live.values())
 
     a, ls = ops[0]
     return _einsum_local([(a, ls)], out_labels)

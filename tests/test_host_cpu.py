@@ -1,0 +1,115 @@
+"""Host-side logic that needs no GPU: the C-ABI library, BIF reader, pruning, planners, encoding.
+
+The library test loads libpgmhip.so and checks it exports every entry point
+declared in include/pgmhip.h (no compute call: no device here).
+"""
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import ve as OVE
+from oracle.network import load_network
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.build import build
+
+    build(verbose=False)
+    lib = N.load_library()
+    header = open(os.path.join(ROOT, "include", "pgmhip.h")).read()
+    declared = set(re.findall(r"\bint\s+(pgm_[a-z0-9_]+)\s*\(", header))
+    assert declared, "no declarations parsed"
+    assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.pgm_version() == 1
+
+
+def test_struct_layouts_match_header():
+    """ctypes mirrors of the descriptors have the C sizes (pgmhip.h)."""
+    import ctypes
+
+    from pgmpy_amd import _native as N
+
+    assert ctypes.sizeof(N.ContractDesc) == 16 + 7 * 8 * N.PGM_MAX_DIMS
+    assert ctypes.sizeof(N.GatherDesc) == 16 + 16 + 6 * 8 * N.PGM_MAX_DIMS
+    assert ctypes.sizeof(N.RowsPlan) == 4 * (8 + N.ROWS_MAX_LOOP + N.ROWS_MAX_FAC * (3 + N.ROWS_MAX_LOOP)
+                                             + 3 * N.ROWS_MAX_EV)
+
+
+def test_no_compute_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.factors.discrete import DiscreteFactor
+
+    phi = DiscreteFactor(["a"], [2], [1.0, 2.0])
+    with pytest.raises(N.NativeUnavailable):
+        phi.normalize(inplace=False)
+
+
+@pytest.mark.parametrize("net", ["alarm", "munin", "pathfinder"])
+def test_bif_reader_matches_reference_export(net):
+    """pgmpy_amd.readwrite.BIFReader == the reference BIFReader's CPTs (pinned by the fixture)."""
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model(net)
+    o = load_network(net)
+    assert sorted(m.nodes()) == o.nodes
+    for v in o.nodes:
+        cpd = m.get_cpds(v)
+        assert list(cpd.variables[1:]) == list(o.parents[v])
+        assert [str(s) for s in cpd.state_names[v]] == o.states[v]
+        np.testing.assert_array_equal(np.asarray(cpd._host).reshape(o.cpts[v].shape), o.cpts[v])
+
+
+def test_pruning_matches_oracle():
+    from pgmpy_amd.inference.base import prune_structure
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("alarm")
+    o = load_network("alarm")
+    rng = np.random.default_rng(0)
+    nodes = sorted(m.nodes())
+    for _ in range(30):
+        picks = list(rng.choice(nodes, size=7, replace=False))
+        q, e = picks[:2], picks[2:]
+        kept, ev = prune_structure(m, q, e)
+        keep_o, _ = OVE.prune(o, q, e)
+        assert set(kept) == keep_o
+
+
+def test_greedy_planner_contract_semantics():
+    from pgmpy_amd.inference.contraction import greedy_path, plan_stats
+
+    labels = [["a", "b"], ["b", "c"], ["c", "d"], ["x"]]
+    dims = {"a": 2, "b": 3, "c": 4, "d": 5, "x": 6}
+    steps, final = greedy_path(labels, ["a", "d"], dims)
+    # x is private and not in the output: summed first
+    assert steps[0][0] == "reduce" and steps[0][2] == []
+    assert final is not None
+    st = plan_stats(labels, ["a", "d"], dims)
+    assert st["steps"] == len(steps)
+
+
+def test_encode_and_group_patterns():
+    from pgmpy_amd.inference.batch import encode_frame, group_patterns
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("asia")
+    df = pd.DataFrame({"asia": ["yes", "no", None, "no"], "smoke": ["no", "yes", "yes", None]})
+    codes = encode_frame(m, df)
+    st_asia = list(m.states["asia"])
+    assert codes[0, 0] == st_asia.index("yes") and codes[0, 2] == 255 and codes[1, 3] == 255
+    groups = group_patterns(codes)
+    assert sorted(len(r) for _, r in groups) == [1, 1, 2]
+    with pytest.raises(KeyError):
+        encode_frame(m, pd.DataFrame({"asia": ["maybe"]}))
