@@ -1,0 +1,357 @@
+#!/usr/bin/env python3
+"""Benchmark: evidence-batched marginal queries/sec on munin (BASELINE.json metric).
+
+Workload: the munin predict_probability template —
+missing = random.Random(0).sample(sorted(nodes), 3), evidence = the other 1,038
+variables — on synthetic forward-sampled evidence rows (seed 42 + rank),
+ROWS per GPU per step (default 100,000 = C3).  One step = one pass of the hot
+path over the batch: the compiled fused row plan (pgm_rows_plan_run: evidence
+gather -> sum-product -> normalize -> per-variable marginals) reading the
+column-major uint8 evidence resident in HBM and writing the [17, rows] fp64
+marginals to HBM.
+
+    python bench.py [--gpus N --steps K --warmup W --rows R]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, rows sharded: weak scaling)
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
+(k_rows; achieved = algorithmic bytes per launch / HIP-event launch time) and a
+CPU baseline (the numpy oracle's per-row predict_probability, single core,
+bounded sample) timed on this host.
+Other workloads for DESIGN.md numbers: --workload c2 (single munin query,
+greedy device contraction) and c4 (pathfinder batched BP calibration).
+"""
+import argparse
+import ctypes
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "evidence-batched marginal queries/sec on munin; achieved HBM GB/s vs peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world
+    if torch.cuda.is_available():
+        torch.cuda.set_device(0)
+    return None, 0, 1
+
+
+def barrier(dist):
+    import torch
+
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class HipTimer:
+    """HIP events on the stream the kernels are launched on (pgm_event_*)."""
+
+    def __init__(self):
+        from pgmpy_amd import _native as N
+
+        self.N = N
+        self.L = N.lib()
+        self.a, self.b = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(self.L.pgm_event_create(ctypes.byref(self.a)))
+        N.check(self.L.pgm_event_create(ctypes.byref(self.b)))
+
+    def start(self):
+        self.N.check(self.L.pgm_event_record(self.a, self.N.stream_handle()))
+
+    def stop_ms(self):
+        self.N.check(self.L.pgm_event_record(self.b, self.N.stream_handle()))
+        ms = ctypes.c_float()
+        self.N.check(self.L.pgm_event_elapsed_ms(self.a, self.b, ctypes.byref(ms)))
+        return float(ms.value)
+
+
+def load_traffic(kernel):
+    """HBM bytes/launch from a committed rocprofv3 PMC summary (profiles/pmc_<kernel>.json), if present."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d.get("rows_per_launch")
+
+
+def cpu_baseline_c3(model, missing, codes_host, nodes, seconds):
+    """numpy oracle (oracle/ve.py), per-row predict_probability semantics, single core."""
+    from oracle import ve as OVE
+    from oracle.network import load_network
+
+    net = load_network("munin")
+    pos = {v: i for i, v in enumerate(nodes)}
+    obs = [v for v in nodes if v not in missing]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        ev = {v: net.states[v][codes_host[pos[v], n]] for v in obs}
+        OVE.query(net, list(missing), ev, joint_out=False)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= codes_host.shape[1]:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} of the same synthetic munin rows, numpy oracle per-row query "
+                      f"(prune + greedy einsum contraction + normalize + marginals), {dt:.1f} s"}
+
+
+def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64):
+    """First rows of the device output against the oracle (1e-6 relative, BASELINE.json)."""
+    from oracle import ve as OVE
+    from oracle.network import load_network
+    from pgmpy_amd.inference.batch import download
+
+    net = load_network("munin")
+    pos = {v: i for i, v in enumerate(nodes)}
+    obs = [v for v in nodes if v not in missing]
+    marg = download(out["marg"])
+    worst = 0.0
+    for r in range(n_check):
+        ev = {v: net.states[v][codes_host[pos[v], r]] for v in obs}
+        m = OVE.query(net, list(plan.variables), ev, joint_out=False)
+        exp = np.concatenate([m[v] for v in plan.variables])
+        got = marg[:, r]
+        both_nan = np.isnan(exp) & np.isnan(got)
+        err = np.abs(got - exp)[~both_nan] / np.maximum(np.abs(exp[~both_nan]), 1e-300)
+        mask = np.abs(exp[~both_nan]) > 1e-12
+        if mask.any():
+            worst = max(worst, float(err[mask].max()))
+    return {"rows_checked": n_check, "max_rel_err": worst, "ok": worst <= 1e-6}
+
+
+def bench_c3(args, dist, rank, world):
+    import torch
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    model = get_example_model("munin")
+    missing_list = random.Random(0).sample(sorted(model.nodes()), 3)
+    missing = set(model.nodes()) - (set(model.nodes()) - set(missing_list))
+    variables = list(missing)  # the reference's predict_probability column order (set iteration)
+    rows = args.rows
+    t0 = time.perf_counter()
+    codes_all, nodes = forward_sample_codes(model, rows, seed=42 + rank)
+    observed = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])  # [1038, rows]
+    col_of = {v: i for i, v in enumerate(observed)}
+    log(f"[rank {rank}] sampled {rows} rows in {time.perf_counter() - t0:.1f}s")
+    plan = PatternPlan(model, variables, observed, col_of)
+    assert plan.kind == "fused", plan.describe()
+    d_codes = upload_codes(codes_ev)
+    out = plan.alloc_outputs(rows, marginals=True)
+    err = torch.zeros(1, dtype=torch.int32, device=d_codes.device)
+    for _ in range(args.warmup):
+        plan.run(d_codes, rows, 0, rows, out, err=err)
+    barrier(dist)
+    timer = HipTimer()
+    timer.start()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run(d_codes, rows, 0, rows, out, err=err)
+    kern_ms_total = timer.stop_ms()
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t_end - t_start)
+    assert int(err.item()) == 0
+    total_rows = rows * world * args.steps
+    value = total_rows / elapsed
+    kern_ms = kern_ms_total / args.steps
+    bpr = plan.algorithmic_bytes_per_row(marginals=True)
+    achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_rows = load_traffic("k_rows")
+    if traffic is not None and traffic_rows:
+        traffic = traffic * rows / traffic_rows
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (forward-sampled munin evidence rows, seed 42+rank)",
+        "config": {
+            "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, "
+                        "fused row plan (pgm_rows_plan_run)",
+            "network": "munin",
+            "missing": variables,
+            "rows_per_gpu_per_step": rows,
+            "global_rows_per_step": rows * world,
+            "parallelism": f"rows sharded over {world} GPU(s), no data-path collective",
+            "plan": plan.describe(),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_rows",
+            "kernel_ms": kern_ms,
+            "algorithmic_bytes_per_row": bpr,
+            "bytes_per_launch": bpr * rows,
+        },
+    }
+    if rank == 0:
+        result["parity"] = parity_spot_check(model, missing, plan, out, codes_all, nodes)
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline_c3(model, missing, codes_all, nodes, args.cpu_seconds)
+            result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
+    if dist is not None and args.gather:
+        from pgmpy_amd.distributed import gather_rows
+
+        barrier(dist)
+        g0 = time.perf_counter()
+        gathered = gather_rows(out["marg"], rows * world, dist)
+        torch.cuda.synchronize()
+        result["gather_ms"] = (time.perf_counter() - g0) * 1e3
+    return result
+
+
+def bench_c2(args):
+    """C2: one munin query, 100 leaf findings -> 1 root, greedy device contraction."""
+    import torch
+
+    from pgmpy_amd.inference import VariableElimination
+    from pgmpy_amd.inference.contraction import plan_stats
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    roots = sorted(n for n in m.nodes() if m.in_degree(n) == 0)
+    rng = random.Random(100000)
+    E = rng.sample(leaves, 100)
+    q = [rng.choice(roots)]
+    codes, nodes = forward_sample_codes(m, 1, seed=0)
+    st = m.states
+    evidence = {v: st[v][codes[nodes.index(v), 0]] for v in E}
+    ve = VariableElimination(m)
+    for _ in range(args.warmup):
+        ve.query(q, evidence, show_progress=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = ve.query(q, evidence, show_progress=False)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
+            "higher_is_better": False, "steps": args.steps, "result": list(np.asarray(r.values))}
+
+
+def bench_c4(args):
+    """C4: pathfinder batched BP calibration (min-fill JT), 4 leaf findings per row."""
+    import torch
+
+    from pgmpy_amd.inference.bp_batch import BatchedJunctionTree
+    from pgmpy_amd.inference.EliminationOrder import junction_tree_from_model
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("pathfinder")
+    jt = junction_tree_from_model(m)
+    bjt = BatchedJunctionTree(jt)
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    n = args.rows
+    codes, nodes = forward_sample_codes(m, n, seed=7)
+    rng = np.random.default_rng(7)
+    ev_vars = leaves
+    ev = np.full((len(ev_vars), n), 255, dtype=np.uint8)
+    for r in range(n):
+        pick = rng.choice(len(ev_vars), size=4, replace=False)
+        for j in pick:
+            ev[j, r] = codes[nodes.index(ev_vars[j]), r]
+    d = upload_codes(ev)
+    for _ in range(args.warmup):
+        bjt.calibrate_codes(d, ev_vars, n)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cal = bjt.calibrate_codes(d, ev_vars, n)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    bpc = bjt.bytes_per_calibration()
+    return {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
+            "rows_per_step": n, "ms_per_step": dt * 1e3, "bytes_per_calibration": bpc,
+            "achieved_GBps": bpc * n / dt / 1e9, "cliques": len(bjt.cliques)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="after timing, gather marginals to rank 0 (RCCL)")
+    args = ap.parse_args()
+    if args.rows is None:
+        args.rows = 100_000 if args.workload == "c3" else 1000
+    from pgmpy_amd.build import build
+
+    build(verbose=False)
+    dist, rank, world = dist_setup(args.gpus)
+    if args.workload == "c3":
+        res = bench_c3(args, dist, rank, world)
+    elif args.workload == "c2":
+        res = bench_c2(args)
+    else:
+        res = bench_c4(args)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,42 @@
+"""Vectorised forward sampling of evidence rows (host-side synthetic-input generator).
+
+Equivalent in distribution to pgmpy's BayesianModelSampling.forward_sample
+(pgmpy/sampling/Sampling.py:30-): ancestral sampling in topological order,
+each variable drawn from its CPT column selected by the sampled parent states.
+Used by bench.py to build the seeded synthetic evidence batches of SURVEY.md
+§8(d) C3/C5; not part of the accelerated path (and it does not reproduce
+pgmpy's RNG stream, so the rows differ from pgmpy's for the same seed).
+"""
+import networkx as nx
+import numpy as np
+
+
+def forward_sample_codes(model, n, seed=42, order=None):
+    """[n_nodes, n] uint8 state codes, rows = nodes in `order` (default sorted(model.nodes()))."""
+    rng = np.random.default_rng(seed)
+    nodes = sorted(model.nodes()) if order is None else list(order)
+    idx = {v: i for i, v in enumerate(nodes)}
+    codes = np.empty((len(nodes), n), dtype=np.uint8)
+    for v in nx.topological_sort(model):
+        cpd = model.get_cpds(v)
+        card = int(cpd.cardinality[0])
+        table = np.asarray(cpd.values, dtype=np.float64).reshape(card, -1)  # (card, prod parent cards)
+        parents = list(cpd.variables[1:])
+        col = np.zeros(n, dtype=np.int64)
+        for p, pc in zip(parents, cpd.cardinality[1:]):
+            col = col * int(pc) + codes[idx[p]].astype(np.int64)
+        cdf = np.cumsum(table, axis=0)  # (card, cols)
+        cdf /= cdf[-1:, :]
+        u = rng.random(n)
+        c = (u[None, :] > cdf[:, col]).sum(axis=0)
+        codes[idx[v]] = np.minimum(c, card - 1).astype(np.uint8)
+    return codes, nodes
+
+
+def codes_to_frame(model, codes, nodes, columns=None):
+    import pandas as pd
+
+    states = model.states
+    columns = nodes if columns is None else columns
+    pos = {v: i for i, v in enumerate(nodes)}
+    return pd.DataFrame({c: np.asarray(states[c], dtype=object)[codes[pos[c]]] for c in columns})
