@@ -140,39 +140,61 @@ int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *ou
 /* ---------------------------------------------------------------- argmax
  * First-flat-index argmax per row (np.argmax semantics incl. NaN-first):
  * replaces compat_fns.argmax (compat_fns.py:70-74) in map_query
- * (ExactInference.py:616).  out_idx[r] = argmax_i X[r*s_row + i*s_elem]. */
+ * (ExactInference.py:616).  idx[r] = argmax_i X[r*s_row + i*s_elem], written to
+ * out_idx (int64) and/or out_idx32 (int32); either may be NULL. */
 int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem,
-               int64_t *out_idx, void *stream);
+               int64_t *out_idx, int32_t *out_idx32, void *stream);
 
 /* ---------------------------------------------------------------- fused row plan
  * The batched-evidence hot path (DiscreteBayesianNetwork.predict /
- * predict_probability, DiscreteBayesianNetwork.py:731-989): per evidence row,
- * the whole reduce -> sum-product -> normalize -> marginalize/argmax chain of
- * one evidence pattern in ONE kernel, one lane per row, CPT slices staged in
- * LDS, no HBM intermediates.  Loop space = query dims (first n_query) then
- * hidden dims (summed).  Factor f's value for a loop point is
- *   values[fac_base[f] + sum_j code_j(row) * ev_stride_j + sum_k digit_k * fac_stride[f][k]].
+ * predict_probability, DiscreteBayesianNetwork.py:731-989; the per-row
+ * VariableElimination.query / map_query of ExactInference.py:246-624): per
+ * evidence row, the whole reduce -> sum-product -> normalize ->
+ * marginalize/argmax chain of one evidence pattern in ONE kernel, one lane per
+ * row, CPT values staged in LDS, no HBM intermediates.
+ *
+ * After evidence reduction the factor graph over the unobserved variables splits
+ * into independent COMPONENTS; each is summed over its own (query x hidden)
+ * index space, so the joint is never expanded across components.  Loop dims are
+ * grouped per component: [comp_loop_begin, +comp_n_query) are query dims,
+ * [.., comp_loop_end) hidden (summed) dims.  Factor f (in component c, factors
+ * of c are [comp_fac_begin, comp_fac_end)) evaluated at a loop point is
+ *   values[fac_base[f] + sum_j code_j(row) * ev_stride_j + sum_k digit_k * fac_stride[f][k]]
+ * Outputs follow the reference exactly: marginal = component marginal / its
+ * mass; if the product of all component masses is 0 (impossible evidence) every
+ * marginal is NaN (0/0 of DiscreteFactor.normalize, DiscreteFactor.py:530) and the
+ * MAP index is 0 (np.argmax of an all-NaN joint).
  */
 #define PGM_ROWS_MAX_LOOP 12
 #define PGM_ROWS_MAX_FAC 16
 #define PGM_ROWS_MAX_EV 48
-#define PGM_ROWS_MAX_ACC 192
+#define PGM_ROWS_MAX_COMP 12
+#define PGM_ROWS_MAX_MARG 192
 
 enum pgm_rows_mode {
   PGM_ROWS_MARGINALS = 1, /* per query var normalized marginal (predict_probability) */
-  PGM_ROWS_JOINT = 2,     /* normalized joint over the query dims (query joint=True) */
+  PGM_ROWS_JOINT = 2,     /* normalized joint over the query dims (query joint=True); n_comp == 1 only */
   PGM_ROWS_MAP = 4,       /* first-index argmax of the joint (map_query / predict)  */
-  PGM_ROWS_MAPGAP = 8     /* also (best - second best) / best, for tie screening      */
+  PGM_ROWS_MAPGAP = 8     /* also (best - second best) / best of the joint, for tie screening */
 };
 
 typedef struct {
   int32_t n_loop;
-  int32_t n_query;
+  int32_t n_query;  /* total query dims */
   int32_t n_fac;
   int32_t n_ev;
   int32_t n_values; /* packed CPT values (doubles) */
-  int32_t _pad[3];
+  int32_t n_comp;
+  int32_t n_marg;   /* rows of the marginal output = sum of query cardinalities */
+  int32_t n_joint;  /* entries of the joint = prod of query cardinalities */
   int32_t loop_card[PGM_ROWS_MAX_LOOP];
+  int32_t loop_marg_off[PGM_ROWS_MAX_LOOP];   /* query dim: first marginal row of its variable (-1 hidden) */
+  int32_t loop_map_stride[PGM_ROWS_MAX_LOOP]; /* query dim: stride in the flat joint / MAP index (0 hidden) */
+  int32_t comp_loop_begin[PGM_ROWS_MAX_COMP];
+  int32_t comp_n_query[PGM_ROWS_MAX_COMP];
+  int32_t comp_loop_end[PGM_ROWS_MAX_COMP];
+  int32_t comp_fac_begin[PGM_ROWS_MAX_COMP];
+  int32_t comp_fac_end[PGM_ROWS_MAX_COMP];
   int32_t fac_base[PGM_ROWS_MAX_FAC];
   int32_t fac_stride[PGM_ROWS_MAX_FAC][PGM_ROWS_MAX_LOOP];
   int32_t fac_ev_begin[PGM_ROWS_MAX_FAC]; /* evidence terms of factor f: [begin, end) */
@@ -184,8 +206,9 @@ typedef struct {
 
 int pgm_rows_plan_create(const pgm_rows_plan *plan, const double *host_values, void **handle);
 int pgm_rows_plan_destroy(void *handle);
-/* outputs are column-major with leading dim ld_out (>= n_rows), any may be NULL unless its mode bit is set:
- *   marg  [sum_q card_q][ld_out]   joint [prod_q card_q][ld_out]   map [n_rows] int32   gap [n_rows] */
+/* Rows [row0, row0 + n_rows) of codes.  Outputs are column-major with leading dim ld_out (>= n_rows) and
+ * row r written at column r (not row0 + r); any may be NULL unless its mode bit is set:
+ *   marg [n_marg][ld_out] f64   joint [n_joint][ld_out] f64   map [n_rows] int32   gap [n_rows] f64 */
 int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
                       int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map,
                       double *gap, int32_t *err_flag, void *stream);

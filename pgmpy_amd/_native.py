@@ -32,7 +32,8 @@ RED_NONE, RED_SUM, RED_MAX = 0, 1, 2
 ROWS_MAX_LOOP = 12
 ROWS_MAX_FAC = 16
 ROWS_MAX_EV = 48
-ROWS_MAX_ACC = 192
+ROWS_MAX_COMP = 12
+ROWS_MAX_MARG = 192
 ROWS_MARGINALS, ROWS_JOINT, ROWS_MAP, ROWS_MAPGAP = 1, 2, 4, 8
 
 
@@ -83,8 +84,17 @@ class RowsPlan(ctypes.Structure):
         ("n_fac", ctypes.c_int32),
         ("n_ev", ctypes.c_int32),
         ("n_values", ctypes.c_int32),
-        ("_pad", ctypes.c_int32 * 3),
+        ("n_comp", ctypes.c_int32),
+        ("n_marg", ctypes.c_int32),
+        ("n_joint", ctypes.c_int32),
         ("loop_card", ctypes.c_int32 * ROWS_MAX_LOOP),
+        ("loop_marg_off", ctypes.c_int32 * ROWS_MAX_LOOP),
+        ("loop_map_stride", ctypes.c_int32 * ROWS_MAX_LOOP),
+        ("comp_loop_begin", ctypes.c_int32 * ROWS_MAX_COMP),
+        ("comp_n_query", ctypes.c_int32 * ROWS_MAX_COMP),
+        ("comp_loop_end", ctypes.c_int32 * ROWS_MAX_COMP),
+        ("comp_fac_begin", ctypes.c_int32 * ROWS_MAX_COMP),
+        ("comp_fac_end", ctypes.c_int32 * ROWS_MAX_COMP),
         ("fac_base", ctypes.c_int32 * ROWS_MAX_FAC),
         ("fac_stride", (ctypes.c_int32 * ROWS_MAX_LOOP) * ROWS_MAX_FAC),
         ("fac_ev_begin", ctypes.c_int32 * ROWS_MAX_FAC),
@@ -117,7 +127,7 @@ _SIGS = {
     "pgm_gather": ([ctypes.POINTER(GatherDesc), _P, _P, _P, _P, _P], ctypes.c_int),
     "pgm_indicator": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P],
                       ctypes.c_int),
-    "pgm_argmax": ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P], ctypes.c_int),
+    "pgm_argmax": ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P, _P], ctypes.c_int),
     "pgm_rows_plan_create": ([ctypes.POINTER(RowsPlan), _P, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_rows_plan_destroy": ([_P], ctypes.c_int),
     "pgm_rows_plan_run": ([_P, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P,

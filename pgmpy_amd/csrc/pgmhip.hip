@@ -24,7 +24,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 1
+#define PGM_ABI_VERSION 2
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -388,7 +388,7 @@ __device__ __forceinline__ bool am_better(double v, uint32_t i, double bv, uint3
 
 __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, uint64_t n_rows, uint32_t row_len,
                                                 int64_t s_row, int64_t s_elem, int g_log2,
-                                                int64_t *__restrict__ out) {
+                                                int64_t *__restrict__ out, int32_t *__restrict__ out32) {
   const uint32_t G = 1u << g_log2;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane_g = (uint32_t)tid & (G - 1);
@@ -411,30 +411,40 @@ __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, ui
         bi = oi;
       }
     }
-    if (lane_g == 0) out[r] = (bi == 0xffffffffu) ? 0 : (int64_t)bi;
+    if (lane_g == 0) {
+      const int64_t v = (bi == 0xffffffffu) ? 0 : (int64_t)bi;
+      if (out) out[r] = v;
+      if (out32) out32[r] = (int32_t)v;
+    }
   }
 }
 
 // ----------------------------------------------------------------------------- fused row plan
 struct RowsK {
   int32_t n_loop, n_query, n_fac, n_ev;
-  int32_t n_values, n_acc, vals_lds, acc_lds;
-  uint32_t P, H;  // query space, hidden space sizes
+  int32_t n_values, n_marg, n_joint, n_comp;
+  int32_t vals_lds, acc_lds, _pad0, _pad1;
   int32_t loop_card[PGM_ROWS_MAX_LOOP];
+  int32_t loop_marg_off[PGM_ROWS_MAX_LOOP];
+  int32_t map_inc[PGM_ROWS_MAX_LOOP];  // change of the flat MAP index when query dim k advances
+  int32_t inc[PGM_ROWS_MAX_LOOP][PGM_ROWS_MAX_FAC];  // factor offset change when loop dim k advances
+  int32_t hspan[PGM_ROWS_MAX_FAC];  // sum over the factor's hidden dims of (card-1)*stride (undone on a wrap)
+  int32_t comp_lb[PGM_ROWS_MAX_COMP], comp_nq[PGM_ROWS_MAX_COMP], comp_le[PGM_ROWS_MAX_COMP];
+  int32_t comp_fb[PGM_ROWS_MAX_COMP], comp_fe[PGM_ROWS_MAX_COMP];
+  uint32_t comp_P[PGM_ROWS_MAX_COMP], comp_H[PGM_ROWS_MAX_COMP];
   int32_t fac_base[PGM_ROWS_MAX_FAC];
-  int32_t inc[PGM_ROWS_MAX_LOOP][PGM_ROWS_MAX_FAC];  // offset increment when loop dim k advances
   int32_t fac_ev_begin[PGM_ROWS_MAX_FAC], fac_ev_end[PGM_ROWS_MAX_FAC];
   int32_t ev_col[PGM_ROWS_MAX_EV], ev_stride[PGM_ROWS_MAX_EV], ev_card[PGM_ROWS_MAX_EV];
-  int32_t acc_off[PGM_ROWS_MAX_LOOP];
-  int32_t hspan[PGM_ROWS_MAX_FAC];  // sum over hidden dims of (card-1)*stride: undone on a full hidden wrap
 };
 
 struct RowsHandle {
   RowsK k;
   double *d_values;
-  int device;
 };
 
+// One lane per evidence row.  Everything that does not depend on the row (loop digits, factor
+// offsets, component bounds) is wave-uniform and lives in scalar registers; per lane there are only
+// the evidence bases of the factors, the running products and the marginal accumulators (LDS).
 template <int MAXF>
 __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__restrict__ gvals,
                                               const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0,
@@ -443,8 +453,8 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
                                               int32_t *__restrict__ map, double *__restrict__ gap,
                                               int32_t *__restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  double *svals = lds;                                   // [n_values] when vals_lds
-  double *sacc = lds + (p.vals_lds ? ((p.n_values + 1) & ~1) : 0);  // [n_acc][blockDim] when acc_lds
+  double *svals = lds;
+  double *sacc = lds + (p.vals_lds ? ((p.n_values + 1) & ~1) : 0);
   if (p.vals_lds) {
     for (int i = threadIdx.x; i < p.n_values; i += blockDim.x) svals[i] = gvals[i];
     __syncthreads();
@@ -455,8 +465,8 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
   const int nb = blockDim.x;
   const int lane = threadIdx.x;
 
-  // evidence part of every factor's offset (per row)
   int32_t base[MAXF];
+  bool bad = false;
 #pragma unroll
   for (int f = 0; f < MAXF; ++f) {
     base[f] = 0;
@@ -465,7 +475,7 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
       for (int j = p.fac_ev_begin[f]; j < p.fac_ev_end[f]; ++j) {
         uint32_t c = codes[(int64_t)p.ev_col[j] * ld_codes + row0 + r];
         if (c >= (uint32_t)p.ev_card[j]) {
-          if (err) atomicOr(err, 1);
+          bad = true;
           c = 0;
         }
         b += (int32_t)c * p.ev_stride[j];
@@ -473,95 +483,125 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
       base[f] = b;
     }
   }
+  if (bad && err) atomicOr(err, 1);
   const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
   const bool do_joint = (mode & PGM_ROWS_JOINT) != 0;
   const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
   double *acc_row = p.acc_lds ? (sacc + lane) : (marg + r);
   const int64_t acc_stride = p.acc_lds ? nb : ld_out;
-  if (do_marg)
-    for (int a = 0; a < p.n_acc; ++a) acc_row[a * acc_stride] = 0.0;
 
-  // uniform odometer state (identical across lanes -> scalar registers); all array indices are
-  // compile-time constants after unrolling so nothing spills to scratch
-  int32_t off[MAXF];
+  double zprod = 1.0, min_gap = 1.0;
+  int32_t map_idx = 0;
+  for (int c = 0; c < p.n_comp; ++c) {
+    const int lb = p.comp_lb[c], nqe = lb + p.comp_nq[c], le = p.comp_le[c];
+    const int fb = p.comp_fb[c], fe = p.comp_fe[c];
+    int32_t off[MAXF];
 #pragma unroll
-  for (int f = 0; f < MAXF; ++f) off[f] = 0;
-  int32_t dig[PGM_ROWS_MAX_LOOP];
+    for (int f = 0; f < MAXF; ++f) off[f] = 0;
+    int32_t dig[PGM_ROWS_MAX_LOOP];
 #pragma unroll
-  for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k) dig[k] = 0;
-
-  double z = 0.0, best = -1.0, second = -1.0;
-  uint32_t best_i = 0;
-  const int nq = p.n_query, nl = p.n_loop;
-  for (uint32_t qi = 0; qi < p.P; ++qi) {
-    double v = 0.0;
-    for (uint32_t hi = 0; hi < p.H; ++hi) {
-      double prod = 1.0;
+    for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k) dig[k] = 0;
+    if (do_marg) {
 #pragma unroll
-      for (int f = 0; f < MAXF; ++f)
-        if (f < p.n_fac) prod *= V[base[f] + off[f]];
-      v += prod;
-      // advance the hidden odometer (dims nq .. nl-1, innermost last)
-      bool carry = true;
+      for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
+        if (k >= lb && k < nqe)
+          for (int s = 0; s < p.loop_card[k]; ++s) acc_row[(p.loop_marg_off[k] + s) * acc_stride] = 0.0;
+    }
+    double mass = 0.0, best = -1.0, second = -1.0;
+    int32_t cur_map = 0, best_map = 0;
+    for (uint32_t qi = 0; qi < p.comp_P[c]; ++qi) {
+      double v = 0.0;
+      for (uint32_t hi = 0; hi < p.comp_H[c]; ++hi) {
+        double prod = 1.0;
+#pragma unroll
+        for (int f = 0; f < MAXF; ++f)
+          if (f >= fb && f < fe) prod *= V[base[f] + off[f]];
+        v += prod;
+        bool carry = true;  // hidden odometer: dims [nqe, le), innermost last
+#pragma unroll
+        for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
+          if (carry && k >= nqe && k < le) {
+            if (++dig[k] < p.loop_card[k]) {
+#pragma unroll
+              for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
+              carry = false;
+            } else {
+              dig[k] = 0;
+            }
+          }
+        }
+        if (carry) {
+#pragma unroll
+          for (int f = 0; f < MAXF; ++f)
+            if (f >= fb && f < fe) off[f] -= p.hspan[f];
+        }
+      }
+      mass += v;
+      if (do_marg) {
+#pragma unroll
+        for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
+          if (k >= lb && k < nqe) acc_row[(p.loop_marg_off[k] + dig[k]) * acc_stride] += v;
+      }
+      if (do_joint) joint[(int64_t)cur_map * ld_out + r] = v;
+      if (do_map) {
+        if (v > best) {
+          second = best;
+          best = v;
+          best_map = cur_map;
+        } else if (v > second) {
+          second = v;
+        }
+      }
+      bool carry = true;  // query odometer: dims [lb, nqe)
 #pragma unroll
       for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
-        if (carry && k >= nq && k < nl) {
+        if (carry && k >= lb && k < nqe) {
           if (++dig[k] < p.loop_card[k]) {
 #pragma unroll
             for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
+            cur_map += p.map_inc[k];
             carry = false;
           } else {
             dig[k] = 0;
           }
         }
       }
-      if (carry) {  // full wrap of the hidden space: digits are back to 0, drop their offsets
-#pragma unroll
-        for (int f = 0; f < MAXF; ++f) off[f] -= p.hspan[f];
-      }
     }
-    z += v;
-    if (do_marg) {
+    zprod *= mass;
+    if (do_marg) {  // component marginals normalised by the component mass
+      const double inv = 1.0 / mass;
 #pragma unroll
-      for (int i = 0; i < PGM_ROWS_MAX_LOOP; ++i)
-        if (i < nq) acc_row[(p.acc_off[i] + dig[i]) * acc_stride] += v;
+      for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
+        if (k >= lb && k < nqe)
+          for (int s = 0; s < p.loop_card[k]; ++s) acc_row[(p.loop_marg_off[k] + s) * acc_stride] *= inv;
     }
-    if (do_joint) joint[(int64_t)qi * ld_out + r] = v;
     if (do_map) {
-      if (v > best) {
-        second = best;
-        best = v;
-        best_i = qi;
-      } else if (v > second) {
-        second = v;
-      }
-    }
-    // advance the query odometer (dims 0 .. nq-1)
-    bool carry = true;
-#pragma unroll
-    for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
-      if (carry && k < nq) {
-        if (++dig[k] < p.loop_card[k]) {
-#pragma unroll
-          for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
-          carry = false;
-        } else {
-          dig[k] = 0;
-        }
+      map_idx += best_map;
+      if (p.comp_P[c] > 1) {
+        const double g = best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0;
+        min_gap = fmin(min_gap, g);
       }
     }
   }
+  // impossible evidence (zero total mass): every marginal is 0/0 = NaN and np.argmax gives 0
+  const bool dead = !(zprod > 0.0);
   if (do_marg) {
-    for (int a = 0; a < p.n_acc; ++a) {
-      const double m = acc_row[a * acc_stride] / z;  // 0/0 = NaN on impossible evidence, as normalize
+    const double nan = __builtin_nan("");
+    for (int a = 0; a < p.n_marg; ++a) {
+      const double m = dead ? nan : acc_row[a * acc_stride];
       marg[(int64_t)a * ld_out + r] = m;
     }
   }
-  if (do_joint)
-    for (uint32_t qi = 0; qi < p.P; ++qi) joint[(int64_t)qi * ld_out + r] /= z;
+  if (do_joint) {
+    const double inv = 1.0 / zprod;
+    for (int q = 0; q < p.n_joint; ++q) {
+      double* j = joint + (int64_t)q * ld_out + r;
+      *j = dead ? __builtin_nan("") : *j * inv;
+    }
+  }
   if (do_map) {
-    if (map) map[r] = (int32_t)best_i;
-    if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0;
+    if (map) map[r] = dead ? 0 : map_idx;
+    if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : min_gap;
   }
 }
 
@@ -744,8 +784,8 @@ int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *ou
 }
 
 int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem, int64_t *out_idx,
-               void *stream) {
-  if (!X || !out_idx) return fail(PGM_EINVAL, "argmax: null argument");
+               int32_t *out_idx32, void *stream) {
+  if (!X || (!out_idx && !out_idx32)) return fail(PGM_EINVAL, "argmax: null argument");
   if (n_rows <= 0) return PGM_OK;
   if (row_len <= 0) return fail(PGM_EINVAL, "argmax: empty rows (np.argmax of an empty sequence)");
   if (row_len >= (1ll << 31)) return fail(PGM_EINVAL, "argmax: row too long");
@@ -754,7 +794,7 @@ int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, 
   uint64_t threads = (uint64_t)n_rows << g;
   uint64_t blocks = std::min<uint64_t>((threads + 255) / 256, 65535);
   hipLaunchKernelGGL(k_argmax, dim3((unsigned)blocks), dim3(256), 0, S(stream), X, (uint64_t)n_rows,
-                     (uint32_t)row_len, s_row, s_elem, g, out_idx);
+                     (uint32_t)row_len, s_row, s_elem, g, out_idx, out_idx32);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }
@@ -764,9 +804,10 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   *handle = nullptr;
   if (pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP || pl->n_query < 0 || pl->n_query > pl->n_loop ||
       pl->n_fac < 0 || pl->n_fac > PGM_ROWS_MAX_FAC || pl->n_ev < 0 || pl->n_ev > PGM_ROWS_MAX_EV ||
-      pl->n_values < 0)
-    return fail(PGM_EINVAL, "rows_plan_create: plan out of range (loop %d query %d fac %d ev %d)", pl->n_loop,
-                pl->n_query, pl->n_fac, pl->n_ev);
+      pl->n_values < 0 || pl->n_comp < 0 || pl->n_comp > PGM_ROWS_MAX_COMP || pl->n_marg < 0 ||
+      pl->n_marg > PGM_ROWS_MAX_MARG)
+    return fail(PGM_EINVAL, "rows_plan_create: plan out of range (loop %d query %d fac %d ev %d comp %d marg %d)",
+                pl->n_loop, pl->n_query, pl->n_fac, pl->n_ev, pl->n_comp, pl->n_marg);
   RowsK k;
   memset(&k, 0, sizeof k);
   k.n_loop = pl->n_loop;
@@ -774,47 +815,76 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   k.n_fac = pl->n_fac;
   k.n_ev = pl->n_ev;
   k.n_values = pl->n_values;
-  uint64_t P = 1, H = 1;
-  int n_acc = 0;
-  for (int i = 0; i < pl->n_loop; ++i) {
-    if (pl->loop_card[i] <= 0) return fail(PGM_EINVAL, "rows_plan_create: loop_card[%d] <= 0", i);
-    k.loop_card[i] = pl->loop_card[i];
-    if (i < pl->n_query) {
-      P *= pl->loop_card[i];
-      k.acc_off[i] = n_acc;
-      n_acc += pl->loop_card[i];
-    } else {
-      H *= pl->loop_card[i];
+  k.n_marg = pl->n_marg;
+  k.n_joint = pl->n_joint;
+  k.n_comp = pl->n_comp;
+  int covered_loop = 0, covered_fac = 0, nq_total = 0;
+  for (int c = 0; c < pl->n_comp; ++c) {
+    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c], le = pl->comp_loop_end[c];
+    const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
+    if (lb != covered_loop || nq < 0 || lb + nq > le || le > pl->n_loop || fb != covered_fac || fe < fb ||
+        fe > pl->n_fac)
+      return fail(PGM_EINVAL, "rows_plan_create: component %d ranges (loops [%d,%d,%d) factors [%d,%d))", c, lb,
+                  lb + nq, le, fb, fe);
+    covered_loop = le;
+    covered_fac = fe;
+    nq_total += nq;
+    uint64_t P = 1, H = 1;
+    for (int kk = lb; kk < le; ++kk) {
+      if (pl->loop_card[kk] <= 0) return fail(PGM_EINVAL, "rows_plan_create: loop_card[%d] <= 0", kk);
+      (kk < lb + nq ? P : H) *= (uint64_t)pl->loop_card[kk];
+    }
+    if (P * H >= (1ull << 31)) return fail(PGM_EINVAL, "rows_plan_create: component %d space too large", c);
+    k.comp_lb[c] = lb;
+    k.comp_nq[c] = nq;
+    k.comp_le[c] = le;
+    k.comp_fb[c] = fb;
+    k.comp_fe[c] = fe;
+    k.comp_P[c] = (uint32_t)P;
+    k.comp_H[c] = (uint32_t)H;
+    for (int kk = lb; kk < le; ++kk) {
+      const bool q = kk < lb + nq;
+      const int end = q ? lb + nq : le;  // odometer group of dim kk
+      int64_t mi = 0;
+      if (q) {
+        if (pl->loop_marg_off[kk] < 0 || pl->loop_marg_off[kk] + pl->loop_card[kk] > pl->n_marg)
+          return fail(PGM_EINVAL, "rows_plan_create: loop %d marginal rows out of range", kk);
+        mi = pl->loop_map_stride[kk];
+        for (int k2 = kk + 1; k2 < end; ++k2) mi -= (int64_t)(pl->loop_card[k2] - 1) * pl->loop_map_stride[k2];
+      }
+      k.map_inc[kk] = (int32_t)mi;
+      for (int f = fb; f < fe; ++f) {
+        int64_t inc = pl->fac_stride[f][kk];
+        for (int k2 = kk + 1; k2 < end; ++k2) inc -= (int64_t)(pl->loop_card[k2] - 1) * pl->fac_stride[f][k2];
+        k.inc[kk][f] = (int32_t)inc;
+      }
+    }
+    for (int f = fb; f < fe; ++f) {
+      int64_t hs = 0;
+      for (int kk = lb + nq; kk < le; ++kk) hs += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
+      k.hspan[f] = (int32_t)hs;
+      for (int kk = 0; kk < pl->n_loop; ++kk)
+        if ((kk < lb || kk >= le) && pl->fac_stride[f][kk] != 0)
+          return fail(PGM_EINVAL, "rows_plan_create: factor %d strides a loop dim outside its component", f);
     }
   }
-  if (P * H >= (1ull << 31)) return fail(PGM_EINVAL, "rows_plan_create: loop space too large");
-  if (n_acc > PGM_ROWS_MAX_ACC) return fail(PGM_EINVAL, "rows_plan_create: %d marginal entries (limit %d)", n_acc,
-                                            PGM_ROWS_MAX_ACC);
-  k.P = (uint32_t)P;
-  k.H = (uint32_t)H;
-  k.n_acc = n_acc;
+  if (covered_loop != pl->n_loop || covered_fac != pl->n_fac || nq_total != pl->n_query)
+    return fail(PGM_EINVAL, "rows_plan_create: components do not cover the loop dims / factors");
+  for (int kk = 0; kk < pl->n_loop; ++kk) {
+    k.loop_card[kk] = pl->loop_card[kk];
+    k.loop_marg_off[kk] = pl->loop_marg_off[kk];
+  }
   for (int f = 0; f < pl->n_fac; ++f) {
     k.fac_base[f] = pl->fac_base[f];
     k.fac_ev_begin[f] = pl->fac_ev_begin[f];
     k.fac_ev_end[f] = pl->fac_ev_end[f];
     if (pl->fac_ev_begin[f] < 0 || pl->fac_ev_end[f] > pl->n_ev || pl->fac_ev_begin[f] > pl->fac_ev_end[f])
       return fail(PGM_EINVAL, "rows_plan_create: factor %d evidence range", f);
-    // odometer increments: advancing dim k resets every deeper dim of the SAME odometer
-    // (query dims [0,nq) and hidden dims [nq,nl) are two separate odometers)
-    for (int kk = 0; kk < pl->n_loop; ++kk) {
-      const int end = kk < pl->n_query ? pl->n_query : pl->n_loop;
-      int64_t inc = pl->fac_stride[f][kk];
-      for (int k2 = kk + 1; k2 < end; ++k2) inc -= (int64_t)(pl->loop_card[k2] - 1) * pl->fac_stride[f][k2];
-      k.inc[kk][f] = (int32_t)inc;
-    }
-    int64_t hs = 0;
-    for (int kk = pl->n_query; kk < pl->n_loop; ++kk) hs += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
-    k.hspan[f] = (int32_t)hs;
-    // bounds: max offset must stay inside values
     int64_t mx = pl->fac_base[f];
     for (int kk = 0; kk < pl->n_loop; ++kk) mx += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
     for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) mx += (int64_t)(pl->ev_card[j] - 1) * pl->ev_stride[j];
-    if (mx >= pl->n_values || pl->fac_base[f] < 0) return fail(PGM_EINVAL, "rows_plan_create: factor %d reads past values", f);
+    if (mx >= pl->n_values || pl->fac_base[f] < 0)
+      return fail(PGM_EINVAL, "rows_plan_create: factor %d reads past values", f);
   }
   for (int j = 0; j < pl->n_ev; ++j) {
     k.ev_col[j] = pl->ev_col[j];
@@ -825,13 +895,12 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   if (!h) return fail(PGM_ENOMEM, "rows_plan_create: host allocation");
   h->k = k;
   h->d_values = nullptr;
-  hipGetDevice(&h->device);
   if (pl->n_values > 0) {
     hipError_t e = hipMalloc((void **)&h->d_values, sizeof(double) * pl->n_values);
     if (e == hipSuccess) e = hipMemcpy(h->d_values, host_values, sizeof(double) * pl->n_values, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      if (h->d_values) hipFree(h->d_values);
+      if (h->d_values) (void)hipFree(h->d_values);
       delete h;
       return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_plan_create: %s", hipGetErrorString(e));
     }
@@ -843,7 +912,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
 int pgm_rows_plan_destroy(void *handle) {
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
-  if (h->d_values) hipFree(h->d_values);
+  if (h->d_values) (void)hipFree(h->d_values);
   delete h;
   return PGM_OK;
 }
@@ -857,12 +926,14 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   if (h->k.n_ev > 0 && !codes) return fail(PGM_EINVAL, "rows_plan_run: null codes");
   if ((mode & PGM_ROWS_MARGINALS) && !marg) return fail(PGM_EINVAL, "rows_plan_run: marginals requested, marg is null");
   if ((mode & PGM_ROWS_JOINT) && !joint) return fail(PGM_EINVAL, "rows_plan_run: joint requested, joint is null");
+  if ((mode & PGM_ROWS_JOINT) && h->k.n_comp != 1)
+    return fail(PGM_EINVAL, "rows_plan_run: joint output needs a single-component plan");
   if ((mode & PGM_ROWS_MAP) && !map) return fail(PGM_EINVAL, "rows_plan_run: MAP requested, map is null");
   if ((mode & PGM_ROWS_MAPGAP) && !gap) return fail(PGM_EINVAL, "rows_plan_run: MAP gap requested, gap is null");
   if ((mode & (PGM_ROWS_MARGINALS | PGM_ROWS_JOINT)) && ld_out < n_rows)
     return fail(PGM_EINVAL, "rows_plan_run: ld_out %lld < n_rows %lld", (long long)ld_out, (long long)n_rows);
   RowsK k = h->k;
-  // LDS budget: CPT values (if they fit) + per-lane marginal accumulators
+  // LDS: CPT values (if they fit) + per-lane marginal accumulators
   const size_t kLds = 64 * 1024;
   size_t vals_bytes = (size_t)((k.n_values + 1) & ~1) * sizeof(double);
   k.vals_lds = vals_bytes <= 48 * 1024 ? 1 : 0;
@@ -870,11 +941,11 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   int block = 256;
   k.acc_lds = 0;
   if (mode & PGM_ROWS_MARGINALS) {
-    while (block > 64 && vals_bytes + (size_t)k.n_acc * block * sizeof(double) > kLds) block >>= 1;
-    k.acc_lds = vals_bytes + (size_t)k.n_acc * block * sizeof(double) <= kLds ? 1 : 0;
+    while (block > 64 && vals_bytes + (size_t)k.n_marg * block * sizeof(double) > kLds) block >>= 1;
+    k.acc_lds = vals_bytes + (size_t)k.n_marg * block * sizeof(double) <= kLds ? 1 : 0;
     if (!k.acc_lds) block = 256;
   }
-  size_t lds = vals_bytes + (k.acc_lds ? (size_t)k.n_acc * block * sizeof(double) : 0);
+  size_t lds = vals_bytes + (k.acc_lds ? (size_t)k.n_marg * block * sizeof(double) : 0);
   uint64_t blocks = ((uint64_t)n_rows + block - 1) / block;
   if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
   hipLaunchKernelGGL((k_rows<PGM_ROWS_MAX_FAC>), dim3((unsigned)blocks), dim3(block), lds, S(stream), k,

@@ -167,14 +167,14 @@ def argmax_rows(A, la, row_label=None):
         X = A if A.is_contiguous() else copy(A)
         out = torch.empty(1, dtype=torch.int64, device=X.device)
         n = X.numel()
-        N.check(L.pgm_argmax(N.ptr(X), 1, n, n, 1, N.ptr(out), N.stream_handle()), "argmax")
+        N.check(L.pgm_argmax(N.ptr(X), 1, n, n, 1, N.ptr(out), None, N.stream_handle()), "argmax")
         return out
     other = [l for l in la if l != row_label]
     X = contract(A, la, None, None, [row_label] + other, combine="copy")
     n_rows = X.shape[0]
     row_len = int(np.prod(X.shape[1:])) if X.dim() > 1 else 1
     out = torch.empty(n_rows, dtype=torch.int64, device=X.device)
-    N.check(L.pgm_argmax(N.ptr(X), n_rows, row_len, row_len, 1, N.ptr(out), N.stream_handle()), "argmax")
+    N.check(L.pgm_argmax(N.ptr(X), n_rows, row_len, row_len, 1, N.ptr(out), None, N.stream_handle()), "argmax")
     return out
 
 

@@ -77,58 +77,135 @@ class PatternPlan:
         self.card = card
         self.H = int(np.prod([card[v] for v in hidden])) if hidden else 1
         n_ev_terms = sum(1 for vars_, _ in factors for v in vars_ if v in ev_set)
+        comps = self.components()
+        comp_space = max((int(np.prod([card[v] for v in q + h])) for q, h, _ in comps), default=1)
         fused_ok = (len(factors) <= N.ROWS_MAX_FAC and len(self.variables) + len(hidden) <= N.ROWS_MAX_LOOP
-                    and n_ev_terms <= N.ROWS_MAX_EV and self.n_acc <= N.ROWS_MAX_ACC
-                    and self.P * self.H <= FUSED_MAX_SPACE)
+                    and n_ev_terms <= N.ROWS_MAX_EV and self.n_acc <= N.ROWS_MAX_MARG
+                    and len(comps) <= N.ROWS_MAX_COMP and comp_space <= FUSED_MAX_SPACE)
+        self.joint_fused_ok = fused_ok and self.P * self.H <= FUSED_MAX_SPACE
         self.kind = force or ("fused" if fused_ok else "steps")
         if self.kind == "fused" and not fused_ok:
             raise ValueError("pattern does not fit the fused row kernel")
         self._handle = None
-        if self.kind == "fused":
-            self._build_fused()
+        self._handle_joint = None
+        self.n_comp = len(comps) if self.kind == "fused" else None
 
     # ------------------------------------------------------------------ fused
-    def _build_fused(self):
+    def components(self):
+        """Independent components of the evidence-reduced factor graph over query + hidden vars.
+
+        Returns [(query vars (original order), hidden vars, factor indices)], ordered by first query var."""
         loop = self.variables + self.hidden
+        parent = {v: v for v in loop}
+
+        def find(v):
+            while parent[v] != v:
+                parent[v] = parent[parent[v]]
+                v = parent[v]
+            return v
+
+        for vars_, _ in self.factors:
+            lv = [v for v in vars_ if v in parent]
+            for v in lv[1:]:
+                a, b = find(lv[0]), find(v)
+                if a != b:
+                    parent[b] = a
+        groups = {}
+        for v in loop:
+            groups.setdefault(find(v), []).append(v)
+        comps = []
+        for root, members in groups.items():
+            ms = set(members)
+            q = [v for v in self.variables if v in ms]
+            h = [v for v in self.hidden if v in ms]
+            f = [i for i, (vars_, _) in enumerate(self.factors) if any(v in ms for v in vars_)]
+            comps.append((q, h, f))
+        order = {v: i for i, v in enumerate(loop)}
+        comps.sort(key=lambda c: min(order[v] for v in c[0] + c[1]))
+        return comps
+
+    def _make_rows_plan(self, split):
+        comps = self.components() if split else [(list(self.variables), list(self.hidden),
+                                                  list(range(len(self.factors))))]
+        if len(comps) > N.ROWS_MAX_COMP:
+            raise ValueError("too many independent components for the fused kernel")
         pl = N.RowsPlan()
+        loop, fac_order = [], []
+        for ci, (q, h, f) in enumerate(comps):
+            pl.comp_loop_begin[ci] = len(loop)
+            pl.comp_n_query[ci] = len(q)
+            loop.extend(q + h)
+            pl.comp_loop_end[ci] = len(loop)
+            pl.comp_fac_begin[ci] = len(fac_order)
+            fac_order.extend(f)
+            pl.comp_fac_end[ci] = len(fac_order)
+        pl.n_comp = len(comps)
         pl.n_loop = len(loop)
         pl.n_query = len(self.variables)
-        pl.n_fac = len(self.factors)
+        pl.n_fac = len(fac_order)
+        pl.n_marg = self.n_acc
+        pl.n_joint = self.P
+        map_stride = {v: int(np.prod(self.cards[i + 1:])) for i, v in enumerate(self.variables)}
         for i, v in enumerate(loop):
             pl.loop_card[i] = self.card[v]
+            if v in self.variables:
+                pl.loop_marg_off[i] = self.acc_off[self.variables.index(v)]
+                pl.loop_map_stride[i] = map_stride[v]
+            else:
+                pl.loop_marg_off[i] = -1
+                pl.loop_map_stride[i] = 0
         chunks, base, ev_terms = [], 0, []
-        for f, (vars_, cpd) in enumerate(self.factors):
-            vals = np.ascontiguousarray(cpd.values, dtype=np.float64).reshape(-1)
+        for f, fi in enumerate(fac_order):
+            vars_, cpd = self.factors[fi]
+            vals = self._host_values(fi)
             cards = [int(c) for c in cpd.cardinality]
             strides = [int(np.prod(cards[i + 1:])) for i in range(len(cards))]
             pl.fac_base[f] = base
             pl.fac_ev_begin[f] = len(ev_terms)
-            for v, s in zip(vars_, strides):
+            for v, st in zip(vars_, strides):
                 if v in loop:
-                    pl.fac_stride[f][loop.index(v)] = s
+                    pl.fac_stride[f][loop.index(v)] = st
                 else:
-                    ev_terms.append((self.col_of[v], s, self.card[v]))
+                    ev_terms.append((self.col_of[v], st, self.card[v]))
             pl.fac_ev_end[f] = len(ev_terms)
             chunks.append(vals)
             base += vals.size
         pl.n_ev = len(ev_terms)
-        for j, (col, s, c) in enumerate(ev_terms):
-            pl.ev_col[j], pl.ev_stride[j], pl.ev_card[j] = col, s, c
+        for j, (col, st, c) in enumerate(ev_terms):
+            pl.ev_col[j], pl.ev_stride[j], pl.ev_card[j] = col, st, c
         values = np.concatenate(chunks) if chunks else np.zeros(1)
         if values.size >= 2 ** 31:
             raise ValueError("plan values too large")
         pl.n_values = int(values.size)
-        self._values = values
-        self._plan = pl
         L = N.lib()
         h = ctypes.c_void_p()
         N.check(L.pgm_rows_plan_create(ctypes.byref(pl), values.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)),
                 "rows_plan_create")
-        self._handle = h
+        return h, pl, len(comps)
+
+    def _host_values(self, fi):
+        """CPT values (C-order) of factor fi, packed into the plan (a copy, no arithmetic)."""
+        cache = self.__dict__.setdefault("_vals_cache", {})
+        if fi not in cache:
+            cache[fi] = np.ascontiguousarray(self.factors[fi][1].values, dtype=np.float64).reshape(-1)
+        return cache[fi]
+
+    def _build_fused(self):
+        """Upload the plan (lazily, on first run)."""
+        if self._handle is None:
+            self._handle, self._plan, self.n_comp = self._make_rows_plan(split=True)
+            if self.n_comp == 1:
+                self._handle_joint = self._handle
+
+    def _joint_handle(self):
+        if self._handle_joint is None:
+            self._handle_joint, _, _ = self._make_rows_plan(split=False)
+        return self._handle_joint
 
     def __del__(self):
-        h = getattr(self, "_handle", None)
-        if h is not None and h.value:
+        hs = {id(h): h for h in (getattr(self, "_handle", None), getattr(self, "_handle_joint", None))
+              if h is not None and h.value}
+        for h in hs.values():
             try:
                 N.load_library().pgm_rows_plan_destroy(h)
             except Exception:
@@ -146,7 +223,7 @@ class PatternPlan:
             out["joint"] = torch.empty((self.P, n_rows), dtype=torch.float64, device=dev)
         if map_ or gap:
             out["map"] = torch.empty(n_rows, dtype=torch.int32, device=dev)
-        if gap:
+        if gap and self.kind == "fused":
             out["gap"] = torch.empty(n_rows, dtype=torch.float64, device=dev)
         return out
 
@@ -157,6 +234,12 @@ class PatternPlan:
         if n_rows <= 0:
             return out
         if self.kind == "fused":
+            if "joint" in out and not self.joint_fused_ok:
+                self._run_steps(codes, ld, row0, n_rows, {"joint": out["joint"]}, err)
+                rest = {k: v for k, v in out.items() if k != "joint"}
+                if rest:
+                    self._run_fused(codes, ld, row0, n_rows, rest, err)
+                return out
             return self._run_fused(codes, ld, row0, n_rows, out, err)
         return self._run_steps(codes, ld, row0, n_rows, out, err)
 
@@ -174,14 +257,25 @@ class PatternPlan:
 
     def _run_fused(self, codes, ld, row0, n_rows, out, err):
         L = N.lib()
-        ld_out = None
-        for k in ("marg", "joint"):
-            if k in out:
-                ld_out = int(out[k].stride(0))
-        N.check(L.pgm_rows_plan_run(self._handle, self._mode(out), N.ptr(codes), int(ld), int(row0), int(n_rows),
-                                    N.ptr(out.get("marg")), N.ptr(out.get("joint")), int(ld_out or n_rows),
-                                    N.ptr(out.get("map")), N.ptr(out.get("gap")), N.ptr(err), N.stream_handle()),
-                "rows_plan_run")
+        self._build_fused()
+        mode = self._mode(out)
+        if (mode & N.ROWS_JOINT) and self.n_comp > 1:
+            # the joint over independent components needs the single-component (monolithic) plan
+            N.check(L.pgm_rows_plan_run(self._joint_handle(), N.ROWS_JOINT, N.ptr(codes), int(ld), int(row0),
+                                        int(n_rows), None, N.ptr(out["joint"]), int(out["joint"].stride(0)), None,
+                                        None, N.ptr(err), N.stream_handle()), "rows_plan_run")
+            mode &= ~N.ROWS_JOINT
+            if not mode:
+                return out
+        ld_out = n_rows
+        if "marg" in out:
+            ld_out = int(out["marg"].stride(0))
+        elif "joint" in out and (mode & N.ROWS_JOINT):
+            ld_out = int(out["joint"].stride(0))
+        N.check(L.pgm_rows_plan_run(self._handle, mode, N.ptr(codes), int(ld), int(row0), int(n_rows),
+                                    N.ptr(out.get("marg")), N.ptr(out.get("joint")) if mode & N.ROWS_JOINT else None,
+                                    int(ld_out), N.ptr(out.get("map")), N.ptr(out.get("gap")), N.ptr(err),
+                                    N.stream_handle()), "rows_plan_run")
         return out
 
     def _dev_factors(self):
@@ -232,11 +326,8 @@ class PatternPlan:
                     m = E.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
                     E.contract(m, [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw", out=view)
             if "map" in out:
-                idx = torch.empty(n, dtype=torch.int64, device=R.device)
-                N.check(L.pgm_argmax(N.ptr(R), n, self.P, 1, n, N.ptr(idx), N.stream_handle()), "argmax")
-                out["map"][c0:c0 + n].copy_(idx.to(torch.int32))
-                if "gap" in out:
-                    out["gap"][c0:c0 + n].fill_(1.0)
+                N.check(L.pgm_argmax(N.ptr(R), n, self.P, 1, n, None, N.ptr(out["map"][c0:c0 + n]),
+                                     N.stream_handle()), "argmax")
             if "joint" in out:
                 jv = out["joint"][:, c0:c0 + n]
                 E.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw", out=jv)
@@ -256,6 +347,7 @@ class PatternPlan:
         return b
 
     def describe(self):
-        return {"kind": self.kind, "factors": [list(v) for v, _ in self.factors], "hidden": self.hidden,
+        return {"kind": self.kind, "components": len(self.components()) if self.kind == "fused" else None,
+                "factors": [list(v) for v, _ in self.factors], "hidden": self.hidden,
                 "evidence_columns": len(self.ev_used), "query_space": self.P, "hidden_space": self.H,
                 "values": int(sum(int(np.prod(c.cardinality)) for _, c in self.factors))}

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 1
+    assert lib.pgm_version() == 2
 
 
 def test_struct_layouts_match_header():
@@ -39,8 +39,8 @@ def test_struct_layouts_match_header():
 
     assert ctypes.sizeof(N.ContractDesc) == 16 + 7 * 8 * N.PGM_MAX_DIMS
     assert ctypes.sizeof(N.GatherDesc) == 16 + 16 + 6 * 8 * N.PGM_MAX_DIMS
-    assert ctypes.sizeof(N.RowsPlan) == 4 * (8 + N.ROWS_MAX_LOOP + N.ROWS_MAX_FAC * (3 + N.ROWS_MAX_LOOP)
-                                             + 3 * N.ROWS_MAX_EV)
+    assert ctypes.sizeof(N.RowsPlan) == 4 * (8 + 3 * N.ROWS_MAX_LOOP + 5 * N.ROWS_MAX_COMP
+                                             + N.ROWS_MAX_FAC * (3 + N.ROWS_MAX_LOOP) + 3 * N.ROWS_MAX_EV)
 
 
 def test_no_compute_without_gpu():

@@ -117,8 +117,13 @@ def test_rows_plan_matches_numpy(gpu):
     vals = np.concatenate([f0.ravel(), f1.ravel(), f2.ravel()])
     P = N.RowsPlan()
     P.n_loop, P.n_query, P.n_fac, P.n_ev, P.n_values = 3, 2, 3, 2, vals.size
+    P.n_comp, P.n_marg, P.n_joint = 1, cq0 + cq1, cq0 * cq1
+    P.comp_loop_begin[0], P.comp_n_query[0], P.comp_loop_end[0] = 0, 2, 3
+    P.comp_fac_begin[0], P.comp_fac_end[0] = 0, 3
     for i, c in enumerate([cq0, cq1, ch]):
         P.loop_card[i] = c
+    P.loop_marg_off[0], P.loop_marg_off[1], P.loop_marg_off[2] = 0, cq0, -1
+    P.loop_map_stride[0], P.loop_map_stride[1] = cq1, 1
     P.fac_base[0], P.fac_base[1], P.fac_base[2] = 0, f0.size, f0.size + f1.size
     s0, s1, s2 = [x // 8 for x in f0.strides], [x // 8 for x in f1.strides], [x // 8 for x in f2.strides]
     # loop dims: 0=q0, 1=q1, 2=h

@@ -1,0 +1,102 @@
+"""Fused row plans vs the oracle on random networks: components, hidden variables, impossible evidence.
+
+Random BNs (seeded) with zero entries in their CPTs so that some evidence rows
+are impossible; for each evidence pattern the batched device plan (fused and
+forced-steps executors) must give the oracle's marginals (1e-9 absolute; NaN
+exactly where the oracle's 0/0 normalisation gives NaN, DiscreteFactor.py:530),
+joint, and MAP (exact when the top-two gap > 1e-9; index 0 on impossible rows,
+as np.argmax of an all-NaN joint).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def random_bn(seed, n=14, max_parents=3):
+    from oracle.network import ONetwork
+    from pgmpy_amd.factors.discrete import TabularCPD
+    from pgmpy_amd.models import DiscreteBayesianNetwork
+
+    rng = np.random.default_rng(seed)
+    names = [f"v{i:02d}" for i in range(n)]
+    card = {v: int(rng.integers(2, 5)) for v in names}
+    parents = {}
+    for i, v in enumerate(names):
+        k = int(rng.integers(0, min(i, max_parents) + 1))
+        parents[v] = [names[j] for j in sorted(rng.choice(i, size=k, replace=False))] if k else []
+    bn = DiscreteBayesianNetwork()
+    bn.add_nodes_from(names)
+    bn.add_edges_from([(p, v) for v in names for p in parents[v]])
+    cpts = {}
+    cpds = []
+    for v in names:
+        cols = int(np.prod([card[p] for p in parents[v]])) if parents[v] else 1
+        t = rng.random((card[v], cols))
+        t[rng.random(t.shape) < 0.15] = 0.0
+        t[0, t.sum(axis=0) == 0] = 1.0
+        t /= t.sum(axis=0, keepdims=True)
+        cpts[v] = t.reshape([card[v]] + [card[p] for p in parents[v]])
+        sn = {x: [f"s{k}" for k in range(card[x])] for x in [v] + parents[v]}
+        cpds.append(TabularCPD(v, card[v], t, parents[v] or None, [card[p] for p in parents[v]] or None,
+                               state_names=sn))
+    bn.add_cpds(*cpds)
+    onet = ONetwork(names, {v: [f"s{k}" for k in range(card[v])] for v in names}, parents, cpts)
+    return bn, onet
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_patterns_vs_oracle(gpu, seed):
+    from oracle import ve as OVE
+    from pgmpy_amd.inference.batch import encode_frame, upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+
+    bn, onet = random_bn(seed)
+    rng = np.random.default_rng(100 + seed)
+    names = sorted(bn.nodes())
+    for trial in range(4):
+        picks = list(rng.choice(names, size=int(rng.integers(3, 9)), replace=False))
+        nq = int(rng.integers(1, 4))
+        q, e = picks[:nq], picks[nq:]
+        n = 40
+        rows = {v: [onet.states[v][int(rng.integers(0, onet.card[v]))] for _ in range(n)] for v in e}
+        df = pd.DataFrame(rows, columns=e)
+        col_of = {c: i for i, c in enumerate(e)}
+        codes = upload_codes(encode_frame(bn, df))
+        for force in (None, "steps"):
+            plan = PatternPlan(bn, q, e, col_of, force=force)
+            out = plan.alloc_outputs(n, marginals=True, joint=True, map_=True)
+            plan.run(codes, n, 0, n, out)
+            marg, joint, mp = (out["marg"].cpu().numpy(), out["joint"].cpu().numpy(), out["map"].cpu().numpy())
+            for r in range(n):
+                ev = {v: rows[v][r] for v in e}
+                j = OVE.joint(onet, q, ev)
+                z = j.sum()
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    jn = j / z
+                np.testing.assert_allclose(joint[:, r], jn.ravel(), atol=1e-12, equal_nan=True)
+                exp_m = np.concatenate([jn.sum(axis=tuple(k for k in range(len(q)) if k != i))
+                                        for i in range(len(q))])
+                np.testing.assert_allclose(marg[:, r], exp_m, atol=1e-12, equal_nan=True)
+                if not (z > 0):
+                    assert mp[r] == 0
+                    continue
+                flat = np.sort(jn.ravel())[::-1]
+                if flat.size == 1 or (flat[0] - flat[1]) / flat[0] > 1e-9:
+                    assert mp[r] == int(np.argmax(jn)), (seed, trial, force, r)
+
+
+def test_c3_template_factorises_into_components(gpu):
+    import random
+
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    obs = [v for v in sorted(m.nodes()) if v not in missing]
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    assert plan.kind == "fused"
+    d = plan.describe()
+    assert d["components"] == 3 and d["evidence_columns"] == 7 and d["values"] == 723
