@@ -21,6 +21,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "pgmhip.h"
 
@@ -420,18 +421,20 @@ __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, ui
 }
 
 // ----------------------------------------------------------------------------- fused row plan
+// Table-driven: for every component c and every entry e of its (query x hidden) index space the
+// host precomputes the offset of each of the component's factors (tab[c.off_base + e*nf + j]), the
+// marginal row each query dim accumulates into (tab[c.marg_base + qi*nq + i]) and the entry's
+// contribution to the flat MAP index (tab[c.map_base + qi]).  The entry loop is wave-uniform, so
+// every table read is a scalar load; per lane there are only the evidence bases of the factors,
+// the running product and the marginal accumulators.
 struct RowsK {
-  int32_t n_loop, n_query, n_fac, n_ev;
-  int32_t n_values, n_marg, n_joint, n_comp;
-  int32_t vals_lds, acc_lds, _pad0, _pad1;
-  int32_t loop_card[PGM_ROWS_MAX_LOOP];
-  int32_t loop_marg_off[PGM_ROWS_MAX_LOOP];
-  int32_t map_inc[PGM_ROWS_MAX_LOOP];  // change of the flat MAP index when query dim k advances
-  int32_t inc[PGM_ROWS_MAX_LOOP][PGM_ROWS_MAX_FAC];  // factor offset change when loop dim k advances
-  int32_t hspan[PGM_ROWS_MAX_FAC];  // sum over the factor's hidden dims of (card-1)*stride (undone on a wrap)
-  int32_t comp_lb[PGM_ROWS_MAX_COMP], comp_nq[PGM_ROWS_MAX_COMP], comp_le[PGM_ROWS_MAX_COMP];
-  int32_t comp_fb[PGM_ROWS_MAX_COMP], comp_fe[PGM_ROWS_MAX_COMP];
+  int32_t n_fac, n_ev, n_values, n_marg;
+  int32_t n_joint, n_comp, n_tab, _pad;
+  int32_t comp_fb[PGM_ROWS_MAX_COMP], comp_nf[PGM_ROWS_MAX_COMP], comp_nq[PGM_ROWS_MAX_COMP];
   uint32_t comp_P[PGM_ROWS_MAX_COMP], comp_H[PGM_ROWS_MAX_COMP];
+  int32_t comp_off_base[PGM_ROWS_MAX_COMP], comp_marg_base[PGM_ROWS_MAX_COMP], comp_map_base[PGM_ROWS_MAX_COMP];
+  int32_t comp_q_lo[PGM_ROWS_MAX_COMP], comp_q_hi[PGM_ROWS_MAX_COMP];  // query dims of c: q_dims[lo, hi)
+  int32_t q_marg_off[PGM_ROWS_MAX_LOOP], q_card[PGM_ROWS_MAX_LOOP];
   int32_t fac_base[PGM_ROWS_MAX_FAC];
   int32_t fac_ev_begin[PGM_ROWS_MAX_FAC], fac_ev_end[PGM_ROWS_MAX_FAC];
   int32_t ev_col[PGM_ROWS_MAX_EV], ev_stride[PGM_ROWS_MAX_EV], ev_card[PGM_ROWS_MAX_EV];
@@ -439,145 +442,127 @@ struct RowsK {
 
 struct RowsHandle {
   RowsK k;
+  int max_nf;
   double *d_values;
+  int32_t *d_tab;
 };
 
-// One lane per evidence row.  Everything that does not depend on the row (loop digits, factor
-// offsets, component bounds) is wave-uniform and lives in scalar registers; per lane there are only
-// the evidence bases of the factors, the running products and the marginal accumulators (LDS).
-template <int MAXF>
+template <bool VL, bool AL, int MAXFC>
 __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__restrict__ gvals,
-                                              const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0,
-                                              int64_t n_rows, int32_t mode, double *__restrict__ marg,
-                                              double *__restrict__ joint, int64_t ld_out,
+                                              const int32_t *__restrict__ tab, const uint8_t *__restrict__ codes,
+                                              int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode,
+                                              double *__restrict__ marg, double *__restrict__ joint, int64_t ld_out,
                                               int32_t *__restrict__ map, double *__restrict__ gap,
                                               int32_t *__restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  double *svals = lds;
-  double *sacc = lds + (p.vals_lds ? ((p.n_values + 1) & ~1) : 0);
-  if (p.vals_lds) {
-    for (int i = threadIdx.x; i < p.n_values; i += blockDim.x) svals[i] = gvals[i];
-    __syncthreads();
-  }
-  const double *V = p.vals_lds ? svals : gvals;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
+  const bool live = r < n_rows;
   const int nb = blockDim.x;
   const int lane = threadIdx.x;
 
-  int32_t base[MAXF];
+  // evidence part of every factor's offset (issued before the LDS staging barrier)
+  int32_t base[PGM_ROWS_MAX_FAC];
   bool bad = false;
 #pragma unroll
-  for (int f = 0; f < MAXF; ++f) {
-    base[f] = 0;
+  for (int f = 0; f < PGM_ROWS_MAX_FAC; ++f) {
+    int32_t b = 0;
     if (f < p.n_fac) {
-      int32_t b = p.fac_base[f];
-      for (int j = p.fac_ev_begin[f]; j < p.fac_ev_end[f]; ++j) {
-        uint32_t c = codes[(int64_t)p.ev_col[j] * ld_codes + row0 + r];
-        if (c >= (uint32_t)p.ev_card[j]) {
-          bad = true;
-          c = 0;
+      b = p.fac_base[f];
+      if (live) {
+        for (int j = p.fac_ev_begin[f]; j < p.fac_ev_end[f]; ++j) {
+          uint32_t c = codes[(int64_t)p.ev_col[j] * ld_codes + row0 + r];
+          if (c >= (uint32_t)p.ev_card[j]) {
+            bad = true;
+            c = 0;
+          }
+          b += (int32_t)c * p.ev_stride[j];
         }
-        b += (int32_t)c * p.ev_stride[j];
       }
-      base[f] = b;
     }
+    base[f] = b;
   }
+  double *svals = lds;
+  double *sacc = lds + (VL ? ((p.n_values + 1) & ~1) : 0);
+  if constexpr (VL) {
+    for (int i = threadIdx.x; i < p.n_values; i += blockDim.x) svals[i] = gvals[i];
+    __syncthreads();
+  }
+  if (!live) return;
   if (bad && err) atomicOr(err, 1);
+  auto val = [&](int32_t i) -> double {
+    if constexpr (VL) return svals[i];
+    else return gvals[i];
+  };
+  auto acc = [&](int32_t t) -> double & {
+    if constexpr (AL) return sacc[t * nb + lane];
+    else return marg[(int64_t)t * ld_out + r];
+  };
   const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
   const bool do_joint = (mode & PGM_ROWS_JOINT) != 0;
   const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
-  double *acc_row = p.acc_lds ? (sacc + lane) : (marg + r);
-  const int64_t acc_stride = p.acc_lds ? nb : ld_out;
 
   double zprod = 1.0, min_gap = 1.0;
   int32_t map_idx = 0;
   for (int c = 0; c < p.n_comp; ++c) {
-    const int lb = p.comp_lb[c], nqe = lb + p.comp_nq[c], le = p.comp_le[c];
-    const int fb = p.comp_fb[c], fe = p.comp_fe[c];
-    int32_t off[MAXF];
+    const int fb = p.comp_fb[c], nf = p.comp_nf[c], nq = p.comp_nq[c];
+    const uint32_t P = p.comp_P[c], H = p.comp_H[c];
+    const int32_t *toff = tab + p.comp_off_base[c];
+    const int32_t *tmarg = tab + p.comp_marg_base[c];
+    const int32_t *tmap = tab + p.comp_map_base[c];
+    // this component's factor bases, compacted to static slots
+    int32_t cb[MAXFC];
 #pragma unroll
-    for (int f = 0; f < MAXF; ++f) off[f] = 0;
-    int32_t dig[PGM_ROWS_MAX_LOOP];
+    for (int j = 0; j < MAXFC; ++j) {
+      int32_t b = 0;
 #pragma unroll
-    for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k) dig[k] = 0;
-    if (do_marg) {
-#pragma unroll
-      for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
-        if (k >= lb && k < nqe)
-          for (int s = 0; s < p.loop_card[k]; ++s) acc_row[(p.loop_marg_off[k] + s) * acc_stride] = 0.0;
+      for (int f = 0; f < PGM_ROWS_MAX_FAC; ++f) b = (f == fb + j) ? base[f] : b;
+      cb[j] = b;
+    }
+    if (do_marg && nq > 1) {
+      for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
+        for (int s = 0; s < p.q_card[q]; ++s) acc(p.q_marg_off[q] + s) = 0.0;
     }
     double mass = 0.0, best = -1.0, second = -1.0;
-    int32_t cur_map = 0, best_map = 0;
-    for (uint32_t qi = 0; qi < p.comp_P[c]; ++qi) {
+    int32_t best_map = 0;
+    uint32_t e = 0;
+    for (uint32_t qi = 0; qi < P; ++qi) {
       double v = 0.0;
-      for (uint32_t hi = 0; hi < p.comp_H[c]; ++hi) {
+      for (uint32_t hi = 0; hi < H; ++hi, ++e) {
+        const int32_t *o = toff + e * nf;
         double prod = 1.0;
 #pragma unroll
-        for (int f = 0; f < MAXF; ++f)
-          if (f >= fb && f < fe) prod *= V[base[f] + off[f]];
+        for (int j = 0; j < MAXFC; ++j)
+          if (j < nf) prod *= val(cb[j] + o[j]);
         v += prod;
-        bool carry = true;  // hidden odometer: dims [nqe, le), innermost last
-#pragma unroll
-        for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
-          if (carry && k >= nqe && k < le) {
-            if (++dig[k] < p.loop_card[k]) {
-#pragma unroll
-              for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
-              carry = false;
-            } else {
-              dig[k] = 0;
-            }
-          }
-        }
-        if (carry) {
-#pragma unroll
-          for (int f = 0; f < MAXF; ++f)
-            if (f >= fb && f < fe) off[f] -= p.hspan[f];
-        }
       }
       mass += v;
       if (do_marg) {
-#pragma unroll
-        for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
-          if (k >= lb && k < nqe) acc_row[(p.loop_marg_off[k] + dig[k]) * acc_stride] += v;
+        if (nq == 1) {
+          acc(tmarg[qi]) = v;  // each marginal row is hit exactly once
+        } else {
+          for (int i = 0; i < nq; ++i) acc(tmarg[qi * nq + i]) += v;
+        }
       }
-      if (do_joint) joint[(int64_t)cur_map * ld_out + r] = v;
+      if (do_joint) joint[(int64_t)tmap[qi] * ld_out + r] = v;
       if (do_map) {
         if (v > best) {
           second = best;
           best = v;
-          best_map = cur_map;
+          best_map = tmap[qi];
         } else if (v > second) {
           second = v;
         }
       }
-      bool carry = true;  // query odometer: dims [lb, nqe)
-#pragma unroll
-      for (int k = PGM_ROWS_MAX_LOOP - 1; k >= 0; --k) {
-        if (carry && k >= lb && k < nqe) {
-          if (++dig[k] < p.loop_card[k]) {
-#pragma unroll
-            for (int f = 0; f < MAXF; ++f) off[f] += p.inc[k][f];
-            cur_map += p.map_inc[k];
-            carry = false;
-          } else {
-            dig[k] = 0;
-          }
-        }
-      }
     }
     zprod *= mass;
-    if (do_marg) {  // component marginals normalised by the component mass
+    if (do_marg && nq > 0) {  // component marginals normalised by the component mass
       const double inv = 1.0 / mass;
-#pragma unroll
-      for (int k = 0; k < PGM_ROWS_MAX_LOOP; ++k)
-        if (k >= lb && k < nqe)
-          for (int s = 0; s < p.loop_card[k]; ++s) acc_row[(p.loop_marg_off[k] + s) * acc_stride] *= inv;
+      for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
+        for (int s = 0; s < p.q_card[q]; ++s) acc(p.q_marg_off[q] + s) *= inv;
     }
     if (do_map) {
       map_idx += best_map;
-      if (p.comp_P[c] > 1) {
+      if (P > 1) {
         const double g = best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0;
         min_gap = fmin(min_gap, g);
       }
@@ -587,15 +572,17 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
   const bool dead = !(zprod > 0.0);
   if (do_marg) {
     const double nan = __builtin_nan("");
-    for (int a = 0; a < p.n_marg; ++a) {
-      const double m = dead ? nan : acc_row[a * acc_stride];
-      marg[(int64_t)a * ld_out + r] = m;
+    if constexpr (AL) {
+      for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = dead ? nan : acc(a);
+    } else {
+      if (dead)
+        for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = nan;
     }
   }
   if (do_joint) {
     const double inv = 1.0 / zprod;
     for (int q = 0; q < p.n_joint; ++q) {
-      double* j = joint + (int64_t)q * ld_out + r;
+      double *j = joint + (int64_t)q * ld_out + r;
       *j = dead ? __builtin_nan("") : *j * inv;
     }
   }
@@ -603,6 +590,20 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
     if (map) map[r] = dead ? 0 : map_idx;
     if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : min_gap;
   }
+}
+
+template <bool VL, bool AL>
+static void launch_rows_f(int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k, const double *v,
+                          const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n, int32_t mode,
+                          double *marg, double *joint, int64_t ldo, int32_t *map, double *gap, int32_t *err) {
+  if (max_nf <= 2)
+    hipLaunchKernelGGL((k_rows<VL, AL, 2>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+  else if (max_nf <= 4)
+    hipLaunchKernelGGL((k_rows<VL, AL, 4>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+  else if (max_nf <= 8)
+    hipLaunchKernelGGL((k_rows<VL, AL, 8>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+  else
+    hipLaunchKernelGGL((k_rows<VL, AL, 16>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
 }
 
 // ============================================================================= C-ABI
@@ -810,15 +811,14 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
                 pl->n_loop, pl->n_query, pl->n_fac, pl->n_ev, pl->n_comp, pl->n_marg);
   RowsK k;
   memset(&k, 0, sizeof k);
-  k.n_loop = pl->n_loop;
-  k.n_query = pl->n_query;
   k.n_fac = pl->n_fac;
   k.n_ev = pl->n_ev;
   k.n_values = pl->n_values;
   k.n_marg = pl->n_marg;
   k.n_joint = pl->n_joint;
   k.n_comp = pl->n_comp;
-  int covered_loop = 0, covered_fac = 0, nq_total = 0;
+  std::vector<int32_t> tab;
+  int covered_loop = 0, covered_fac = 0, nq_total = 0, max_nf = 1;
   for (int c = 0; c < pl->n_comp; ++c) {
     const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c], le = pl->comp_loop_end[c];
     const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
@@ -828,52 +828,71 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
                   lb + nq, le, fb, fe);
     covered_loop = le;
     covered_fac = fe;
-    nq_total += nq;
     uint64_t P = 1, H = 1;
     for (int kk = lb; kk < le; ++kk) {
       if (pl->loop_card[kk] <= 0) return fail(PGM_EINVAL, "rows_plan_create: loop_card[%d] <= 0", kk);
       (kk < lb + nq ? P : H) *= (uint64_t)pl->loop_card[kk];
+      if (kk < lb + nq && (pl->loop_marg_off[kk] < 0 || pl->loop_marg_off[kk] + pl->loop_card[kk] > pl->n_marg))
+        return fail(PGM_EINVAL, "rows_plan_create: loop %d marginal rows out of range", kk);
     }
-    if (P * H >= (1ull << 31)) return fail(PGM_EINVAL, "rows_plan_create: component %d space too large", c);
-    k.comp_lb[c] = lb;
-    k.comp_nq[c] = nq;
-    k.comp_le[c] = le;
-    k.comp_fb[c] = fb;
-    k.comp_fe[c] = fe;
-    k.comp_P[c] = (uint32_t)P;
-    k.comp_H[c] = (uint32_t)H;
-    for (int kk = lb; kk < le; ++kk) {
-      const bool q = kk < lb + nq;
-      const int end = q ? lb + nq : le;  // odometer group of dim kk
-      int64_t mi = 0;
-      if (q) {
-        if (pl->loop_marg_off[kk] < 0 || pl->loop_marg_off[kk] + pl->loop_card[kk] > pl->n_marg)
-          return fail(PGM_EINVAL, "rows_plan_create: loop %d marginal rows out of range", kk);
-        mi = pl->loop_map_stride[kk];
-        for (int k2 = kk + 1; k2 < end; ++k2) mi -= (int64_t)(pl->loop_card[k2] - 1) * pl->loop_map_stride[k2];
-      }
-      k.map_inc[kk] = (int32_t)mi;
-      for (int f = fb; f < fe; ++f) {
-        int64_t inc = pl->fac_stride[f][kk];
-        for (int k2 = kk + 1; k2 < end; ++k2) inc -= (int64_t)(pl->loop_card[k2] - 1) * pl->fac_stride[f][k2];
-        k.inc[kk][f] = (int32_t)inc;
-      }
-    }
-    for (int f = fb; f < fe; ++f) {
-      int64_t hs = 0;
-      for (int kk = lb + nq; kk < le; ++kk) hs += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
-      k.hspan[f] = (int32_t)hs;
+    const int nf = fe - fb;
+    if (P * H * (uint64_t)std::max(nf, 1) + tab.size() >= (1ull << 26))
+      return fail(PGM_EINVAL, "rows_plan_create: component %d index space too large for the fused kernel", c);
+    for (int f = fb; f < fe; ++f)
       for (int kk = 0; kk < pl->n_loop; ++kk)
         if ((kk < lb || kk >= le) && pl->fac_stride[f][kk] != 0)
           return fail(PGM_EINVAL, "rows_plan_create: factor %d strides a loop dim outside its component", f);
+    max_nf = std::max(max_nf, nf);
+    k.comp_fb[c] = fb;
+    k.comp_nf[c] = nf;
+    k.comp_nq[c] = nq;
+    k.comp_P[c] = (uint32_t)P;
+    k.comp_H[c] = (uint32_t)H;
+    k.comp_q_lo[c] = nq_total;
+    for (int kk = lb; kk < lb + nq; ++kk) {
+      k.q_marg_off[nq_total] = pl->loop_marg_off[kk];
+      k.q_card[nq_total] = pl->loop_card[kk];
+      ++nq_total;
+    }
+    k.comp_q_hi[c] = nq_total;
+    // per-entry tables, entries in C-order over [query dims..., hidden dims...] (last fastest)
+    const int nl = le - lb;
+    std::vector<int32_t> dig(nl, 0);
+    k.comp_off_base[c] = (int32_t)tab.size();
+    for (uint64_t e = 0; e < P * H; ++e) {
+      uint64_t t = e;
+      for (int d = nl - 1; d >= 0; --d) {
+        dig[d] = (int32_t)(t % (uint64_t)pl->loop_card[lb + d]);
+        t /= (uint64_t)pl->loop_card[lb + d];
+      }
+      for (int f = fb; f < fe; ++f) {
+        int64_t o = 0;
+        for (int d = 0; d < nl; ++d) o += (int64_t)dig[d] * pl->fac_stride[f][lb + d];
+        tab.push_back((int32_t)o);
+      }
+    }
+    k.comp_marg_base[c] = (int32_t)tab.size();
+    for (uint64_t qi = 0; qi < P; ++qi) {
+      uint64_t t = qi;
+      for (int d = nq - 1; d >= 0; --d) {
+        dig[d] = (int32_t)(t % (uint64_t)pl->loop_card[lb + d]);
+        t /= (uint64_t)pl->loop_card[lb + d];
+      }
+      for (int d = 0; d < nq; ++d) tab.push_back(pl->loop_marg_off[lb + d] + dig[d]);
+    }
+    k.comp_map_base[c] = (int32_t)tab.size();
+    for (uint64_t qi = 0; qi < P; ++qi) {
+      uint64_t t = qi;
+      int64_t m = 0;
+      for (int d = nq - 1; d >= 0; --d) {
+        m += (int64_t)(t % (uint64_t)pl->loop_card[lb + d]) * pl->loop_map_stride[lb + d];
+        t /= (uint64_t)pl->loop_card[lb + d];
+      }
+      tab.push_back((int32_t)m);
     }
   }
   if (covered_loop != pl->n_loop || covered_fac != pl->n_fac || nq_total != pl->n_query)
     return fail(PGM_EINVAL, "rows_plan_create: components do not cover the loop dims / factors");
-  for (int kk = 0; kk < pl->n_loop; ++kk) {
-    k.loop_card[kk] = pl->loop_card[kk];
-    k.loop_marg_off[kk] = pl->loop_marg_off[kk];
-  }
   for (int f = 0; f < pl->n_fac; ++f) {
     k.fac_base[f] = pl->fac_base[f];
     k.fac_ev_begin[f] = pl->fac_ev_begin[f];
@@ -891,19 +910,27 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
     k.ev_stride[j] = pl->ev_stride[j];
     k.ev_card[j] = pl->ev_card[j];
   }
+  if (tab.empty()) tab.push_back(0);
+  k.n_tab = (int32_t)tab.size();
   RowsHandle *h = new (std::nothrow) RowsHandle;
   if (!h) return fail(PGM_ENOMEM, "rows_plan_create: host allocation");
   h->k = k;
+  h->max_nf = max_nf;
   h->d_values = nullptr;
+  h->d_tab = nullptr;
+  hipError_t e = hipSuccess;
   if (pl->n_values > 0) {
-    hipError_t e = hipMalloc((void **)&h->d_values, sizeof(double) * pl->n_values);
+    e = hipMalloc((void **)&h->d_values, sizeof(double) * pl->n_values);
     if (e == hipSuccess) e = hipMemcpy(h->d_values, host_values, sizeof(double) * pl->n_values, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      if (h->d_values) (void)hipFree(h->d_values);
-      delete h;
-      return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_plan_create: %s", hipGetErrorString(e));
-    }
+  }
+  if (e == hipSuccess) e = hipMalloc((void **)&h->d_tab, sizeof(int32_t) * tab.size());
+  if (e == hipSuccess) e = hipMemcpy(h->d_tab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    if (h->d_values) (void)hipFree(h->d_values);
+    if (h->d_tab) (void)hipFree(h->d_tab);
+    delete h;
+    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_plan_create: %s", hipGetErrorString(e));
   }
   *handle = h;
   return PGM_OK;
@@ -913,6 +940,7 @@ int pgm_rows_plan_destroy(void *handle) {
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
   if (h->d_values) (void)hipFree(h->d_values);
+  if (h->d_tab) (void)hipFree(h->d_tab);
   delete h;
   return PGM_OK;
 }
@@ -932,25 +960,34 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   if ((mode & PGM_ROWS_MAPGAP) && !gap) return fail(PGM_EINVAL, "rows_plan_run: MAP gap requested, gap is null");
   if ((mode & (PGM_ROWS_MARGINALS | PGM_ROWS_JOINT)) && ld_out < n_rows)
     return fail(PGM_EINVAL, "rows_plan_run: ld_out %lld < n_rows %lld", (long long)ld_out, (long long)n_rows);
-  RowsK k = h->k;
+  const RowsK &k = h->k;
   // LDS: CPT values (if they fit) + per-lane marginal accumulators
   const size_t kLds = 64 * 1024;
   size_t vals_bytes = (size_t)((k.n_values + 1) & ~1) * sizeof(double);
-  k.vals_lds = vals_bytes <= 48 * 1024 ? 1 : 0;
-  if (!k.vals_lds) vals_bytes = 0;
+  const bool vals_lds = vals_bytes <= 48 * 1024;
+  if (!vals_lds) vals_bytes = 0;
   int block = 256;
-  k.acc_lds = 0;
+  bool acc_lds = false;
   if (mode & PGM_ROWS_MARGINALS) {
     while (block > 64 && vals_bytes + (size_t)k.n_marg * block * sizeof(double) > kLds) block >>= 1;
-    k.acc_lds = vals_bytes + (size_t)k.n_marg * block * sizeof(double) <= kLds ? 1 : 0;
-    if (!k.acc_lds) block = 256;
+    acc_lds = vals_bytes + (size_t)k.n_marg * block * sizeof(double) <= kLds;
+    if (!acc_lds) block = 256;
   }
-  size_t lds = vals_bytes + (k.acc_lds ? (size_t)k.n_marg * block * sizeof(double) : 0);
-  uint64_t blocks = ((uint64_t)n_rows + block - 1) / block;
+  const size_t lds = vals_bytes + (acc_lds ? (size_t)k.n_marg * block * sizeof(double) : 0);
+  const uint64_t blocks = ((uint64_t)n_rows + block - 1) / block;
   if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
-  hipLaunchKernelGGL((k_rows<PGM_ROWS_MAX_FAC>), dim3((unsigned)blocks), dim3(block), lds, S(stream), k,
-                     (const double *)h->d_values, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap,
-                     err_flag);
+  const dim3 g((unsigned)blocks), b(block);
+  hipStream_t s = S(stream);
+  const double *v = h->d_values;
+  const int32_t *t = h->d_tab;
+  if (vals_lds && acc_lds)
+    launch_rows_f<true, true>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+  else if (vals_lds)
+    launch_rows_f<true, false>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+  else if (acc_lds)
+    launch_rows_f<false, true>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+  else
+    launch_rows_f<false, false>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }
