@@ -175,7 +175,8 @@ enum pgm_rows_mode {
   PGM_ROWS_MARGINALS = 1, /* per query var normalized marginal (predict_probability) */
   PGM_ROWS_JOINT = 2,     /* normalized joint over the query dims (query joint=True); n_comp == 1 only */
   PGM_ROWS_MAP = 4,       /* first-index argmax of the joint (map_query / predict)  */
-  PGM_ROWS_MAPGAP = 8     /* also (best - second best) / best of the joint, for tie screening */
+  PGM_ROWS_MAPGAP = 8,    /* also (best - second best) / best of the joint, for tie screening */
+  PGM_ROWS_VALUES_GLOBAL = 16 /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
 };
 
 typedef struct {

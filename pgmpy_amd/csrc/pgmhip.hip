@@ -435,6 +435,10 @@ struct RowsK {
   int32_t comp_off_base[PGM_ROWS_MAX_COMP], comp_marg_base[PGM_ROWS_MAX_COMP], comp_map_base[PGM_ROWS_MAX_COMP];
   int32_t comp_q_lo[PGM_ROWS_MAX_COMP], comp_q_hi[PGM_ROWS_MAX_COMP];  // query dims of c: q_dims[lo, hi)
   int32_t q_marg_off[PGM_ROWS_MAX_LOOP], q_card[PGM_ROWS_MAX_LOOP];
+  // affine components (one query dim, no hidden dim): factor j of component c sits at
+  // cb[j] + s * comp_fstride[c][j] for query state s; the MAP index moves by comp_mstride[c]
+  int32_t comp_simple[PGM_ROWS_MAX_COMP], comp_mstride[PGM_ROWS_MAX_COMP];
+  int32_t comp_fstride[PGM_ROWS_MAX_COMP][PGM_ROWS_MAX_FAC];
   int32_t fac_base[PGM_ROWS_MAX_FAC];
   int32_t fac_ev_begin[PGM_ROWS_MAX_FAC], fac_ev_end[PGM_ROWS_MAX_FAC];
   int32_t ev_col[PGM_ROWS_MAX_EV], ev_stride[PGM_ROWS_MAX_EV], ev_card[PGM_ROWS_MAX_EV];
@@ -442,12 +446,12 @@ struct RowsK {
 
 struct RowsHandle {
   RowsK k;
-  int max_nf;
+  int max_nf, max_f;
   double *d_values;
   int32_t *d_tab;
 };
 
-template <bool VL, bool AL, int MAXFC>
+template <bool VL, bool AL, int MAXF, int MAXFC>
 __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__restrict__ gvals,
                                               const int32_t *__restrict__ tab, const uint8_t *__restrict__ codes,
                                               int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode,
@@ -461,10 +465,10 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
   const int lane = threadIdx.x;
 
   // evidence part of every factor's offset (issued before the LDS staging barrier)
-  int32_t base[PGM_ROWS_MAX_FAC];
+  int32_t base[MAXF];
   bool bad = false;
 #pragma unroll
-  for (int f = 0; f < PGM_ROWS_MAX_FAC; ++f) {
+  for (int f = 0; f < MAXF; ++f) {
     int32_t b = 0;
     if (f < p.n_fac) {
       b = p.fac_base[f];
@@ -515,8 +519,53 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
     for (int j = 0; j < MAXFC; ++j) {
       int32_t b = 0;
 #pragma unroll
-      for (int f = 0; f < PGM_ROWS_MAX_FAC; ++f) b = (f == fb + j) ? base[f] : b;
+      for (int f = 0; f < MAXF; ++f) b = (f == fb + j) ? base[f] : b;
       cb[j] = b;
+    }
+    if (p.comp_simple[c]) {
+      // affine fast path: entries are the states of the component's single query variable.
+      // pass 1: component mass (+ MAP, joint); pass 2: recompute and stream the normalised
+      // marginal straight to HBM (no accumulator state, so LDS holds only the CPT values)
+      int32_t st[MAXFC];
+#pragma unroll
+      for (int j = 0; j < MAXFC; ++j) st[j] = p.comp_fstride[c][j];
+      const int32_t ms = p.comp_mstride[c];
+      double mass = 0.0, best = -1.0, second = -1.0;
+      int32_t best_s = 0;
+      for (uint32_t qs = 0; qs < P; ++qs) {
+        double prod = 1.0;
+#pragma unroll
+        for (int j = 0; j < MAXFC; ++j)
+          if (j < nf) prod *= val(cb[j] + (int32_t)qs * st[j]);
+        mass += prod;
+        if (do_joint) joint[(int64_t)qs * ms * ld_out + r] = prod;
+        if (do_map) {
+          if (prod > best) {
+            second = best;
+            best = prod;
+            best_s = (int32_t)qs;
+          } else if (prod > second) {
+            second = prod;
+          }
+        }
+      }
+      zprod *= mass;
+      if (do_marg && nq) {
+        const double inv = 1.0 / mass;
+        double *out = marg + (int64_t)p.q_marg_off[p.comp_q_lo[c]] * ld_out + r;
+        for (uint32_t qs = 0; qs < P; ++qs) {
+          double prod = 1.0;
+#pragma unroll
+          for (int j = 0; j < MAXFC; ++j)
+            if (j < nf) prod *= val(cb[j] + (int32_t)qs * st[j]);
+          __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
+        }
+      }
+      if (do_map) {
+        map_idx += best_s * ms;
+        if (P > 1) min_gap = fmin(min_gap, best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0);
+      }
+      continue;
     }
     if (do_marg && nq > 1) {
       for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
@@ -525,15 +574,25 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
     double mass = 0.0, best = -1.0, second = -1.0;
     int32_t best_map = 0;
     uint32_t e = 0;
+#pragma unroll 2
     for (uint32_t qi = 0; qi < P; ++qi) {
       double v = 0.0;
-      for (uint32_t hi = 0; hi < H; ++hi, ++e) {
-        const int32_t *o = toff + e * nf;
+      if (H == 1) {  // no hidden dims: one product per query entry
+        const int32_t *o = toff + qi * nf;
         double prod = 1.0;
 #pragma unroll
         for (int j = 0; j < MAXFC; ++j)
           if (j < nf) prod *= val(cb[j] + o[j]);
-        v += prod;
+        v = prod;
+      } else {
+        for (uint32_t hi = 0; hi < H; ++hi, ++e) {
+          const int32_t *o = toff + e * nf;
+          double prod = 1.0;
+#pragma unroll
+          for (int j = 0; j < MAXFC; ++j)
+            if (j < nf) prod *= val(cb[j] + o[j]);
+          v += prod;
+        }
       }
       mass += v;
       if (do_marg) {
@@ -572,11 +631,17 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
   const bool dead = !(zprod > 0.0);
   if (do_marg) {
     const double nan = __builtin_nan("");
-    if constexpr (AL) {
-      for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = dead ? nan : acc(a);
-    } else {
-      if (dead)
-        for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = nan;
+    if (dead) {
+      for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = nan;
+    } else if constexpr (AL) {
+      for (int c = 0; c < p.n_comp; ++c) {
+        if (p.comp_simple[c]) continue;
+        for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
+          for (int s2 = 0; s2 < p.q_card[q]; ++s2) {
+            const int a = p.q_marg_off[q] + s2;
+            marg[(int64_t)a * ld_out + r] = acc(a);
+          }
+      }
     }
   }
   if (do_joint) {
@@ -592,18 +657,27 @@ __global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__res
   }
 }
 
-template <bool VL, bool AL>
-static void launch_rows_f(int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k, const double *v,
-                          const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n, int32_t mode,
-                          double *marg, double *joint, int64_t ldo, int32_t *map, double *gap, int32_t *err) {
+template <bool VL, bool AL, int MAXF>
+static void launch_rows_ff(int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k, const double *v,
+                           const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n, int32_t mode,
+                           double *marg, double *joint, int64_t ldo, int32_t *map, double *gap, int32_t *err) {
   if (max_nf <= 2)
-    hipLaunchKernelGGL((k_rows<VL, AL, 2>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, 2>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
   else if (max_nf <= 4)
-    hipLaunchKernelGGL((k_rows<VL, AL, 4>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
-  else if (max_nf <= 8)
-    hipLaunchKernelGGL((k_rows<VL, AL, 8>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, 4>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
   else
-    hipLaunchKernelGGL((k_rows<VL, AL, 16>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, (MAXF < 16 ? MAXF : 16)>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+}
+
+template <bool VL, bool AL>
+static void launch_rows_f(int max_f, int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
+                          const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n,
+                          int32_t mode, double *marg, double *joint, int64_t ldo, int32_t *map, double *gap,
+                          int32_t *err) {
+  if (max_f <= 8)
+    launch_rows_ff<VL, AL, 8>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+  else
+    launch_rows_ff<VL, AL, 16>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
 }
 
 // ============================================================================= C-ABI
@@ -855,6 +929,9 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
       ++nq_total;
     }
     k.comp_q_hi[c] = nq_total;
+    k.comp_simple[c] = (nq <= 1 && H == 1) ? 1 : 0;
+    k.comp_mstride[c] = nq == 1 ? pl->loop_map_stride[lb] : 0;
+    for (int f = fb; f < fe; ++f) k.comp_fstride[c][f - fb] = nq == 1 ? pl->fac_stride[f][lb] : 0;
     // per-entry tables, entries in C-order over [query dims..., hidden dims...] (last fastest)
     const int nl = le - lb;
     std::vector<int32_t> dig(nl, 0);
@@ -916,6 +993,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   if (!h) return fail(PGM_ENOMEM, "rows_plan_create: host allocation");
   h->k = k;
   h->max_nf = max_nf;
+  h->max_f = pl->n_fac;
   h->d_values = nullptr;
   h->d_tab = nullptr;
   hipError_t e = hipSuccess;
@@ -964,11 +1042,13 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   // LDS: CPT values (if they fit) + per-lane marginal accumulators
   const size_t kLds = 64 * 1024;
   size_t vals_bytes = (size_t)((k.n_values + 1) & ~1) * sizeof(double);
-  const bool vals_lds = vals_bytes <= 48 * 1024;
+  const bool vals_lds = vals_bytes <= 48 * 1024 && !(mode & PGM_ROWS_VALUES_GLOBAL);
   if (!vals_lds) vals_bytes = 0;
   int block = 256;
   bool acc_lds = false;
-  if (mode & PGM_ROWS_MARGINALS) {
+  bool need_acc = false;
+  for (int c = 0; c < k.n_comp; ++c) need_acc |= !k.comp_simple[c] && k.comp_nq[c] > 0;
+  if ((mode & PGM_ROWS_MARGINALS) && need_acc) {
     while (block > 64 && vals_bytes + (size_t)k.n_marg * block * sizeof(double) > kLds) block >>= 1;
     acc_lds = vals_bytes + (size_t)k.n_marg * block * sizeof(double) <= kLds;
     if (!acc_lds) block = 256;
@@ -981,13 +1061,13 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   const double *v = h->d_values;
   const int32_t *t = h->d_tab;
   if (vals_lds && acc_lds)
-    launch_rows_f<true, true>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<true, true>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
   else if (vals_lds)
-    launch_rows_f<true, false>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<true, false>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
   else if (acc_lds)
-    launch_rows_f<false, true>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<false, true>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
   else
-    launch_rows_f<false, false>(h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<false, false>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

@@ -88,6 +88,7 @@ class PatternPlan:
             raise ValueError("pattern does not fit the fused row kernel")
         self._handle = None
         self._handle_joint = None
+        self.extra_mode = 0  # tuning bits (N.ROWS_VALUES_GLOBAL)
         self.n_comp = len(comps) if self.kind == "fused" else None
 
     # ------------------------------------------------------------------ fused
@@ -244,7 +245,7 @@ class PatternPlan:
         return self._run_steps(codes, ld, row0, n_rows, out, err)
 
     def _mode(self, out):
-        mode = 0
+        mode = self.extra_mode
         if "marg" in out:
             mode |= N.ROWS_MARGINALS
         if "joint" in out:
