@@ -41,7 +41,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus):
+_BACKEND = "nccl"
+
+
+def dist_setup(n_gpus, backend="nccl"):
+    """One rank per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*).
+
+    backend "nccl" is RCCL on ROCm; "gloo" lets several ranks share one GPU for a rehearsal."""
+    global _BACKEND
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -50,8 +57,13 @@ def dist_setup(n_gpus):
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        _BACKEND = backend
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
         return dist, rank, world
     if torch.cuda.is_available():
         torch.cuda.set_device(0)
@@ -72,7 +84,7 @@ def max_over_ranks(dist, x):
         return x
     import torch
 
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if _BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -249,7 +261,8 @@ def bench_c3(args, dist, rank, world):
 
         barrier(dist)
         g0 = time.perf_counter()
-        gathered = gather_rows(out["marg"], rows * world, dist)
+        src = out["marg"] if _BACKEND == "nccl" else out["marg"].cpu()
+        gathered = gather_rows(src, rows * world, dist)
         torch.cuda.synchronize()
         result["gather_ms"] = (time.perf_counter() - g0) * 1e3
     return result
@@ -334,13 +347,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="after timing, gather marginals to rank 0 (RCCL)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     args = ap.parse_args()
     if args.rows is None:
         args.rows = 100_000 if args.workload == "c3" else 1000
     from pgmpy_amd.build import build
 
     build(verbose=False)
-    dist, rank, world = dist_setup(args.gpus)
+    dist, rank, world = dist_setup(args.gpus, args.dist_backend)
     if args.workload == "c3":
         res = bench_c3(args, dist, rank, world)
     elif args.workload == "c2":
