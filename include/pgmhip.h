@@ -105,6 +105,38 @@ int pgm_contract_workspace(const pgm_contract_desc *d, size_t *bytes);
 int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, double *C,
                  void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---------------------------------------------------------------- n-ary product
+ * C[keep] = prod_i X_i[keep . keep_s[i]]  (up to PGM_PRODN_MAX_OPS broadcast operands).
+ * factor_product's left fold of __mul__ (pgmpy/factors/base.py:20-66) in one pass, and the
+ * batched-BP clique update beta = psi x findings x prod(child messages) written once instead of
+ * once per incoming message (ExactInference.py:798-802).  ops is a HOST array of device pointers.
+ */
+#define PGM_PRODN_MAX_OPS 8
+enum pgm_prodn_kind {
+  PGM_PRODN_MUL = 0,   /* prod *= X_i                                                    */
+  PGM_PRODN_RATIO = 1, /* prod *= X_i / X_{i+1}, NaN -> 0 (sepset update sigma / mu,     */
+  PGM_PRODN_DEN = 2    /*   ExactInference.py:798-802 + DiscreteFactor.py:859-863)       */
+};
+typedef struct {
+  int32_t n_ops;
+  int32_t n_keep;
+  int32_t op_kind[PGM_PRODN_MAX_OPS];
+  int64_t keep_card[PGM_MAX_DIMS];
+  int64_t keep_sc[PGM_MAX_DIMS];
+  int64_t keep_s[PGM_PRODN_MAX_OPS][PGM_MAX_DIMS];
+} pgm_productn_desc;
+
+int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream);
+
+/* ---------------------------------------------------------------- HIP graphs
+ * Capture every launch issued on `stream` between begin and end into an executable graph, then
+ * replay it with one launch (compiled BP schedules, fixed-shape contraction plans).  The stream
+ * must not be the legacy default stream. */
+int pgm_graph_capture_begin(void *stream);
+int pgm_graph_capture_end(void *stream, void **graph_exec);
+int pgm_graph_launch(void *graph_exec, void *stream);
+int pgm_graph_destroy(void *graph_exec);
+
 /* ---------------------------------------------------------------- evidence gather
  * Batched DiscreteFactor.reduce: one evidence row per value of the batch
  * loop dim; the reduced variables' states come from the per-row codes.

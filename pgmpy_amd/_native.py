@@ -60,6 +60,23 @@ class ContractDesc(ctypes.Structure):
     ]
 
 
+PRODN_MAX_OPS = 8
+
+
+PRODN_MUL, PRODN_RATIO, PRODN_DEN = 0, 1, 2
+
+
+class ProductNDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_ops", ctypes.c_int32),
+        ("n_keep", ctypes.c_int32),
+        ("op_kind", ctypes.c_int32 * PRODN_MAX_OPS),
+        ("keep_card", _I64),
+        ("keep_sc", _I64),
+        ("keep_s", _I64 * PRODN_MAX_OPS),
+    ]
+
+
 class GatherDesc(ctypes.Structure):
     _fields_ = [
         ("n_keep", ctypes.c_int32),
@@ -124,6 +141,11 @@ _SIGS = {
     "pgm_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "pgm_contract_workspace": ([ctypes.POINTER(ContractDesc), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_product_n": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, _P], ctypes.c_int),
+    "pgm_graph_capture_begin": ([_P], ctypes.c_int),
+    "pgm_graph_capture_end": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_graph_launch": ([_P, _P], ctypes.c_int),
+    "pgm_graph_destroy": ([_P], ctypes.c_int),
     "pgm_gather": ([ctypes.POINTER(GatherDesc), _P, _P, _P, _P, _P], ctypes.c_int),
     "pgm_indicator": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P, _P],
                       ctypes.c_int),

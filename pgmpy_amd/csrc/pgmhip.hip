@@ -25,7 +25,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 2
+#define PGM_ABI_VERSION 4
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -80,7 +80,11 @@ __device__ __forceinline__ double max_nan(double a, double b) {
 
 struct ContractK {
   int32_t nk, nr, g_log2, n_split;
-  uint32_t n_out, n_red, red_chunk, _pad;
+  uint32_t n_out, n_red, red_chunk, row_mode;  // red_chunk: reduction-OUTER indices per split
+  uint32_t n_ro, ri_card;                       // reduction = n_ro outer x ri_card innermost
+  int64_t ri_sa, ri_sb;                         // strides of the innermost reduction dim
+  uint32_t ri_chunk, ri_nb;                     // row mode: innermost dim cut in ri_nb chunks of ri_chunk
+  uint32_t n_v, _pad2;                          // row mode: virtual reduction-outer count n_ro * ri_nb
   FDiv kdiv[KMAX];
   int64_t ksa[KMAX], ksb[KMAX], ksc[KMAX];
   FDiv rdiv[KMAX];
@@ -112,6 +116,21 @@ __device__ __forceinline__ double red_op(double acc, double v) {
   return v;
 }
 
+// reduction-outer index -> offsets (wave-uniform when ro is)
+__device__ __forceinline__ void decode_ro(const ContractK &p, uint32_t ro, int64_t &ra, int64_t &rb) {
+  ra = 0;
+  rb = 0;
+  for (int k = p.nr - 2; k >= 0; --k) {
+    const uint32_t q = fdiv(ro, p.rdiv[k]);
+    const uint32_t dg = ro - q * p.rdiv[k].d;
+    ra += (int64_t)dg * p.rsa[k];
+    rb += (int64_t)dg * p.rsb[k];
+    ro = q;
+  }
+}
+
+// Flat mode: G lanes cooperate on one output (any keep layout); lanes stride the innermost
+// reduction dim, the reduction-outer index is walked wave-uniformly.
 template <int CMB, int RED>
 __global__ __launch_bounds__(256) void k_contract(const ContractK p, const double *__restrict__ A,
                                                   const double *__restrict__ B, double *__restrict__ C,
@@ -121,8 +140,8 @@ __global__ __launch_bounds__(256) void k_contract(const ContractK p, const doubl
   const uint32_t lane_g = (uint32_t)tid & (G - 1);
   const uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) >> p.g_log2;
   const uint32_t split = blockIdx.y;
-  const uint32_t e0 = split * p.red_chunk;
-  const uint32_t e1 = min(p.n_red, e0 + p.red_chunk);
+  const uint32_t r0 = split * p.red_chunk;
+  const uint32_t r1 = min(p.n_ro, r0 + p.red_chunk);
   for (uint64_t out = tid >> p.g_log2; out < p.n_out; out += ngroups) {
     int64_t oa = 0, ob = 0, oc = 0;
     uint32_t idx = (uint32_t)out;
@@ -135,22 +154,19 @@ __global__ __launch_bounds__(256) void k_contract(const ContractK p, const doubl
       idx = q;
     }
     double acc = red_init<RED>();
-    for (uint32_t e = e0 + lane_g; e < e1; e += G) {
-      int64_t ra = oa, rb = ob;
-      uint32_t r = e;
-      for (int k = p.nr - 1; k >= 0; --k) {
-        const uint32_t q = fdiv(r, p.rdiv[k]);
-        const uint32_t dg = r - q * p.rdiv[k].d;
-        ra += (int64_t)dg * p.rsa[k];
-        if constexpr (CMB != PGM_COMBINE_COPY) rb += (int64_t)dg * p.rsb[k];
-        r = q;
+    for (uint32_t ro = r0; ro < r1; ++ro) {
+      int64_t ra, rb;
+      decode_ro(p, ro, ra, rb);
+      const double *a = A + oa + ra;
+      const double *b = B + ob + rb;
+      for (uint32_t ri = lane_g; ri < p.ri_card; ri += G) {
+        double v;
+        if constexpr (CMB == PGM_COMBINE_COPY)
+          v = a[(int64_t)ri * p.ri_sa];
+        else
+          v = combine<CMB>(a[(int64_t)ri * p.ri_sa], b[(int64_t)ri * p.ri_sb]);
+        acc = red_op<RED>(acc, v);
       }
-      double v;
-      if constexpr (CMB == PGM_COMBINE_COPY)
-        v = A[ra];
-      else
-        v = combine<CMB>(A[ra], B[rb]);
-      acc = red_op<RED>(acc, v);
     }
     if constexpr (RED != PGM_RED_NONE) {
       for (uint32_t off = G >> 1; off > 0; off >>= 1) acc = red_op<RED>(acc, __shfl_xor(acc, (int)off, 64));
@@ -160,6 +176,101 @@ __global__ __launch_bounds__(256) void k_contract(const ContractK p, const doubl
         C[oc] = acc;
       else
         ws[(uint64_t)split * p.n_out + out] = acc;
+    }
+  }
+}
+
+// Row mode: the innermost keep dim runs across the lanes (coalesced when it is innermost in the
+// operands, e.g. the evidence-row axis), the outer keep index and the reduction-outer index are
+// wave-uniform (scalar decode), the innermost reduction dim is walked by increments.
+template <int CMB>
+__device__ __forceinline__ double ld_combine(const double *a, const double *b, int64_t ia, int64_t ib) {
+  if constexpr (CMB == PGM_COMBINE_COPY)
+    return a[ia];
+  else
+    return combine<CMB>(a[ia], b[ib]);
+}
+
+// Row mode: the innermost keep dim runs across the lanes (coalesced when it is innermost in the
+// operands, e.g. the evidence-row axis), the outer keep index and the reduction-outer index are
+// wave-uniform (scalar decode), the innermost reduction dim is walked by increments.  Loops are
+// unrolled 4-wide with independent accumulators so each lane keeps 4-8 loads in flight.
+template <int CMB, int RED>
+__global__ __launch_bounds__(256) void k_contract_rows(const ContractK p, const double *__restrict__ A,
+                                                       const double *__restrict__ B, double *__restrict__ C,
+                                                       double *__restrict__ ws) {
+  // grid: x-blocks stride the innermost keep dim, y-blocks stride the outer keep index, z = split.
+  // A block decodes an outer index once (wave-uniform, scalar) and reuses it for all its rows.
+  const int kx = p.nk - 1;
+  const uint32_t NX = p.kdiv[kx].d;
+  const int64_t sxa = p.ksa[kx], sxb = p.ksb[kx], sxc = p.ksc[kx];
+  const uint32_t n_outer = p.n_out / NX;
+  const uint32_t xstep = gridDim.x * blockDim.x;
+  auto decode_o = [&](uint32_t idx, int64_t &oa, int64_t &ob, int64_t &oc) {
+    oa = ob = oc = 0;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      if constexpr (CMB != PGM_COMBINE_COPY) ob += (int64_t)dg * p.ksb[k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+  };
+  if constexpr (RED == PGM_RED_NONE) {
+    for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+      int64_t oa, ob, oc;
+      decode_o(o, oa, ob, oc);
+      uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+      for (; x + 3 * xstep < NX; x += 4 * xstep) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t xx = x + u * xstep;
+          v[u] = ld_combine<CMB>(A, B, oa + xx * sxa, ob + xx * sxb);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) C[oc + (int64_t)(x + u * xstep) * sxc] = v[u];
+      }
+      for (; x < NX; x += xstep) C[oc + (int64_t)x * sxc] = ld_combine<CMB>(A, B, oa + (int64_t)x * sxa, ob + (int64_t)x * sxb);
+    }
+    return;
+  }
+  const uint32_t split = blockIdx.z;
+  const uint32_t v0 = split * p.red_chunk;
+  const uint32_t v1 = min(p.n_v, v0 + p.red_chunk);
+  const uint32_t nb = p.ri_nb, CH = p.ri_chunk, RI = p.ri_card;
+  for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+    int64_t oa, ob, oc;
+    decode_o(o, oa, ob, oc);
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < NX; x += xstep) {
+      const double *a = A + oa + (int64_t)x * sxa;
+      const double *b = B + ob + (int64_t)x * sxb;
+      double acc0 = red_init<RED>(), acc1 = acc0, acc2 = acc0, acc3 = acc0;
+      for (uint32_t v = v0; v < v1; ++v) {
+        const uint32_t ro = nb == 1 ? v : v / nb;
+        const uint32_t bk = v - ro * nb;
+        int64_t ra, rb;
+        decode_ro(p, ro, ra, rb);
+        const uint32_t ri1 = min(RI, (bk + 1) * CH);
+        uint32_t ri = bk * CH;
+        for (; ri + 4 <= ri1; ri += 4) {
+          const double w0 = ld_combine<CMB>(a, b, ra + (int64_t)ri * p.ri_sa, rb + (int64_t)ri * p.ri_sb);
+          const double w1 = ld_combine<CMB>(a, b, ra + (int64_t)(ri + 1) * p.ri_sa, rb + (int64_t)(ri + 1) * p.ri_sb);
+          const double w2 = ld_combine<CMB>(a, b, ra + (int64_t)(ri + 2) * p.ri_sa, rb + (int64_t)(ri + 2) * p.ri_sb);
+          const double w3 = ld_combine<CMB>(a, b, ra + (int64_t)(ri + 3) * p.ri_sa, rb + (int64_t)(ri + 3) * p.ri_sb);
+          acc0 = red_op<RED>(acc0, w0);
+          acc1 = red_op<RED>(acc1, w1);
+          acc2 = red_op<RED>(acc2, w2);
+          acc3 = red_op<RED>(acc3, w3);
+        }
+        for (; ri < ri1; ++ri) acc0 = red_op<RED>(acc0, ld_combine<CMB>(a, b, ra + (int64_t)ri * p.ri_sa, rb + (int64_t)ri * p.ri_sb));
+      }
+      const double acc = red_op<RED>(red_op<RED>(acc0, acc1), red_op<RED>(acc2, acc3));
+      if (p.n_split == 1)
+        C[oc + (int64_t)x * sxc] = acc;
+      else
+        ws[(uint64_t)split * p.n_out + (uint64_t)o * NX + x] = acc;
     }
   }
 }
@@ -272,31 +383,61 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
   k.n_out = (uint32_t)n_out;
   k.n_red = (uint32_t)n_red;
   L.empty = (n_out == 0);
-  // work decomposition: G lanes cooperate on one output, S splits of the reduction over blocks
+  // reduction = outer (decoded, wave-uniform) x innermost (walked by increments)
+  if (rd.n > 0) {
+    k.ri_card = (uint32_t)rd.card[rd.n - 1];
+    k.ri_sa = rd.s[0][rd.n - 1];
+    k.ri_sb = rd.s[1][rd.n - 1];
+  } else {
+    k.ri_card = 1;
+    k.ri_sa = k.ri_sb = 0;
+  }
+  k.n_ro = (uint32_t)(n_red / k.ri_card);
+  const bool has_red = d->reduce != PGM_RED_NONE && n_red > 1;
+  const uint64_t NX = kd.n > 0 ? (uint64_t)kd.card[kd.n - 1] : 1;
+  // row mode when the innermost output dim fills waves and no lane-parallel reduction is needed
+  const bool red_contig = rd.n > 0 && rd.s[0][rd.n - 1] == 1;
+  k.row_mode = (kd.n > 0 && NX >= 64 && !(has_red && red_contig && NX < 256 && n_out < kTargetThreads)) ? 1 : 0;
   int g_log2 = 0;
   uint32_t n_split = 1;
-  if (d->reduce != PGM_RED_NONE && n_red > 1) {
-    const bool red_contig = rd.n > 0 && rd.s[0][rd.n - 1] == 1;
-    const bool keep_contig = kd.n > 0 && kd.s[0][kd.n - 1] == 1;
-    if (!(keep_contig && !red_contig)) {
-      // lanes stride the reduction (coalesced when the reduced axis is innermost)
-      while (g_log2 < 6 && (n_out << g_log2) < kTargetThreads && (1ull << (g_log2 + 1)) <= n_red) ++g_log2;
+  if (k.row_mode) {
+    const uint64_t n_outer = n_out / NX;
+    const uint64_t xchunks = (NX + 255) / 256;
+    const uint64_t target_blocks = 2048;
+    uint64_t gy = std::min<uint64_t>(n_outer, 65535);
+    uint64_t gx = std::min<uint64_t>(xchunks, std::max<uint64_t>(1, target_blocks / gy));
+    k.ri_chunk = k.ri_card;
+    k.ri_nb = 1;
+    if (has_red && gx * gy < target_blocks / 2) {
+      // few outputs and a long reduction: split it (virtual outer index = (ro, chunk of the inner dim))
+      const uint64_t want = (target_blocks / 2 + gx * gy - 1) / (gx * gy);
+      if (k.n_ro < want && k.ri_card >= 64) {
+        const uint64_t nb = std::min<uint64_t>((want + k.n_ro - 1) / k.n_ro, k.ri_card / 16);
+        k.ri_nb = (uint32_t)std::max<uint64_t>(nb, 1);
+        k.ri_chunk = (uint32_t)((k.ri_card + k.ri_nb - 1) / k.ri_nb);
+        k.ri_nb = (k.ri_card + k.ri_chunk - 1) / k.ri_chunk;
+      }
+      n_split = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(want, (uint64_t)k.n_ro * k.ri_nb), 256);
     }
-    const uint64_t par = n_out << g_log2;
-    if (par < kTargetThreads / 4) {
-      uint64_t want = (kTargetThreads / 4 + par - 1) / par;
-      uint64_t max_split = std::max<uint64_t>(1, n_red / ((1ull << g_log2) * 16));
-      n_split = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(want, max_split), 1024);
-      if (n_split < 1) n_split = 1;
+    k.n_v = k.n_ro * k.ri_nb;
+    L.grid = dim3((unsigned)gx, (unsigned)gy, n_split);
+  } else {
+    if (has_red) {
+      while (g_log2 < 6 && (n_out << g_log2) < kTargetThreads && (1ull << (g_log2 + 1)) <= k.ri_card) ++g_log2;
+      const uint64_t par = n_out << g_log2;
+      if (par < kTargetThreads / 4 && k.n_ro > 1) {
+        uint64_t want = (kTargetThreads / 4 + par - 1) / par;
+        n_split = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(want, k.n_ro), 1024);
+      }
     }
+    const uint64_t threads = n_out << g_log2;
+    uint64_t blocks = (threads + 255) / 256;
+    blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 65535);
+    L.grid = dim3((unsigned)blocks, n_split, 1);
   }
   k.g_log2 = g_log2;
   k.n_split = (int32_t)n_split;
-  k.red_chunk = (uint32_t)((n_red + n_split - 1) / n_split);
-  const uint64_t threads = n_out << g_log2;
-  uint64_t blocks = (threads + 255) / 256;
-  blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 65535);
-  L.grid = dim3((unsigned)blocks, n_split, 1);
+  k.red_chunk = k.row_mode ? (uint32_t)((k.n_v + n_split - 1) / n_split) : (uint32_t)((k.n_ro + n_split - 1) / n_split);
   L.ws_doubles = n_split > 1 ? (uint64_t)n_split * n_out : 0;
   return PGM_OK;
 }
@@ -304,7 +445,10 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
 template <int CMB, int RED>
 static void launch_contract_t(const ContractLaunch &L, const double *A, const double *B, double *C, double *ws,
                               hipStream_t s) {
-  hipLaunchKernelGGL((k_contract<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
+  if (L.k.row_mode)
+    hipLaunchKernelGGL((k_contract_rows<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
+  else
+    hipLaunchKernelGGL((k_contract<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
   if (L.k.n_split > 1) {
     uint64_t blocks = std::min<uint64_t>((L.k.n_out + 255) / 256, 65535);
     hipLaunchKernelGGL((k_contract_final<RED>), dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s,
@@ -319,6 +463,94 @@ static void launch_contract_c(int red, const ContractLaunch &L, const double *A,
     case PGM_RED_NONE: launch_contract_t<CMB, PGM_RED_NONE>(L, A, B, C, ws, s); break;
     case PGM_RED_SUM: launch_contract_t<CMB, PGM_RED_SUM>(L, A, B, C, ws, s); break;
     default: launch_contract_t<CMB, PGM_RED_MAX>(L, A, B, C, ws, s); break;
+  }
+}
+
+// ----------------------------------------------------------------------------- n-ary product
+#define PMAX PGM_PRODN_MAX_OPS
+struct ProdNK {
+  int32_t n_ops, nk;
+  int32_t kind[PMAX];
+  uint32_t n_out, row_mode;
+  FDiv kdiv[KMAX];
+  int64_t ksc[KMAX];
+  int64_t ks[PMAX][KMAX];
+  const double *ops[PMAX];
+};
+
+template <int NOPS>
+__global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__restrict__ C) {
+  if (p.row_mode) {
+    const int kx = p.nk - 1;
+    const uint32_t NX = p.kdiv[kx].d;
+    const uint32_t n_outer = p.n_out / NX;
+    const uint32_t xstep = gridDim.x * blockDim.x;
+    for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+      // outer decode once per block and outer index (wave-uniform), reused for all rows
+      int64_t off[NOPS];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] = 0;
+      int64_t oc = 0;
+      uint32_t idx = o;
+      for (int k = kx - 1; k >= 0; --k) {
+        const uint32_t q = fdiv(idx, p.kdiv[k]);
+        const uint32_t dg = idx - q * p.kdiv[k].d;
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+        oc += (int64_t)dg * p.ksc[k];
+        idx = q;
+      }
+      const double *op[NOPS];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) op[i] = i < p.n_ops ? p.ops[i] + off[i] : nullptr;
+      for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < NX; x += xstep) {
+        double prod = 1.0;
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          if (i < p.n_ops) {
+            const double v = op[i][(int64_t)x * p.ks[i][kx]];
+            if (p.kind[i] == PGM_PRODN_MUL) {
+              prod *= v;
+            } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
+              const double r = v / op[i + 1][(int64_t)x * p.ks[i + 1][kx]];
+              prod *= (r != r) ? 0.0 : r;
+            }
+          }
+        }
+        C[oc + (int64_t)x * p.ksc[kx]] = prod;
+      }
+    }
+    return;
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t out = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; out < p.n_out; out += stride) {
+    uint32_t idx = (uint32_t)out;
+    int64_t off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    int64_t oc = 0;
+    for (int k = p.nk - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    double prod = 1.0;
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) {
+      if (i < p.n_ops) {
+        const double v = p.ops[i][off[i]];
+        if (p.kind[i] == PGM_PRODN_MUL) {
+          prod *= v;
+        } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
+          const double r = v / p.ops[i + 1][off[i + 1]];
+          prod *= (r != r) ? 0.0 : r;
+        }
+      }
+    }
+    C[oc] = prod;
   }
 }
 
@@ -808,6 +1040,108 @@ int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, d
     default: launch_contract_c<PGM_COMBINE_COPY>(d->reduce, L, A, B, C, ws, s); break;
   }
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream) {
+  if (!d || !ops || !C) return fail(PGM_EINVAL, "product_n: null argument");
+  if (d->n_ops < 1 || d->n_ops > PMAX || d->n_keep < 0 || d->n_keep > PGM_MAX_DIMS)
+    return fail(PGM_EINVAL, "product_n: n_ops %d (1..%d) / n_keep %d", d->n_ops, PMAX, d->n_keep);
+  // coalesce: one Dims per group of up to 3 operand strides is not enough -> do it by hand
+  int n = 0;
+  int64_t card[PGM_MAX_DIMS], sc[PGM_MAX_DIMS], so[PMAX][PGM_MAX_DIMS];
+  uint64_t n_out = 1;
+  for (int i = 0; i < d->n_keep; ++i) {
+    if (d->keep_card[i] <= 0) return fail(PGM_EINVAL, "product_n: keep_card[%d] <= 0", i);
+    n_out *= (uint64_t)d->keep_card[i];
+    if (d->keep_card[i] == 1) continue;
+    if (n > 0) {
+      bool ok = sc[n - 1] == d->keep_card[i] * d->keep_sc[i];
+      for (int t = 0; t < d->n_ops; ++t) ok = ok && so[t][n - 1] == d->keep_card[i] * d->keep_s[t][i];
+      if (ok) {
+        card[n - 1] *= d->keep_card[i];
+        sc[n - 1] = d->keep_sc[i];
+        for (int t = 0; t < d->n_ops; ++t) so[t][n - 1] = d->keep_s[t][i];
+        continue;
+      }
+    }
+    card[n] = d->keep_card[i];
+    sc[n] = d->keep_sc[i];
+    for (int t = 0; t < d->n_ops; ++t) so[t][n] = d->keep_s[t][i];
+    ++n;
+  }
+  if (n_out >= (1ull << 31)) return fail(PGM_EINVAL, "product_n: output too large");
+  if (n > KMAX) return fail(PGM_EINVAL, "product_n: %d dims after coalescing (limit %d)", n, KMAX);
+  ProdNK k;
+  memset(&k, 0, sizeof k);
+  k.n_ops = d->n_ops;
+  k.nk = n;
+  k.n_out = (uint32_t)n_out;
+  for (int i = 0; i < n; ++i) {
+    k.kdiv[i] = make_fdiv((uint32_t)card[i]);
+    k.ksc[i] = sc[i];
+    for (int t = 0; t < d->n_ops; ++t) k.ks[t][i] = so[t][i];
+  }
+  for (int t = 0; t < d->n_ops; ++t) {
+    if (!ops[t]) return fail(PGM_EINVAL, "product_n: null operand %d", t);
+    k.ops[t] = ops[t];
+    k.kind[t] = d->op_kind[t];
+    if (d->op_kind[t] < 0 || d->op_kind[t] > 2) return fail(PGM_EINVAL, "product_n: bad op_kind[%d]", t);
+    if (d->op_kind[t] == PGM_PRODN_RATIO && (t + 1 >= d->n_ops || d->op_kind[t + 1] != PGM_PRODN_DEN))
+      return fail(PGM_EINVAL, "product_n: a RATIO operand must be followed by its DEN operand");
+    if (d->op_kind[t] == PGM_PRODN_DEN && (t == 0 || d->op_kind[t - 1] != PGM_PRODN_RATIO))
+      return fail(PGM_EINVAL, "product_n: a DEN operand must follow a RATIO operand");
+  }
+  const uint64_t NX = n > 0 ? (uint64_t)card[n - 1] : 1;
+  k.row_mode = (n > 0 && NX >= 64) ? 1 : 0;
+  dim3 grid;
+  if (k.row_mode) {
+    const uint64_t xchunks = (NX + 255) / 256, n_outer = n_out / NX;
+    const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
+    const uint64_t gx = std::min<uint64_t>(xchunks, std::max<uint64_t>(1, 2048 / gy));
+    grid = dim3((unsigned)gx, (unsigned)gy, 1);
+  } else {
+    grid = dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>((n_out + 255) / 256, 1), 65535), 1, 1);
+  }
+  hipStream_t s = S(stream);
+  switch (d->n_ops <= 2 ? 2 : d->n_ops <= 4 ? 4 : 8) {
+    case 2: hipLaunchKernelGGL((k_productn<2>), grid, dim3(256), 0, s, k, C); break;
+    case 4: hipLaunchKernelGGL((k_productn<4>), grid, dim3(256), 0, s, k, C); break;
+    default: hipLaunchKernelGGL((k_productn<8>), grid, dim3(256), 0, s, k, C); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_graph_capture_begin(void *stream) {
+  if (!stream) return fail(PGM_EINVAL, "graph capture needs a non-default stream");
+  HIP_TRY(hipStreamBeginCapture(S(stream), hipStreamCaptureModeRelaxed));
+  return PGM_OK;
+}
+
+int pgm_graph_capture_end(void *stream, void **graph_exec) {
+  if (!graph_exec) return fail(PGM_EINVAL, "null pointer");
+  hipGraph_t g = nullptr;
+  HIP_TRY(hipStreamEndCapture(S(stream), &g));
+  hipGraphExec_t e = nullptr;
+  hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (err != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(PGM_EDEVICE, "hipGraphInstantiate: %s", hipGetErrorString(err));
+  }
+  *graph_exec = (void *)e;
+  return PGM_OK;
+}
+
+int pgm_graph_launch(void *graph_exec, void *stream) {
+  if (!graph_exec) return fail(PGM_EINVAL, "null graph");
+  HIP_TRY(hipGraphLaunch((hipGraphExec_t)graph_exec, S(stream)));
+  return PGM_OK;
+}
+
+int pgm_graph_destroy(void *graph_exec) {
+  if (graph_exec) HIP_TRY(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return PGM_OK;
 }
 

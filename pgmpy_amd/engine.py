@@ -69,12 +69,12 @@ def scalar(x):
     return to_device(np.array(x, dtype=np.float64))
 
 
-def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
-    """C[out_labels] = REDUCE_{labels not in out} COMBINE(A[la], B[lb]).
+def prepare_contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
+    """Build (descriptor, out, workspace, ws_bytes) for C[out_labels] = REDUCE COMBINE(A, B).
 
     A/B: device fp64 tensors (any strides), la/lb: one label per axis (B may be
-    None for combine="copy").  Labels absent from an operand broadcast.  Returns
-    the output tensor (C-order over out_labels unless `out` is given)."""
+    None for combine="copy").  Labels absent from an operand broadcast (stride 0);
+    labels absent from out_labels are reduced."""
     L = N.lib()
     la = list(la)
     lb = list(lb) if B is not None else []
@@ -123,13 +123,62 @@ def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
         d.red_sb[i] = st(B, lb, l)
     ws_bytes = ctypes.c_size_t(0)
     N.check(L.pgm_contract_workspace(ctypes.byref(d), ctypes.byref(ws_bytes)), "contract")
-    ws = None
-    if ws_bytes.value:
-        ws = empty([ws_bytes.value // 8])
-    N.check(L.pgm_contract(ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), ws_bytes.value,
-                           N.stream_handle()), "contract")
+    ws = empty([ws_bytes.value // 8]) if ws_bytes.value else None
+    return d, out, ws, ws_bytes.value
+
+
+def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
+    """C[out_labels] = REDUCE_{labels not in out} COMBINE(A[la], B[lb]) (one pgm_contract call).
+
+    Returns the output tensor (C-order over out_labels unless `out` is given)."""
+    L = N.lib()
+    d, out, ws, wsb = prepare_contract(A, la, B, lb, out_labels, reduce, combine, out)
+    N.check(L.pgm_contract(ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb, N.stream_handle()),
+            "contract")
     # ws may be freed here: torch's caching allocator is stream-ordered, so its memory is only
     # handed to work queued after these kernels on the same stream.
+    return out
+
+
+def prepare_product_n(operands, out_labels, out=None, kinds=None):
+    """Descriptor for C[out_labels] = prod_i X_i (broadcast, no reduction), up to 8 operands.
+
+    kinds: per operand N.PRODN_MUL (default) or a N.PRODN_RATIO / N.PRODN_DEN pair
+    (X_i / X_{i+1} with NaN -> 0)."""
+    N.lib()
+    out_labels = list(out_labels)
+    if not 1 <= len(operands) <= N.PRODN_MAX_OPS:
+        raise ValueError(f"product_n takes 1..{N.PRODN_MAX_OPS} operands")
+    card = {}
+    for t, ls in operands:
+        if len(ls) != t.dim():
+            raise ValueError("label count does not match tensor rank")
+        for d, l in enumerate(ls):
+            c = int(t.shape[d])
+            if card.setdefault(l, c) != c:
+                raise ValueError(f"cardinality mismatch for {l!r}")
+            if l not in out_labels:
+                raise ValueError(f"label {l!r} would need a reduction")
+    if out is None:
+        out = empty([card[l] for l in out_labels])
+    d = N.ProductNDesc()
+    d.n_ops = len(operands)
+    d.n_keep = len(out_labels)
+    for i, k in enumerate(kinds or []):
+        d.op_kind[i] = int(k)
+    for i, l in enumerate(out_labels):
+        d.keep_card[i] = card[l]
+        d.keep_sc[i] = int(out.stride(i))
+        for t_i, (t, ls) in enumerate(operands):
+            d.keep_s[t_i][i] = int(t.stride(list(ls).index(l))) if l in ls else 0
+    ptrs = (ctypes.c_void_p * len(operands))(*[t.data_ptr() for t, _ in operands])
+    return d, ptrs, out
+
+
+def product_n(operands, out_labels, out=None, kinds=None):
+    L = N.lib()
+    d, ptrs, out = prepare_product_n(operands, out_labels, out, kinds)
+    N.check(L.pgm_product_n(ctypes.byref(d), ptrs, N.ptr(out), N.stream_handle()), "product_n")
     return out
 
 

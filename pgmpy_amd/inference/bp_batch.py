@@ -2,29 +2,35 @@
 
 Each clique belief is a device tensor [clique vars..., ROW] with the evidence
 row innermost (stride 1), so every message kernel is coalesced along rows
-regardless of which clique axes it reduces.  Schedule = one collect
-(leaves -> root) and one distribute (root -> leaves) sweep of
-Lauritzen-Spiegelhalter belief update, the fixed point of the reference's
-_calibrate_junction_tree (pgmpy/inference/ExactInference.py:770-895):
+whatever clique axes it reduces.  The schedule is one collect (leaves -> root)
+and one distribute (root -> leaves) sweep of Lauritzen-Spiegelhalter belief
+update — the fixed point of the reference's _calibrate_junction_tree
+(pgmpy/inference/ExactInference.py:770-895):
 
-  collect   sigma = marg_{C_c \\ S}(beta_c);  beta_p *= sigma;            mu = sigma
-  distribute sigma = marg_{C_p \\ S}(beta_p);  beta_c *= sigma / mu (0/0->0); mu = sigma
+  collect    beta_c = psi_c x findings_c x prod_{children k} sigma_k   (one n-ary product, written once)
+             sigma_c = marg_{C_c \\ S}(beta_c)                         (message to the parent; mu = sigma)
+  distribute sigma' = marg_{C_p \\ S}(beta_p);  beta_c *= sigma' / mu (0/0 -> 0, DiscreteFactor.py:859-863)
 
-Findings enter as 0/1 indicators (pgm_indicator) multiplied into the first
-clique that holds each observed variable.
-Algorithmic bytes per calibration: 8 (4 sum|C| + 4 sum|S|).
+Findings enter as 0/1 indicators (pgm_indicator) of the first clique holding
+each observed variable.  A compiled schedule (per batch size and evidence
+columns) is a pgmpy_amd.program.Program: all buffers preallocated, replayed as
+one HIP graph.  Algorithmic bytes per calibration: 8 (4 sum|C| + 4 sum|S|)
+(SURVEY.md §8(d)).
 """
 import numpy as np
 
+from .. import _native as N
 from .. import engine as E
+from ..program import Program
 
 
 class BatchedCalibration:
-    def __init__(self, bjt, beliefs, seps, n_rows):
+    def __init__(self, bjt, beliefs, seps, n_rows, marginals=None):
         self.bjt = bjt
         self.beliefs = beliefs  # clique -> (tensor [labels..., ROW], labels)
-        self.seps = seps
+        self.seps = seps        # (parent, child) -> (tensor [sep..., ROW], sep labels)
         self.n_rows = n_rows
+        self._marg = marginals or {}
 
     def clique_belief(self, clique, row):
         """Host copy of one row's belief, axes in the clique tuple's order (C-order flat)."""
@@ -34,22 +40,96 @@ class BatchedCalibration:
 
     def marginal(self, var):
         """[n_rows, card] normalized marginal of `var` per row."""
+        if var in self._marg:
+            return E.to_host(self._marg[var]).T.copy()
         c = self.bjt.var_clique[var]
         t, ls = self.beliefs[c]
         m = E.contract(t, ls + [E.ROW], None, None, [E.ROW, var], reduce="sum", combine="copy")
         E.normalize_rows_(m, [E.ROW, var], E.ROW)
         return E.to_host(m)
 
-    def marginals_device(self, variables=None):
-        """{var: device [card, n_rows]} normalized marginals."""
-        out = {}
-        for var in (variables or self.bjt.variables):
-            c = self.bjt.var_clique[var]
-            t, ls = self.beliefs[c]
-            m = E.contract(t, ls + [E.ROW], None, None, [var, E.ROW], reduce="sum", combine="copy")
-            E.normalize_rows_(m, [var, E.ROW], E.ROW)
-            out[var] = m
-        return out
+    def marginals_device(self):
+        return dict(self._marg)
+
+
+class BPSchedule:
+    """A compiled batched calibration for fixed (n_rows, evidence columns, operation)."""
+
+    def __init__(self, bjt, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True):
+        import torch
+
+        self.bjt = bjt
+        self.n_rows = n_rows
+        self.ev_vars = list(ev_vars)
+        red = "sum" if operation == "marginalize" else "max"
+        R = E.ROW
+        prog = Program()
+        dev = E.device()
+        self.codes = torch.empty((max(1, len(self.ev_vars)), n_rows), dtype=torch.uint8, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        ev_by_clique = {}
+        for j, v in enumerate(self.ev_vars):
+            ev_by_clique.setdefault(bjt.var_clique[v], []).append((j, v))
+        children = {c: [] for c in bjt.cliques}
+        parent = {}
+        for p, c in bjt.order:
+            children[p].append(c)
+            parent[c] = p
+        beliefs, msgs, seps = {}, {}, {}
+        # collect: post-order (children before parents)
+        post = [c for _, c in reversed(bjt.order)] + [bjt.root]
+        for c in post:
+            t, ls = bjt.pot[c]
+            ops = [(t, ls)]
+            for j, v in ev_by_clique.get(c, []):
+                ops.append((prog.indicator(self.codes[j], bjt.card[v], n_rows, err=self.err), [v, R]))
+            for k in children[c]:
+                ops.append(msgs[k])
+            if len(ops) == 1:
+                ops.append((E.to_device(np.ones(n_rows)), [R]))  # broadcast psi over the rows
+            beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
+            if c in parent:
+                sep = [v for v in ls if v in parent[c]]
+                msgs[c] = (prog.contract(beliefs[c][0], ls + [R], None, None, sep + [R], reduce=red,
+                                         combine="copy"), sep + [R])
+        # distribute: root -> leaves
+        for p, c in bjt.order:
+            tp, lp = beliefs[p]
+            tc, lc = beliefs[c]
+            mu, sl = msgs[c]
+            sigma = prog.contract(tp, lp + [R], None, None, sl, reduce=red, combine="copy")
+            # beta_c *= sigma / mu (0/0 -> 0) in one pass
+            prog.product_n([(tc, lc + [R]), (sigma, sl), (mu, sl)], lc + [R], out=tc,
+                           kinds=[N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN])
+            seps[(p, c)] = (sigma, sl[:-1])
+        marg = {}
+        if marginals:
+            for var in bjt.variables:
+                t, ls = beliefs[bjt.var_clique[var]]
+                m = prog.contract(t, ls + [R], None, None, [var, R], reduce="sum", combine="copy")
+                z = prog.contract(m, [var, R], None, None, [R], reduce="sum", combine="copy")
+                prog.contract(m, [var, R], z, [R], [var, R], combine="div_raw", out=m)
+                marg[var] = m
+        self.prog = prog
+        self.beliefs = beliefs
+        self.seps = seps
+        self.marg = marg
+        if graph:
+            prog.capture()
+
+    def run(self, codes=None):
+        """codes: device uint8 [len(ev_vars), n_rows] (copied into the schedule's input buffer)."""
+        from .. import _native as N
+
+        L = N.lib()
+        s = N.stream_handle()
+        N.check(L.pgm_memset(N.ptr(self.err), 0, 4, s), "memset")
+        if codes is not None and len(self.ev_vars):
+            if tuple(codes.shape) != tuple(self.codes.shape) or not codes.is_contiguous():
+                raise ValueError(f"codes must be a contiguous uint8 [{len(self.ev_vars)}, {self.n_rows}] tensor")
+            N.check(L.pgm_memcpy_d2d(N.ptr(self.codes), N.ptr(codes), codes.numel(), s), "memcpy_d2d")
+        self.prog.run()
+        return BatchedCalibration(self.bjt, self.beliefs, self.seps, self.n_rows, self.marg)
 
 
 class BatchedJunctionTree:
@@ -75,6 +155,7 @@ class BatchedJunctionTree:
                 self.var_clique.setdefault(v, c)
         self.variables = sorted(self.var_clique, key=str)
         self.sizes = {c: int(np.prod([self.card[v] for v in c])) for c in self.cliques}
+        self._schedules = {}
 
     def bytes_per_calibration(self):
         """SURVEY.md §8(d) C4 algorithmic bytes: 8 (4 sum|C| + 4 sum|S|)."""
@@ -83,39 +164,21 @@ class BatchedJunctionTree:
             s += int(np.prod([self.card[v] for v in c if v in p]))
         return 8 * (4 * sum(self.sizes.values()) + 4 * s)
 
-    def calibrate_codes(self, codes, ev_vars, n_rows, operation="marginalize", err=None):
+    def schedule(self, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True):
+        key = (n_rows, tuple(ev_vars), operation, marginals, graph)
+        sch = self._schedules.get(key)
+        if sch is None:
+            sch = BPSchedule(self, n_rows, ev_vars, operation, marginals, graph)
+            self._schedules[key] = sch
+        return sch
+
+    def calibrate_codes(self, codes, ev_vars, n_rows, operation="marginalize", err=None, marginals=False):
         """codes: device uint8 [len(ev_vars), n_rows] (255 = unobserved)."""
-        red = "sum" if operation == "marginalize" else "max"
-        R = E.ROW
-        ones = E.to_device(np.ones(n_rows))
-        beliefs = {}
-        ev_by_clique = {}
-        for j, v in enumerate(ev_vars):
-            ev_by_clique.setdefault(self.var_clique[v], []).append((j, v))
-        for c in self.cliques:
-            t, ls = self.pot[c]
-            b = E.contract(t, ls, ones, [R], ls + [R], combine="mul")
-            for j, v in ev_by_clique.get(c, []):
-                ind = E.indicator(codes[j], self.card[v], n_rows, err=err)
-                E.contract(b, ls + [R], ind, [v, R], ls + [R], combine="mul", out=b)
-            beliefs[c] = (b, ls)
-        seps = {}
-        for p, c in reversed(self.order):  # collect
-            tc, lc = beliefs[c]
-            tp, lp = beliefs[p]
-            sep = [v for v in lc if v in p]
-            sigma = E.contract(tc, lc + [R], None, None, sep + [R], reduce=red, combine="copy")
-            E.contract(tp, lp + [R], sigma, sep + [R], lp + [R], combine="mul", out=tp)
-            seps[(p, c)] = (sigma, sep)
-        for p, c in self.order:  # distribute
-            tc, lc = beliefs[c]
-            tp, lp = beliefs[p]
-            mu, sep = seps[(p, c)]
-            sigma = E.contract(tp, lp + [R], None, None, sep + [R], reduce=red, combine="copy")
-            ratio = E.contract(sigma, sep + [R], mu, sep + [R], sep + [R], combine="div")
-            E.contract(tc, lc + [R], ratio, sep + [R], lc + [R], combine="mul", out=tc)
-            seps[(p, c)] = (sigma, sep)
-        return BatchedCalibration(self, beliefs, seps, n_rows)
+        sch = self.schedule(n_rows, ev_vars, operation, marginals)
+        cal = sch.run(codes)
+        if err is not None:
+            err.copy_(sch.err)
+        return cal
 
     def encode(self, df):
         import pandas as pd
@@ -134,14 +197,12 @@ class BatchedJunctionTree:
         return codes, ev_vars
 
     def calibrate_frame(self, df, operation="marginalize"):
-        import torch
-
-        from .batch import upload_codes
+        from .batch import download, upload_codes
 
         codes, ev_vars = self.encode(df)
         d = upload_codes(codes)
-        err = torch.zeros(1, dtype=torch.int32, device=d.device)
-        cal = self.calibrate_codes(d, ev_vars, len(df), operation=operation, err=err)
-        if int(err.item()) != 0:
+        sch = self.schedule(len(df), ev_vars, operation)
+        cal = sch.run(d)
+        if int(download(sch.err)[0]) != 0:
             raise IndexError("evidence state code out of range")
         return cal

@@ -161,3 +161,106 @@ def test_rows_plan_matches_numpy(gpu):
         np.testing.assert_allclose(marg_h[cq0:, r], j.sum(0) / z, rtol=1e-12)
         assert int(mp_h[r]) == int(np.argmax(j))
     N.check(L.pgm_rows_plan_destroy(h))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_contract_row_mode_shapes(gpu, seed):
+    """Shapes that take the row-mode kernel (innermost output dim >= 64), with and without
+    reductions, transposed operands, broadcast operands and split reductions."""
+    E = _e()
+    rng = np.random.default_rng(1000 + seed)
+    labels = list("abcdef")
+    card = {l: int(rng.integers(2, 6)) for l in labels}
+    card["r"] = int(rng.choice([64, 100, 257, 1000]))  # row-like axis
+    la = list(rng.choice(labels, size=int(rng.integers(1, 4)), replace=False)) + ["r"]
+    lb = list(rng.choice(labels, size=int(rng.integers(0, 3)), replace=False))
+    if seed % 2:
+        lb = lb + ["r"]
+    rng.shuffle(la)
+    a = rng.random([card[l] for l in la])
+    b = rng.random([card[l] for l in lb]) if lb else np.array(rng.random())
+    union = list(dict.fromkeys(la + lb))
+    keep = [l for l in union if l != "r" and rng.random() < 0.5] + ["r"]
+    A, B = E.to_device(a), E.to_device(b)
+    idx = {l: i for i, l in enumerate(union)}
+    ref = np.einsum(a, [idx[l] for l in la], b, [idx[l] for l in lb], [idx[l] for l in keep])
+    got = E.to_host(E.contract(A, la, B, lb, keep, reduce="sum", combine="mul"))
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
+    full = np.einsum(a, [idx[l] for l in la], b, [idx[l] for l in lb], list(range(len(union))))
+    red = tuple(i for i, l in enumerate(union) if l not in keep)
+    refm = np.max(full, axis=red) if red else full
+    refm = np.transpose(refm, [[l for l in union if l in keep].index(l) for l in keep])
+    np.testing.assert_array_equal(E.to_host(E.contract(A, la, B, lb, keep, reduce="max", combine="mul")), refm)
+    # elementwise divide with a broadcast operand over the row axis
+    keep2 = union
+    D = E.contract(A, la, B, lb, keep2, combine="div")
+    with np.errstate(divide="ignore", invalid="ignore"):
+        refd = np.einsum(a, [idx[l] for l in la], list(range(len(union)))) if False else None
+    bb = np.broadcast_to(np.einsum(b, [idx[l] for l in lb], sorted(idx[l] for l in lb)).reshape(
+        [card[l] if l in lb else 1 for l in union]), [card[l] for l in union]) if lb else b
+    aa = np.broadcast_to(np.einsum(a, [idx[l] for l in la], sorted(idx[l] for l in la)).reshape(
+        [card[l] if l in la else 1 for l in union]), [card[l] for l in union])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = aa / bb
+    q[np.isnan(q)] = 0
+    np.testing.assert_allclose(E.to_host(D), q, rtol=1e-15)
+
+
+def test_contract_row_mode_split_reduction(gpu):
+    """Few outputs along a 512-wide row axis, long reduction: row mode + split-K + finalize."""
+    E = _e()
+    rng = np.random.default_rng(7)
+    a = rng.random((4000, 512))
+    b = rng.random((4000,))
+    A, B = E.to_device(a), E.to_device(b)
+    got = E.to_host(E.contract(A, ["k", "r"], B, ["k"], ["r"], reduce="sum", combine="mul"))
+    np.testing.assert_allclose(got, b @ a, rtol=1e-12)
+
+
+def test_product_n_and_graph_replay(gpu):
+    """pgm_product_n (up to 8 broadcast operands, row and flat mode) and HIP-graph replay."""
+    import torch
+
+    from pgmpy_amd.program import Program
+
+    E = _e()
+    rng = np.random.default_rng(3)
+    for rows in (1, 300):
+        a = rng.random((3, 4, rows))
+        b = rng.random((4, rows))
+        c = rng.random((3,))
+        d = rng.random((5, 3, rows))
+        ops = [(E.to_device(a), ["x", "y", "r"]), (E.to_device(b), ["y", "r"]), (E.to_device(c), ["x"]),
+               (E.to_device(d), ["z", "x", "r"])]
+        got = E.to_host(E.product_n(ops, ["z", "x", "y", "r"]))
+        ref = np.einsum("xyr,yr,x,zxr->zxyr", a, b, c, d)
+        np.testing.assert_allclose(got, ref, rtol=1e-15)
+    # ratio pair: C = X * (N / D) with 0/0 -> 0 (x/0 -> inf)
+    X = rng.random((3, 50))
+    Nn = rng.random((3, 50))
+    Dd = rng.random((3, 50))
+    Nn[0, :5] = 0.0
+    Dd[0, :5] = 0.0
+    Dd[1, :3] = 0.0
+    from pgmpy_amd import _native as NN
+
+    got = E.to_host(E.product_n([(E.to_device(X), ["a", "r"]), (E.to_device(Nn), ["a", "r"]),
+                                 (E.to_device(Dd), ["a", "r"])], ["a", "r"],
+                                kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN]))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = Nn / Dd
+    r[np.isnan(r)] = 0
+    np.testing.assert_array_equal(got, X * r)
+    # a captured program: out = (A*B) summed over y, replayed after A changes in place
+    A = E.to_device(rng.random((6, 500)))
+    B = E.to_device(rng.random((6,)))
+    prog = Program()
+    out = prog.contract(A, ["y", "r"], B, ["y"], ["r"], reduce="sum", combine="mul")
+    prog.capture()
+    prog.run()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(E.to_host(out), E.to_host(B) @ E.to_host(A), rtol=1e-12)
+    A.mul_(2.0)
+    prog.run()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(E.to_host(out), E.to_host(B) @ E.to_host(A), rtol=1e-12)
