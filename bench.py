@@ -14,7 +14,7 @@ marginals to HBM.
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, rows sharded: weak scaling)
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
-(k_rows; achieved = algorithmic bytes per launch / HIP-event launch time) and a
+(k_rows_affine for the C3 template; achieved = algorithmic bytes per launch / HIP-event launch time) and a
 CPU baseline (the numpy oracle's per-row predict_probability, single core,
 bounded sample) timed on this host.
 Other workloads for DESIGN.md numbers: --workload c2 (single munin query,
@@ -196,6 +196,8 @@ def bench_c3(args, dist, rank, world):
     for _ in range(args.warmup):
         plan.run(d_codes, rows, 0, rows, out, err=err)
     barrier(dist)
+    # HIP events on the launch stream bracketing the timed region: average launch duration
+    # (includes the ~1 us gap between back-to-back launches that rocprofv3's kernel time omits)
     timer = HipTimer()
     timer.start()
     t_start = time.perf_counter()
@@ -212,7 +214,8 @@ def bench_c3(args, dist, rank, world):
     kern_ms = kern_ms_total / args.steps
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_rows = load_traffic("k_rows")
+    kname = plan.kernel_name()
+    traffic, traffic_rows = load_traffic(kname)
     if traffic is not None and traffic_rows:
         traffic = traffic * rows / traffic_rows
     result = {
@@ -245,7 +248,7 @@ def bench_c3(args, dist, rank, world):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "k_rows",
+            "kernel": kname,
             "kernel_ms": kern_ms,
             "algorithmic_bytes_per_row": bpr,
             "bytes_per_launch": bpr * rows,

@@ -208,7 +208,9 @@ enum pgm_rows_mode {
   PGM_ROWS_JOINT = 2,     /* normalized joint over the query dims (query joint=True); n_comp == 1 only */
   PGM_ROWS_MAP = 4,       /* first-index argmax of the joint (map_query / predict)  */
   PGM_ROWS_MAPGAP = 8,    /* also (best - second best) / best of the joint, for tie screening */
-  PGM_ROWS_VALUES_GLOBAL = 16 /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
+  PGM_ROWS_VALUES_GLOBAL = 16, /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
+  PGM_ROWS_ONE_GROUP = 32,     /* tuning: one 64-row group per workgroup (no staging amortisation) */
+  PGM_ROWS_GENERIC = 64        /* tuning: table-driven kernel even for all-affine plans (testing)  */
 };
 
 typedef struct {

@@ -653,263 +653,500 @@ __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, ui
 }
 
 // ----------------------------------------------------------------------------- fused row plan
-// Table-driven: for every component c and every entry e of its (query x hidden) index space the
-// host precomputes the offset of each of the component's factors (tab[c.off_base + e*nf + j]), the
-// marginal row each query dim accumulates into (tab[c.marg_base + qi*nq + i]) and the entry's
-// contribution to the flat MAP index (tab[c.map_base + qi]).  The entry loop is wave-uniform, so
-// every table read is a scalar load; per lane there are only the evidence bases of the factors,
-// the running product and the marginal accumulators.
+// One workgroup owns 64 evidence rows (one per lane) for RG consecutive row groups; its waves split
+// the plan's independent components (wave w takes components w, w+W, ...), so every descriptor
+// read, loop bound and branch is wave-uniform (scalar) and a row's work is spread over W
+// wavefronts.  A wave loads only its components' evidence codes (all in flight at once) and
+// stages only their CPT values into LDS.  Components meet once per row group through LDS: masses
+// (impossible evidence makes every marginal NaN), MAP index digits and MAP gaps.
+//
+// Descriptors live in device memory as packed structs (one s_load_dwordx16 per component, one
+// s_load_dwordx4 per evidence term).  Table-driven components: for every entry e of a component's
+// (query x hidden) index space the host precomputes each factor's offset (tab[off_base + e*nf + j]),
+// the marginal rows each query dim accumulates into (tab[marg_base + qi*nq + i]) and the entry's MAP
+// index digit (tab[map_base + qi]).  Affine components (one query dim, no hidden dim) need no
+// table: factor j sits at base_j + s * fstride[j] for query state s.
+struct RowsComp {
+  int32_t nf, nt, P, H;
+  int32_t simple, mstride, q_lo, q_hi;
+  int32_t off_base, marg_base, map_base, ev_lo;  // ev_lo: first evidence term (n_ev when none)
+  int32_t val_lo, val_hi, marg0, nq;              // marg0: marginal row of the (affine) query dim
+  int32_t fbase[PGM_ROWS_MAX_FAC];
+  int32_t fstride[PGM_ROWS_MAX_FAC];
+  // affine fast kernel: evidence terms folded into per-slot strides (term j adds code_j * aS[j][k]
+  // to factor slot k), padded to 8 terms (stride 0, card 256, a real column)
+  int32_t a_S[8][4];
+  int32_t a_col[8], a_card[8];
+};
+struct RowsTerm {
+  int32_t col, stride, card, slot;  // evidence column, stride in its factor, cardinality, factor slot
+};
 struct RowsK {
-  int32_t n_fac, n_ev, n_values, n_marg;
-  int32_t n_joint, n_comp, n_tab, _pad;
-  int32_t comp_fb[PGM_ROWS_MAX_COMP], comp_nf[PGM_ROWS_MAX_COMP], comp_nq[PGM_ROWS_MAX_COMP];
-  uint32_t comp_P[PGM_ROWS_MAX_COMP], comp_H[PGM_ROWS_MAX_COMP];
-  int32_t comp_off_base[PGM_ROWS_MAX_COMP], comp_marg_base[PGM_ROWS_MAX_COMP], comp_map_base[PGM_ROWS_MAX_COMP];
-  int32_t comp_q_lo[PGM_ROWS_MAX_COMP], comp_q_hi[PGM_ROWS_MAX_COMP];  // query dims of c: q_dims[lo, hi)
+  int32_t n_values, n_marg, n_joint, n_comp;  // n_values includes the trailing 1.0 (index one_idx)
+  int32_t n_waves, terms_off, tab_off, one_idx;  // offsets (in int32) into the descriptor buffer
   int32_t q_marg_off[PGM_ROWS_MAX_LOOP], q_card[PGM_ROWS_MAX_LOOP];
-  // affine components (one query dim, no hidden dim): factor j of component c sits at
-  // cb[j] + s * comp_fstride[c][j] for query state s; the MAP index moves by comp_mstride[c]
-  int32_t comp_simple[PGM_ROWS_MAX_COMP], comp_mstride[PGM_ROWS_MAX_COMP];
-  int32_t comp_fstride[PGM_ROWS_MAX_COMP][PGM_ROWS_MAX_FAC];
-  int32_t fac_base[PGM_ROWS_MAX_FAC];
-  int32_t fac_ev_begin[PGM_ROWS_MAX_FAC], fac_ev_end[PGM_ROWS_MAX_FAC];
-  int32_t ev_col[PGM_ROWS_MAX_EV], ev_stride[PGM_ROWS_MAX_EV], ev_card[PGM_ROWS_MAX_EV];
 };
 
 struct RowsHandle {
   RowsK k;
-  int max_nf, max_f;
+  int max_nf, max_nt;
+  bool any_table, all_affine;
   double *d_values;
-  int32_t *d_tab;
+  int32_t *d_desc;
 };
 
-template <bool VL, bool AL, int MAXF, int MAXFC>
-__global__ __launch_bounds__(256) void k_rows(const RowsK p, const double *__restrict__ gvals,
-                                              const int32_t *__restrict__ tab, const uint8_t *__restrict__ codes,
-                                              int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode,
-                                              double *__restrict__ marg, double *__restrict__ joint, int64_t ld_out,
-                                              int32_t *__restrict__ map, double *__restrict__ gap,
-                                              int32_t *__restrict__ err) {
+template <bool VL, bool AL, int MAXFC, int MAXT>
+__global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows(
+    const RowsK p, const double *__restrict__ gvals, const int32_t *__restrict__ desc,
+    const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode, int32_t RG,
+    double *__restrict__ marg, double *__restrict__ joint, int64_t ld_out, int32_t *__restrict__ map,
+    double *__restrict__ gap, int32_t *__restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = r < n_rows;
-  const int nb = blockDim.x;
-  const int lane = threadIdx.x;
-
-  // evidence part of every factor's offset (issued before the LDS staging barrier)
-  int32_t base[MAXF];
-  bool bad = false;
-#pragma unroll
-  for (int f = 0; f < MAXF; ++f) {
-    int32_t b = 0;
-    if (f < p.n_fac) {
-      b = p.fac_base[f];
-      if (live) {
-        for (int j = p.fac_ev_begin[f]; j < p.fac_ev_end[f]; ++j) {
-          uint32_t c = codes[(int64_t)p.ev_col[j] * ld_codes + row0 + r];
-          if (c >= (uint32_t)p.ev_card[j]) {
-            bad = true;
-            c = 0;
-          }
-          b += (int32_t)c * p.ev_stride[j];
-        }
-      }
-    }
-    base[f] = b;
-  }
+  const int lane = threadIdx.x & 63;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // this wave's component
+  const int NC = p.n_comp;
+  const RowsComp &cd = ((const RowsComp *)desc)[c];
+  const RowsTerm *__restrict__ tt = (const RowsTerm *)(desc + p.terms_off) + cd.ev_lo;
+  const int32_t *__restrict__ tab = desc + p.tab_off;
   double *svals = lds;
-  double *sacc = lds + (VL ? ((p.n_values + 1) & ~1) : 0);
-  if constexpr (VL) {
-    for (int i = threadIdx.x; i < p.n_values; i += blockDim.x) svals[i] = gvals[i];
-    __syncthreads();
-  }
-  if (!live) return;
-  if (bad && err) atomicOr(err, 1);
+  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0);  // [NC][64]
+  double *xgap = xmass + NC * 64;                              // [NC][64]
+  int32_t *xmap = (int32_t *)(xgap + NC * 64);                 // [NC][64]
+  double *sacc = (double *)(xmap + NC * 64);                   // [n_marg][64]
+  const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
+  const bool do_joint = (mode & PGM_ROWS_JOINT) != 0;
+  const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
+  const int nf = cd.nf, nq = cd.nq, nt = cd.nt;
+  const uint32_t P = cd.P, H = cd.H;
   auto val = [&](int32_t i) -> double {
     if constexpr (VL) return svals[i];
     else return gvals[i];
   };
-  auto acc = [&](int32_t t) -> double & {
-    if constexpr (AL) return sacc[t * nb + lane];
-    else return marg[(int64_t)t * ld_out + r];
+  // stage this component's CPT values once per workgroup (no other wave reads them: no barrier)
+  if constexpr (VL) {
+    if (lane == 0) svals[p.one_idx] = 1.0;
+    for (int i = cd.val_lo + lane; i < cd.val_hi; i += 64) svals[i] = gvals[i];
+  }
+  // evidence codes of row group g (MAXT <= 8: padded terms, static descriptor offsets)
+  constexpr int NT = MAXT <= 8 ? MAXT : 1;
+  auto load_codes = [&](int g, uint32_t (&code)[NT]) {
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const uint8_t *crow = codes + row0 + (r < n_rows ? r : 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) code[j] = crow[(int64_t)tt[j].col * ld_codes];
   };
-  const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
-  const bool do_joint = (mode & PGM_ROWS_JOINT) != 0;
-  const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
-
-  double zprod = 1.0, min_gap = 1.0;
-  int32_t map_idx = 0;
-  for (int c = 0; c < p.n_comp; ++c) {
-    const int fb = p.comp_fb[c], nf = p.comp_nf[c], nq = p.comp_nq[c];
-    const uint32_t P = p.comp_P[c], H = p.comp_H[c];
-    const int32_t *toff = tab + p.comp_off_base[c];
-    const int32_t *tmarg = tab + p.comp_marg_base[c];
-    const int32_t *tmap = tab + p.comp_map_base[c];
-    // this component's factor bases, compacted to static slots
-    int32_t cb[MAXFC];
+  uint32_t nxt[NT];
+  if (MAXT <= 8 && nt > 0) load_codes(0, nxt);
+  for (int g = 0; g < RG; ++g) {
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const bool live = r < n_rows;
+    auto acc = [&](int32_t t) -> double & {
+      if constexpr (AL) return sacc[t * 64 + lane];
+      else return marg[(int64_t)t * ld_out + r];
+    };
+    int32_t cb[MAXFC];  // slots >= nf point at the constant 1.0 (fbase = one_idx, fstride = 0)
 #pragma unroll
-    for (int j = 0; j < MAXFC; ++j) {
-      int32_t b = 0;
+    for (int j = 0; j < MAXFC; ++j) cb[j] = cd.fbase[j];
+    bool bad = false;
+    if (nt == 0) {
+      // no evidence in this component: nothing to load (codes may have no columns at all)
+    } else if constexpr (MAXT <= 8) {
+      uint32_t code[NT];
 #pragma unroll
-      for (int f = 0; f < MAXF; ++f) b = (f == fb + j) ? base[f] : b;
-      cb[j] = b;
+      for (int j = 0; j < NT; ++j) code[j] = nxt[j];
+      if (g + 1 < RG) load_codes(g + 1, nxt);  // next row group's codes in flight during this one
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const RowsTerm &t = tt[j];
+        const bool oob = code[j] >= (uint32_t)t.card;
+        bad |= oob;
+        const int32_t w = oob ? 0 : (int32_t)code[j] * t.stride;
+#pragma unroll
+        for (int k = 0; k < MAXFC; ++k) cb[k] += (k == t.slot) ? w : 0;
+      }
+    } else {
+      const uint8_t *crow = codes + row0 + (live ? r : 0);
+      for (int j = 0; j < nt; ++j) {
+        const RowsTerm &t = tt[j];
+        uint32_t cv = crow[(int64_t)t.col * ld_codes];
+        if (cv >= (uint32_t)t.card) {
+          bad = true;
+          cv = 0;
+        }
+        const int32_t w = (int32_t)cv * t.stride;
+#pragma unroll
+        for (int k = 0; k < MAXFC; ++k) cb[k] += (k == t.slot) ? w : 0;
+      }
     }
-    if (p.comp_simple[c]) {
-      // affine fast path: entries are the states of the component's single query variable.
-      // pass 1: component mass (+ MAP, joint); pass 2: recompute and stream the normalised
-      // marginal straight to HBM (no accumulator state, so LDS holds only the CPT values)
-      int32_t st[MAXFC];
+    if (bad && live && err) atomicOr(err, 1);
+    double mass = 0.0, best = -1.0, second = -1.0;
+    int32_t best_map = 0;
+    if (cd.simple) {
+      // affine: states [0, RC) stay in registers (branch-free clamped loads, all LDS reads of
+      // the pass in flight at once); states >= RC are recomputed in the write pass
+      const int32_t ms = cd.mstride;
+      constexpr int RC = 8;
+      double pc[RC];
+      const int32_t plast = (int32_t)P - 1;
 #pragma unroll
-      for (int j = 0; j < MAXFC; ++j) st[j] = p.comp_fstride[c][j];
-      const int32_t ms = p.comp_mstride[c];
-      double mass = 0.0, best = -1.0, second = -1.0;
-      int32_t best_s = 0;
-      for (uint32_t qs = 0; qs < P; ++qs) {
-        double prod = 1.0;
+      for (int qs = 0; qs < RC; ++qs) {
+        const int32_t q = qs < plast ? qs : plast;
+        double prod = val(cb[0] + q * cd.fstride[0]);
 #pragma unroll
-        for (int j = 0; j < MAXFC; ++j)
-          if (j < nf) prod *= val(cb[j] + (int32_t)qs * st[j]);
+        for (int j = 1; j < MAXFC; ++j) prod *= val(cb[j] + q * cd.fstride[j]);
+        pc[qs] = prod;
+      }
+      auto visit = [&](uint32_t qs, double prod) {
         mass += prod;
-        if (do_joint) joint[(int64_t)qs * ms * ld_out + r] = prod;
+        if (do_joint && live) joint[(int64_t)qs * ms * ld_out + r] = prod;
         if (do_map) {
           if (prod > best) {
             second = best;
             best = prod;
-            best_s = (int32_t)qs;
+            best_map = (int32_t)qs * ms;
           } else if (prod > second) {
             second = prod;
           }
         }
-      }
-      zprod *= mass;
-      if (do_marg && nq) {
-        const double inv = 1.0 / mass;
-        double *out = marg + (int64_t)p.q_marg_off[p.comp_q_lo[c]] * ld_out + r;
-        for (uint32_t qs = 0; qs < P; ++qs) {
-          double prod = 1.0;
+      };
 #pragma unroll
-          for (int j = 0; j < MAXFC; ++j)
-            if (j < nf) prod *= val(cb[j] + (int32_t)qs * st[j]);
+      for (int qs = 0; qs < RC; ++qs)
+        if ((uint32_t)qs < P) visit(qs, pc[qs]);
+      for (uint32_t qs = RC; qs < P; ++qs) {
+        double prod = val(cb[0] + (int32_t)qs * cd.fstride[0]);
+#pragma unroll
+        for (int j = 1; j < MAXFC; ++j) prod *= val(cb[j] + (int32_t)qs * cd.fstride[j]);
+        visit(qs, prod);
+      }
+      if (do_marg && nq && live) {  // normalised marginal streamed straight to HBM
+        const double inv = 1.0 / mass;
+        double *out = marg + (int64_t)cd.marg0 * ld_out + r;
+#pragma unroll
+        for (int qs = 0; qs < RC; ++qs)
+          if ((uint32_t)qs < P) __builtin_nontemporal_store(pc[qs] * inv, out + (int64_t)qs * ld_out);
+        for (uint32_t qs = RC; qs < P; ++qs) {
+          double prod = val(cb[0] + (int32_t)qs * cd.fstride[0]);
+#pragma unroll
+          for (int j = 1; j < MAXFC; ++j) prod *= val(cb[j] + (int32_t)qs * cd.fstride[j]);
           __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
         }
       }
-      if (do_map) {
-        map_idx += best_s * ms;
-        if (P > 1) min_gap = fmin(min_gap, best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0);
+    } else if (live) {
+      const int32_t *toff = tab + cd.off_base;
+      const int32_t *tmarg = tab + cd.marg_base;
+      const int32_t *tmap = tab + cd.map_base;
+      if (do_marg && nq > 1) {
+        for (int q = cd.q_lo; q < cd.q_hi; ++q)
+          for (int s = 0; s < p.q_card[q]; ++s) acc(p.q_marg_off[q] + s) = 0.0;
       }
-      continue;
-    }
-    if (do_marg && nq > 1) {
-      for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
-        for (int s = 0; s < p.q_card[q]; ++s) acc(p.q_marg_off[q] + s) = 0.0;
-    }
-    double mass = 0.0, best = -1.0, second = -1.0;
-    int32_t best_map = 0;
-    uint32_t e = 0;
+      uint32_t e = 0;
 #pragma unroll 2
-    for (uint32_t qi = 0; qi < P; ++qi) {
-      double v = 0.0;
-      if (H == 1) {  // no hidden dims: one product per query entry
-        const int32_t *o = toff + qi * nf;
-        double prod = 1.0;
-#pragma unroll
-        for (int j = 0; j < MAXFC; ++j)
-          if (j < nf) prod *= val(cb[j] + o[j]);
-        v = prod;
-      } else {
-        for (uint32_t hi = 0; hi < H; ++hi, ++e) {
-          const int32_t *o = toff + e * nf;
+      for (uint32_t qi = 0; qi < P; ++qi) {
+        double v = 0.0;
+        if (H == 1) {  // no hidden dims: one product per query entry
+          const int32_t *o = toff + qi * nf;
           double prod = 1.0;
 #pragma unroll
           for (int j = 0; j < MAXFC; ++j)
             if (j < nf) prod *= val(cb[j] + o[j]);
-          v += prod;
-        }
-      }
-      mass += v;
-      if (do_marg) {
-        if (nq == 1) {
-          acc(tmarg[qi]) = v;  // each marginal row is hit exactly once
+          v = prod;
         } else {
-          for (int i = 0; i < nq; ++i) acc(tmarg[qi * nq + i]) += v;
+          for (uint32_t hi = 0; hi < H; ++hi, ++e) {
+            const int32_t *o = toff + e * nf;
+            double prod = 1.0;
+#pragma unroll
+            for (int j = 0; j < MAXFC; ++j)
+              if (j < nf) prod *= val(cb[j] + o[j]);
+            v += prod;
+          }
+        }
+        mass += v;
+        if (do_marg) {
+          if (nq == 1) {
+            acc(tmarg[qi]) = v;  // each marginal row is hit exactly once
+          } else {
+            for (int i = 0; i < nq; ++i) acc(tmarg[qi * nq + i]) += v;
+          }
+        }
+        if (do_joint) joint[(int64_t)tmap[qi] * ld_out + r] = v;
+        if (do_map) {
+          if (v > best) {
+            second = best;
+            best = v;
+            best_map = tmap[qi];
+          } else if (v > second) {
+            second = v;
+          }
         }
       }
-      if (do_joint) joint[(int64_t)tmap[qi] * ld_out + r] = v;
-      if (do_map) {
-        if (v > best) {
-          second = best;
-          best = v;
-          best_map = tmap[qi];
-        } else if (v > second) {
-          second = v;
-        }
-      }
-    }
-    zprod *= mass;
-    if (do_marg && nq > 0) {  // component marginals normalised by the component mass
-      const double inv = 1.0 / mass;
-      for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
-        for (int s = 0; s < p.q_card[q]; ++s) acc(p.q_marg_off[q] + s) *= inv;
-    }
-    if (do_map) {
-      map_idx += best_map;
-      if (P > 1) {
-        const double g = best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0;
-        min_gap = fmin(min_gap, g);
-      }
-    }
-  }
-  // impossible evidence (zero total mass): every marginal is 0/0 = NaN and np.argmax gives 0
-  const bool dead = !(zprod > 0.0);
-  if (do_marg) {
-    const double nan = __builtin_nan("");
-    if (dead) {
-      for (int a = 0; a < p.n_marg; ++a) marg[(int64_t)a * ld_out + r] = nan;
-    } else if constexpr (AL) {
-      for (int c = 0; c < p.n_comp; ++c) {
-        if (p.comp_simple[c]) continue;
-        for (int q = p.comp_q_lo[c]; q < p.comp_q_hi[c]; ++q)
-          for (int s2 = 0; s2 < p.q_card[q]; ++s2) {
-            const int a = p.q_marg_off[q] + s2;
-            marg[(int64_t)a * ld_out + r] = acc(a);
+      if (do_marg && nq > 0) {  // component marginals normalised by the component mass
+        const double inv = 1.0 / mass;
+        for (int q = cd.q_lo; q < cd.q_hi; ++q)
+          for (int s = 0; s < p.q_card[q]; ++s) {
+            const int a = p.q_marg_off[q] + s;
+            if constexpr (AL) marg[(int64_t)a * ld_out + r] = acc(a) * inv;
+            else acc(a) *= inv;
           }
       }
     }
-  }
-  if (do_joint) {
-    const double inv = 1.0 / zprod;
-    for (int q = 0; q < p.n_joint; ++q) {
-      double *j = joint + (int64_t)q * ld_out + r;
-      *j = dead ? __builtin_nan("") : *j * inv;
+    if (NC > 1 || do_map) {
+      xmass[c * 64 + lane] = mass;
+      if (do_map) {
+        xmap[c * 64 + lane] = best_map;
+        xgap[c * 64 + lane] = (P > 1) ? (best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0) : 1.0;
+      }
     }
-  }
-  if (do_map) {
-    if (map) map[r] = dead ? 0 : map_idx;
-    if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : min_gap;
+    if (NC > 1) __syncthreads();
+    if (live) {
+      double z = mass;
+      if (NC > 1) {
+        z = 1.0;
+        for (int c2 = 0; c2 < NC; ++c2) z *= xmass[c2 * 64 + lane];
+      }
+      // impossible evidence (zero total mass): every marginal is 0/0 = NaN and np.argmax gives 0
+      const bool dead = !(z > 0.0);
+      if (do_marg && dead) {
+        const double nan = __builtin_nan("");
+        for (int q = cd.q_lo; q < cd.q_hi; ++q)
+          for (int s = 0; s < p.q_card[q]; ++s) marg[(int64_t)(p.q_marg_off[q] + s) * ld_out + r] = nan;
+      }
+      if (do_joint && c == 0) {  // single-component plans only
+        const double inv = 1.0 / z;
+        for (int q = 0; q < p.n_joint; ++q) {
+          double *j = joint + (int64_t)q * ld_out + r;
+          *j = dead ? __builtin_nan("") : *j * inv;
+        }
+      }
+      if (do_map && c == 0) {
+        int32_t m = 0;
+        double mg = 1.0;
+        for (int c2 = 0; c2 < NC; ++c2) {
+          m += xmap[c2 * 64 + lane];
+          mg = fmin(mg, xgap[c2 * 64 + lane]);
+        }
+        if (map) map[r] = dead ? 0 : m;
+        if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : mg;
+      }
+    }
+    if (NC > 1 && g + 1 < RG) __syncthreads();  // the exchange slots are reused by the next row group
   }
 }
 
-template <bool VL, bool AL, int MAXF>
-static void launch_rows_ff(int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k, const double *v,
-                           const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n, int32_t mode,
-                           double *marg, double *joint, int64_t ldo, int32_t *map, double *gap, int32_t *err) {
-  if (max_nf <= 2)
-    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, 2>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
-  else if (max_nf <= 4)
-    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, 4>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+// All-affine plans (every component one query dim, no hidden dim, <= 4 factors, <= 8 evidence
+// terms: the common batched-predict shape, e.g. munin C3).  Same work split as k_rows, but each
+// wave loads its component's descriptor into registers once, folds evidence with multiply-adds
+// against host-precomputed per-slot strides, and carries the MAP bookkeeping only when asked.
+template <bool VL, int NF, int NT, bool MAP>
+__global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
+    const RowsK p, const double *__restrict__ gvals, const int32_t *__restrict__ desc,
+    const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode, int32_t RG,
+    double *__restrict__ marg, int64_t ld_out, int32_t *__restrict__ map, double *__restrict__ gap,
+    int32_t *__restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x & 63;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NC = p.n_comp;
+  const RowsComp &cd = ((const RowsComp *)desc)[c];
+  double *svals = lds;
+  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0);  // [NC][64]
+  double *xgap = xmass + NC * 64;                              // [NC][64]
+  int32_t *xmap = (int32_t *)(xgap + NC * 64);                 // [NC][64]
+  const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
+  // descriptor -> registers (wave-uniform)
+  int32_t fb[NF], fs[NF], S[NT][NF];
+  uint32_t card[NT];
+  int64_t cofs[NT];
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    fb[k] = cd.fbase[k];
+    fs[k] = cd.fstride[k];
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    card[j] = (uint32_t)cd.a_card[j];
+    cofs[j] = (int64_t)cd.a_col[j] * ld_codes + row0;
+#pragma unroll
+    for (int k = 0; k < NF; ++k) S[j][k] = cd.a_S[j][k];
+  }
+  const int nt = cd.nt;
+  const uint32_t P = (uint32_t)cd.P;
+  const int32_t ms = cd.mstride;
+  double *mrow = marg + (int64_t)cd.marg0 * ld_out;
+  auto val = [&](int32_t i) -> double {
+    if constexpr (VL) return svals[i];
+    else return gvals[i];
+  };
+  if constexpr (VL) {
+    if (lane == 0) svals[p.one_idx] = 1.0;
+    for (int i = cd.val_lo + lane; i < cd.val_hi; i += 64) svals[i] = gvals[i];
+  }
+  auto load_codes = [&](int g, uint32_t (&code)[NT]) {
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const uint8_t *crow = codes + (r < n_rows ? r : 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) code[j] = crow[cofs[j]];
+  };
+  uint32_t nx[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) nx[j] = 0;
+  if (nt > 0) load_codes(0, nx);
+  for (int g = 0; g < RG; ++g) {
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const bool live = r < n_rows;
+    uint32_t code[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) code[j] = nx[j];
+    if (nt > 0 && g + 1 < RG) load_codes(g + 1, nx);  // next group's codes in flight during this one
+    int32_t cb[NF];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) cb[k] = fb[k];
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bool oob = code[j] >= card[j];
+      bad |= oob;
+      const int32_t cj = oob ? 0 : (int32_t)code[j];
+#pragma unroll
+      for (int k = 0; k < NF; ++k) cb[k] += cj * S[j][k];
+    }
+    if (bad && live && err) atomicOr(err, 1);
+    constexpr int RC = 8;
+    double pc[RC];
+    const int32_t plast = (int32_t)P - 1;
+#pragma unroll
+    for (int qs = 0; qs < RC; ++qs) {
+      const int32_t q = qs < plast ? qs : plast;
+      double prod = val(cb[0] + q * fs[0]);
+#pragma unroll
+      for (int k = 1; k < NF; ++k) prod *= val(cb[k] + q * fs[k]);
+      pc[qs] = prod;
+    }
+    double mass = 0.0, best = -1.0, second = -1.0;
+    int32_t best_s = 0;
+    auto visit = [&](uint32_t qs, double prod) {
+      mass += prod;
+      if constexpr (MAP) {
+        if (prod > best) {
+          second = best;
+          best = prod;
+          best_s = (int32_t)qs;
+        } else if (prod > second) {
+          second = prod;
+        }
+      }
+    };
+#pragma unroll
+    for (int qs = 0; qs < RC; ++qs)
+      if ((uint32_t)qs < P) visit(qs, pc[qs]);
+    for (uint32_t qs = RC; qs < P; ++qs) {
+      double prod = val(cb[0] + (int32_t)qs * fs[0]);
+#pragma unroll
+      for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
+      visit(qs, prod);
+    }
+    if (do_marg && live) {  // normalised marginal streamed straight to HBM
+      const double inv = 1.0 / mass;
+      double *out = mrow + r;
+#pragma unroll
+      for (int qs = 0; qs < RC; ++qs)
+        if ((uint32_t)qs < P) __builtin_nontemporal_store(pc[qs] * inv, out + (int64_t)qs * ld_out);
+      for (uint32_t qs = RC; qs < P; ++qs) {
+        double prod = val(cb[0] + (int32_t)qs * fs[0]);
+#pragma unroll
+        for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
+        __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
+      }
+    }
+    double z = mass;
+    if (NC > 1) {
+      xmass[c * 64 + lane] = mass;
+      if constexpr (MAP) {
+        xmap[c * 64 + lane] = best_s * ms;
+        xgap[c * 64 + lane] = (P > 1) ? (best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0) : 1.0;
+      }
+      __syncthreads();
+      z = 1.0;
+      for (int c2 = 0; c2 < NC; ++c2) z *= xmass[c2 * 64 + lane];
+    }
+    // impossible evidence (zero total mass): every marginal is 0/0 = NaN and np.argmax gives 0
+    const bool dead = !(z > 0.0);
+    if (live && do_marg && dead) {
+      for (uint32_t qs = 0; qs < P; ++qs) mrow[(int64_t)qs * ld_out + r] = __builtin_nan("");
+    }
+    if constexpr (MAP) {
+      if (live && c == 0) {
+        int32_t m = best_s * ms;
+        double mg = (P > 1) ? (best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0) : 1.0;
+        if (NC > 1) {
+          m = 0;
+          mg = 1.0;
+          for (int c2 = 0; c2 < NC; ++c2) {
+            m += xmap[c2 * 64 + lane];
+            mg = fmin(mg, xgap[c2 * 64 + lane]);
+          }
+        }
+        if (map) map[r] = dead ? 0 : m;
+        if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : mg;
+      }
+    }
+    if (NC > 1 && g + 1 < RG) __syncthreads();  // the exchange slots are reused by the next row group
+  }
+}
+
+template <bool VL, int NF, int NT>
+static void launch_affine_m(bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
+                            const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0,
+                            int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo, int32_t *map, double *gap,
+                            int32_t *err) {
+  if (do_map)
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, true>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
   else
-    hipLaunchKernelGGL((k_rows<VL, AL, MAXF, (MAXF < 16 ? MAXF : 16)>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, false>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
+}
+
+template <bool VL>
+static void launch_affine(int max_nf, int max_nt, bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s,
+                          const RowsK &k, const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc,
+                          int64_t row0, int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo, int32_t *map,
+                          double *gap, int32_t *err) {
+#define PGM_AFF(NF, NT) launch_affine_m<VL, NF, NT>(do_map, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err)
+  if (max_nt <= 4) {
+    if (max_nf <= 1) PGM_AFF(1, 4);
+    else if (max_nf <= 2) PGM_AFF(2, 4);
+    else PGM_AFF(4, 4);
+  } else {
+    if (max_nf <= 1) PGM_AFF(1, 8);
+    else if (max_nf <= 2) PGM_AFF(2, 8);
+    else PGM_AFF(4, 8);
+  }
+#undef PGM_AFF
+}
+
+template <bool VL, bool AL, int MAXT>
+static void launch_rows_t(int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k, const double *v,
+                          const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n, int32_t mode,
+                          int32_t RG, double *marg, double *joint, int64_t ldo, int32_t *map, double *gap, int32_t *err) {
+  if (max_nf <= 2)
+    hipLaunchKernelGGL((k_rows<VL, AL, 2, MAXT>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
+  else if (max_nf <= 4)
+    hipLaunchKernelGGL((k_rows<VL, AL, 4, MAXT>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
+  else if (max_nf <= 8)
+    hipLaunchKernelGGL((k_rows<VL, AL, 8, MAXT>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
+  else
+    hipLaunchKernelGGL((k_rows<VL, AL, PGM_ROWS_MAX_FAC, MAXT>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
 }
 
 template <bool VL, bool AL>
-static void launch_rows_f(int max_f, int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
+static void launch_rows_f(int max_nt, int max_nf, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
                           const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0, int64_t n,
-                          int32_t mode, double *marg, double *joint, int64_t ldo, int32_t *map, double *gap,
+                          int32_t mode, int32_t RG, double *marg, double *joint, int64_t ldo, int32_t *map, double *gap,
                           int32_t *err) {
-  if (max_f <= 8)
-    launch_rows_ff<VL, AL, 8>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+  if (max_nt <= 4)
+    launch_rows_t<VL, AL, 4>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
+  else if (max_nt <= 8)
+    launch_rows_t<VL, AL, 8>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
   else
-    launch_rows_ff<VL, AL, 16>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, marg, joint, ldo, map, gap, err);
+    launch_rows_t<VL, AL, PGM_ROWS_MAX_EV>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
 }
 
 // ============================================================================= C-ABI
@@ -1213,20 +1450,39 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   *handle = nullptr;
   if (pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP || pl->n_query < 0 || pl->n_query > pl->n_loop ||
       pl->n_fac < 0 || pl->n_fac > PGM_ROWS_MAX_FAC || pl->n_ev < 0 || pl->n_ev > PGM_ROWS_MAX_EV ||
-      pl->n_values < 0 || pl->n_comp < 0 || pl->n_comp > PGM_ROWS_MAX_COMP || pl->n_marg < 0 ||
+      pl->n_values < 0 || pl->n_comp < 1 || pl->n_comp > PGM_ROWS_MAX_COMP || pl->n_marg < 0 ||
       pl->n_marg > PGM_ROWS_MAX_MARG)
     return fail(PGM_EINVAL, "rows_plan_create: plan out of range (loop %d query %d fac %d ev %d comp %d marg %d)",
                 pl->n_loop, pl->n_query, pl->n_fac, pl->n_ev, pl->n_comp, pl->n_marg);
   RowsK k;
   memset(&k, 0, sizeof k);
-  k.n_fac = pl->n_fac;
-  k.n_ev = pl->n_ev;
-  k.n_values = pl->n_values;
+  k.one_idx = pl->n_values;  // a trailing 1.0 multiplies into the products of unused factor slots
+  k.n_values = pl->n_values + 1;
   k.n_marg = pl->n_marg;
   k.n_joint = pl->n_joint;
   k.n_comp = pl->n_comp;
+  // factors: value ranges and evidence ownership
+  std::vector<int64_t> fac_hi(pl->n_fac);
+  for (int f = 0; f < pl->n_fac; ++f) {
+    if (pl->fac_ev_begin[f] < 0 || pl->fac_ev_end[f] > pl->n_ev || pl->fac_ev_begin[f] > pl->fac_ev_end[f])
+      return fail(PGM_EINVAL, "rows_plan_create: factor %d evidence range", f);
+    int64_t mx = pl->fac_base[f];
+    for (int kk = 0; kk < pl->n_loop; ++kk) mx += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
+    for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) mx += (int64_t)(pl->ev_card[j] - 1) * pl->ev_stride[j];
+    if (mx >= pl->n_values || pl->fac_base[f] < 0)
+      return fail(PGM_EINVAL, "rows_plan_create: factor %d reads past values", f);
+    fac_hi[f] = mx + 1;
+  }
+  std::vector<int> ev_owner(pl->n_ev, -1);
+  for (int f = 0; f < pl->n_fac; ++f)
+    for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) {
+      if (ev_owner[j] != -1) return fail(PGM_EINVAL, "rows_plan_create: evidence term %d feeds two factors", j);
+      ev_owner[j] = f;
+    }
+  std::vector<RowsComp> comps(pl->n_comp);
   std::vector<int32_t> tab;
-  int covered_loop = 0, covered_fac = 0, nq_total = 0, max_nf = 1;
+  int covered_loop = 0, covered_fac = 0, nq_total = 0, max_nf = 1, max_nt = 0;
+  bool any_table = false;
   for (int c = 0; c < pl->n_comp; ++c) {
     const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c], le = pl->comp_loop_end[c];
     const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
@@ -1251,25 +1507,62 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
         if ((kk < lb || kk >= le) && pl->fac_stride[f][kk] != 0)
           return fail(PGM_EINVAL, "rows_plan_create: factor %d strides a loop dim outside its component", f);
     max_nf = std::max(max_nf, nf);
-    k.comp_fb[c] = fb;
-    k.comp_nf[c] = nf;
-    k.comp_nq[c] = nq;
-    k.comp_P[c] = (uint32_t)P;
-    k.comp_H[c] = (uint32_t)H;
-    k.comp_q_lo[c] = nq_total;
+    RowsComp &cd = comps[c];
+    memset(&cd, 0, sizeof cd);
+    cd.nf = nf;
+    cd.nq = nq;
+    cd.P = (int32_t)P;
+    cd.H = (int32_t)H;
+    cd.q_lo = nq_total;
     for (int kk = lb; kk < lb + nq; ++kk) {
       k.q_marg_off[nq_total] = pl->loop_marg_off[kk];
       k.q_card[nq_total] = pl->loop_card[kk];
       ++nq_total;
     }
-    k.comp_q_hi[c] = nq_total;
-    k.comp_simple[c] = (nq <= 1 && H == 1) ? 1 : 0;
-    k.comp_mstride[c] = nq == 1 ? pl->loop_map_stride[lb] : 0;
-    for (int f = fb; f < fe; ++f) k.comp_fstride[c][f - fb] = nq == 1 ? pl->fac_stride[f][lb] : 0;
+    cd.q_hi = nq_total;
+    cd.marg0 = nq >= 1 ? pl->loop_marg_off[lb] : 0;
+    cd.simple = (nq <= 1 && H == 1) ? 1 : 0;
+    any_table |= !cd.simple;
+    cd.mstride = nq == 1 ? pl->loop_map_stride[lb] : 0;
+    int64_t vlo = pl->n_values, vhi = 0;
+    for (int j = 0; j < PGM_ROWS_MAX_FAC; ++j) cd.fbase[j] = k.one_idx;
+    for (int f = fb; f < fe; ++f) {
+      cd.fbase[f - fb] = pl->fac_base[f];
+      cd.fstride[f - fb] = nq == 1 ? pl->fac_stride[f][lb] : 0;
+      vlo = std::min<int64_t>(vlo, pl->fac_base[f]);
+      vhi = std::max<int64_t>(vhi, fac_hi[f]);
+    }
+    cd.val_lo = vlo < vhi ? (int32_t)vlo : 0;
+    cd.val_hi = vlo < vhi ? (int32_t)vhi : 0;
+    // evidence terms: one contiguous run per component
+    int lo = pl->n_ev, hi = 0;
+    for (int f = fb; f < fe; ++f)
+      if (pl->fac_ev_end[f] > pl->fac_ev_begin[f]) {
+        lo = std::min(lo, pl->fac_ev_begin[f]);
+        hi = std::max(hi, pl->fac_ev_end[f]);
+      }
+    if (lo >= hi) lo = hi = pl->n_ev;
+    for (int j = lo; j < hi; ++j)
+      if (ev_owner[j] < fb || ev_owner[j] >= fe)
+        return fail(PGM_EINVAL, "rows_plan_create: component %d evidence terms are not contiguous", c);
+    cd.ev_lo = lo;
+    cd.nt = hi - lo;
+    max_nt = std::max(max_nt, hi - lo);
+    for (int j = 0; j < 8; ++j) {
+      cd.a_col[j] = hi > lo ? pl->ev_col[lo] : 0;
+      cd.a_card[j] = 256;
+    }
+    if (hi - lo <= 8)
+      for (int j = lo; j < hi; ++j) {
+        cd.a_col[j - lo] = pl->ev_col[j];
+        cd.a_card[j - lo] = pl->ev_card[j];
+        if (ev_owner[j] - fb < 4) cd.a_S[j - lo][ev_owner[j] - fb] = pl->ev_stride[j];
+      }
+    if (cd.simple) continue;
     // per-entry tables, entries in C-order over [query dims..., hidden dims...] (last fastest)
     const int nl = le - lb;
     std::vector<int32_t> dig(nl, 0);
-    k.comp_off_base[c] = (int32_t)tab.size();
+    cd.off_base = (int32_t)tab.size();
     for (uint64_t e = 0; e < P * H; ++e) {
       uint64_t t = e;
       for (int d = nl - 1; d >= 0; --d) {
@@ -1282,7 +1575,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
         tab.push_back((int32_t)o);
       }
     }
-    k.comp_marg_base[c] = (int32_t)tab.size();
+    cd.marg_base = (int32_t)tab.size();
     for (uint64_t qi = 0; qi < P; ++qi) {
       uint64_t t = qi;
       for (int d = nq - 1; d >= 0; --d) {
@@ -1291,7 +1584,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
       }
       for (int d = 0; d < nq; ++d) tab.push_back(pl->loop_marg_off[lb + d] + dig[d]);
     }
-    k.comp_map_base[c] = (int32_t)tab.size();
+    cd.map_base = (int32_t)tab.size();
     for (uint64_t qi = 0; qi < P; ++qi) {
       uint64_t t = qi;
       int64_t m = 0;
@@ -1304,43 +1597,52 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   }
   if (covered_loop != pl->n_loop || covered_fac != pl->n_fac || nq_total != pl->n_query)
     return fail(PGM_EINVAL, "rows_plan_create: components do not cover the loop dims / factors");
-  for (int f = 0; f < pl->n_fac; ++f) {
-    k.fac_base[f] = pl->fac_base[f];
-    k.fac_ev_begin[f] = pl->fac_ev_begin[f];
-    k.fac_ev_end[f] = pl->fac_ev_end[f];
-    if (pl->fac_ev_begin[f] < 0 || pl->fac_ev_end[f] > pl->n_ev || pl->fac_ev_begin[f] > pl->fac_ev_end[f])
-      return fail(PGM_EINVAL, "rows_plan_create: factor %d evidence range", f);
-    int64_t mx = pl->fac_base[f];
-    for (int kk = 0; kk < pl->n_loop; ++kk) mx += (int64_t)(pl->loop_card[kk] - 1) * pl->fac_stride[f][kk];
-    for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) mx += (int64_t)(pl->ev_card[j] - 1) * pl->ev_stride[j];
-    if (mx >= pl->n_values || pl->fac_base[f] < 0)
-      return fail(PGM_EINVAL, "rows_plan_create: factor %d reads past values", f);
+  // descriptor buffer: [RowsComp x n_comp][RowsTerm blocks][tables].  Each component's terms are
+  // padded with no-op terms to the kernel's static term count (4 or 8) when they fit it.
+  const int padt = max_nt <= 4 ? 4 : max_nt <= 8 ? 8 : 0;
+  std::vector<RowsTerm> terms;
+  for (int c = 0; c < pl->n_comp; ++c) {
+    RowsComp &cd = comps[c];
+    const int lo = cd.ev_lo, nt = cd.nt, fb = pl->comp_fac_begin[c];
+    cd.ev_lo = (int32_t)terms.size();
+    for (int j = lo; j < lo + nt; ++j)
+      terms.push_back(RowsTerm{pl->ev_col[j], pl->ev_stride[j], pl->ev_card[j], ev_owner[j] - fb});
+    if (nt > 0)
+      for (int j = nt; j < padt; ++j) terms.push_back(RowsTerm{pl->ev_col[lo], 0, 256, -1});
   }
-  for (int j = 0; j < pl->n_ev; ++j) {
-    k.ev_col[j] = pl->ev_col[j];
-    k.ev_stride[j] = pl->ev_stride[j];
-    k.ev_card[j] = pl->ev_card[j];
-  }
-  if (tab.empty()) tab.push_back(0);
-  k.n_tab = (int32_t)tab.size();
+  terms.push_back(RowsTerm{0, 0, 256, -1});
+  static_assert(sizeof(RowsComp) % 16 == 0 && sizeof(RowsTerm) == 16, "descriptor packing");
+  std::vector<int32_t> buf(comps.size() * (sizeof(RowsComp) / 4));
+  if (!comps.empty()) memcpy(buf.data(), comps.data(), comps.size() * sizeof(RowsComp));
+  k.terms_off = (int32_t)buf.size();
+  buf.resize(buf.size() + terms.size() * 4);
+  memcpy(buf.data() + k.terms_off, terms.data(), terms.size() * sizeof(RowsTerm));
+  k.tab_off = (int32_t)buf.size();
+  buf.insert(buf.end(), tab.begin(), tab.end());
+  buf.push_back(0);
   RowsHandle *h = new (std::nothrow) RowsHandle;
   if (!h) return fail(PGM_ENOMEM, "rows_plan_create: host allocation");
   h->k = k;
   h->max_nf = max_nf;
-  h->max_f = pl->n_fac;
+  h->max_nt = max_nt;
+  h->any_table = any_table;
+  h->all_affine = !any_table && max_nf <= 4 && max_nt <= 8;
   h->d_values = nullptr;
-  h->d_tab = nullptr;
+  h->d_desc = nullptr;
   hipError_t e = hipSuccess;
-  if (pl->n_values > 0) {
-    e = hipMalloc((void **)&h->d_values, sizeof(double) * pl->n_values);
-    if (e == hipSuccess) e = hipMemcpy(h->d_values, host_values, sizeof(double) * pl->n_values, hipMemcpyHostToDevice);
+  e = hipMalloc((void **)&h->d_values, sizeof(double) * (pl->n_values + 1));
+  if (e == hipSuccess && pl->n_values > 0)
+    e = hipMemcpy(h->d_values, host_values, sizeof(double) * pl->n_values, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const double one = 1.0;
+    e = hipMemcpy(h->d_values + pl->n_values, &one, sizeof(double), hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) e = hipMalloc((void **)&h->d_tab, sizeof(int32_t) * tab.size());
-  if (e == hipSuccess) e = hipMemcpy(h->d_tab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc((void **)&h->d_desc, sizeof(int32_t) * buf.size());
+  if (e == hipSuccess) e = hipMemcpy(h->d_desc, buf.data(), sizeof(int32_t) * buf.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     if (h->d_values) (void)hipFree(h->d_values);
-    if (h->d_tab) (void)hipFree(h->d_tab);
+    if (h->d_desc) (void)hipFree(h->d_desc);
     delete h;
     return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_plan_create: %s", hipGetErrorString(e));
   }
@@ -1352,7 +1654,7 @@ int pgm_rows_plan_destroy(void *handle) {
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
   if (h->d_values) (void)hipFree(h->d_values);
-  if (h->d_tab) (void)hipFree(h->d_tab);
+  if (h->d_desc) (void)hipFree(h->d_desc);
   delete h;
   return PGM_OK;
 }
@@ -1363,7 +1665,7 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "rows_plan_run: null handle");
   if (n_rows <= 0) return PGM_OK;
-  if (h->k.n_ev > 0 && !codes) return fail(PGM_EINVAL, "rows_plan_run: null codes");
+  if (h->max_nt > 0 && !codes) return fail(PGM_EINVAL, "rows_plan_run: null codes");
   if ((mode & PGM_ROWS_MARGINALS) && !marg) return fail(PGM_EINVAL, "rows_plan_run: marginals requested, marg is null");
   if ((mode & PGM_ROWS_JOINT) && !joint) return fail(PGM_EINVAL, "rows_plan_run: joint requested, joint is null");
   if ((mode & PGM_ROWS_JOINT) && h->k.n_comp != 1)
@@ -1372,36 +1674,41 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   if ((mode & PGM_ROWS_MAPGAP) && !gap) return fail(PGM_EINVAL, "rows_plan_run: MAP gap requested, gap is null");
   if ((mode & (PGM_ROWS_MARGINALS | PGM_ROWS_JOINT)) && ld_out < n_rows)
     return fail(PGM_EINVAL, "rows_plan_run: ld_out %lld < n_rows %lld", (long long)ld_out, (long long)n_rows);
-  const RowsK &k = h->k;
-  // LDS: CPT values (if they fit) + per-lane marginal accumulators
+  // one workgroup = 64 rows x RG row groups; W waves split the components
+  RowsK k = h->k;
+  k.n_waves = k.n_comp;  // one wave per component
   const size_t kLds = 64 * 1024;
   size_t vals_bytes = (size_t)((k.n_values + 1) & ~1) * sizeof(double);
-  const bool vals_lds = vals_bytes <= 48 * 1024 && !(mode & PGM_ROWS_VALUES_GLOBAL);
+  const bool vals_lds = vals_bytes <= 40 * 1024 && !(mode & PGM_ROWS_VALUES_GLOBAL);
   if (!vals_lds) vals_bytes = 0;
-  int block = 256;
-  bool acc_lds = false;
-  bool need_acc = false;
-  for (int c = 0; c < k.n_comp; ++c) need_acc |= !k.comp_simple[c] && k.comp_nq[c] > 0;
-  if ((mode & PGM_ROWS_MARGINALS) && need_acc) {
-    while (block > 64 && vals_bytes + (size_t)k.n_marg * block * sizeof(double) > kLds) block >>= 1;
-    acc_lds = vals_bytes + (size_t)k.n_marg * block * sizeof(double) <= kLds;
-    if (!acc_lds) block = 256;
-  }
-  const size_t lds = vals_bytes + (acc_lds ? (size_t)k.n_marg * block * sizeof(double) : 0);
-  const uint64_t blocks = ((uint64_t)n_rows + block - 1) / block;
+  const size_t x_bytes = (size_t)k.n_comp * 64 * (2 * sizeof(double) + sizeof(int32_t));
+  const size_t acc_bytes = (size_t)k.n_marg * 64 * sizeof(double);
+  const bool acc_lds = (mode & PGM_ROWS_MARGINALS) && h->any_table && vals_bytes + x_bytes + acc_bytes <= kLds;
+  const size_t lds = vals_bytes + x_bytes + (acc_lds ? acc_bytes : 0);
+  const uint64_t groups = ((uint64_t)n_rows + 63) / 64;
+  // amortise the LDS staging of the CPT values over several row groups once the grid is large
+  int32_t RG = 1;
+  if (vals_lds && !(mode & PGM_ROWS_ONE_GROUP)) RG = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, groups / 4096));
+  const uint64_t blocks = (groups + RG - 1) / RG;
   if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
-  const dim3 g((unsigned)blocks), b(block);
+  const dim3 g((unsigned)blocks), b(64 * k.n_waves);
   hipStream_t s = S(stream);
   const double *v = h->d_values;
-  const int32_t *t = h->d_tab;
-  if (vals_lds && acc_lds)
-    launch_rows_f<true, true>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+  const int32_t *t = h->d_desc;
+  if (h->all_affine && !(mode & PGM_ROWS_JOINT) && !(mode & PGM_ROWS_GENERIC)) {
+    const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
+    if (vals_lds)
+      launch_affine<true>(h->max_nf, h->max_nt, do_map, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
+    else
+      launch_affine<false>(h->max_nf, h->max_nt, do_map, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
+  } else if (vals_lds && acc_lds)
+    launch_rows_f<true, true>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   else if (vals_lds)
-    launch_rows_f<true, false>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<true, false>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   else if (acc_lds)
-    launch_rows_f<false, true>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<false, true>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   else
-    launch_rows_f<false, false>(h->max_f, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, marg, joint, ld_out, map, gap, err_flag);
+    launch_rows_f<false, false>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

@@ -125,6 +125,19 @@ class PatternPlan:
         comps.sort(key=lambda c: min(order[v] for v in c[0] + c[1]))
         return comps
 
+    def kernel_name(self):
+        """The device kernel pgm_rows_plan_run launches for this plan's marginal/MAP outputs
+        (the all-affine kernel when every component has one query variable, no hidden variable,
+        <= 4 factors and <= 8 evidence terms; pgmhip.hip pgm_rows_plan_create)."""
+        if self.kind != "fused":
+            return None
+        ev = set(self.evidence_vars)
+        for q, h, f in self.components():
+            n_terms = sum(1 for i in f for v in self.factors[i][0] if v in ev)
+            if len(q) != 1 or h or len(f) > 4 or n_terms > 8:
+                return "k_rows"
+        return "k_rows_affine"
+
     def _make_rows_plan(self, split):
         comps = self.components() if split else [(list(self.variables), list(self.hidden),
                                                   list(range(len(self.factors))))]

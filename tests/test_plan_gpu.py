@@ -64,8 +64,12 @@ def test_random_patterns_vs_oracle(gpu, seed):
         df = pd.DataFrame(rows, columns=e)
         col_of = {c: i for i, c in enumerate(e)}
         codes = upload_codes(encode_frame(bn, df))
-        for force in (None, "steps"):
-            plan = PatternPlan(bn, q, e, col_of, force=force)
+        for force in (None, "generic", "steps"):
+            plan = PatternPlan(bn, q, e, col_of, force=None if force == "generic" else force)
+            if force == "generic":  # table-driven kernel even where the all-affine kernel applies
+                from pgmpy_amd import _native as N
+
+                plan.extra_mode = N.ROWS_GENERIC
             out = plan.alloc_outputs(n, marginals=True, joint=True, map_=True)
             plan.run(codes, n, 0, n, out)
             marg, joint, mp = (out["marg"].cpu().numpy(), out["joint"].cpu().numpy(), out["map"].cpu().numpy())
