@@ -290,6 +290,11 @@ def bench_c2(args):
     st = m.states
     evidence = {v: st[v][codes[nodes.index(v), 0]] for v in E}
     ve = VariableElimination(m)
+    torch.cuda.synchronize()
+    t_cold = time.perf_counter()
+    ve.query(q, evidence, show_progress=False)  # first query of the pattern: prune, plan, compile, capture
+    torch.cuda.synchronize()
+    t_cold = time.perf_counter() - t_cold
     for _ in range(args.warmup):
         ve.query(q, evidence, show_progress=False)
     torch.cuda.synchronize()
@@ -299,7 +304,10 @@ def bench_c2(args):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
-            "higher_is_better": False, "steps": args.steps, "result": list(np.asarray(r.values))}
+            "higher_is_better": False, "steps": args.steps, "first_query_s": t_cold,
+            "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
+                    "same query/evidence variables); first_query_s includes pruning, planning and graph capture",
+            "result": list(np.asarray(r.values))}
 
 
 def bench_c4(args):

@@ -128,6 +128,30 @@ typedef struct {
 
 int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream);
 
+/* ---------------------------------------------------------------- dense pairwise step (FP64 MFMA)
+ * C[b, m, n] = sum_k A[b, m, k] * B[b, k, n] with an element stride per group.  The greedy
+ * contraction's pairwise steps that are genuine GEMMs — the two factors share summed-out
+ * variables (k), each keeps its own (m, n), shared kept variables batch (b) — as in the
+ * tensordot/BLAS calls opt_einsum makes for opt_einsum.contract(..., optimize="greedy")
+ * (pgmpy/inference/ExactInference.py:404-406, pgmpy/factors/base.py:106).  Exact fp64 products
+ * (v_mfma_f64_16x16x4_f64); k-summation order differs from a sequential loop.
+ */
+typedef struct {
+  int64_t batch, m, n, k;
+  int64_t sa_b, sa_m, sa_k;
+  int64_t sb_b, sb_k, sb_n;
+  int64_t sc_b, sc_m, sc_n;
+} pgm_gemm_desc;
+
+int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream);
+
+/* ---------------------------------------------------------------- evidence column select
+ * out[j * n_rows + r] = codes[cols[j] * ld + row0 + r]: copies the evidence columns a compiled
+ * plan reads into its own fixed buffer (so the captured graph never sees caller pointers).
+ * cols is a DEVICE int32 array of n_cols column indices. */
+int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32_t *cols, int32_t n_cols,
+                     int64_t n_rows, uint8_t *out, void *stream);
+
 /* ---------------------------------------------------------------- HIP graphs
  * Capture every launch issued on `stream` between begin and end into an executable graph, then
  * replay it with one launch (compiled BP schedules, fixed-shape contraction plans).  The stream

@@ -78,6 +78,11 @@ class ProductNDesc(ctypes.Structure):
     ]
 
 
+class GemmDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("batch", "m", "n", "k", "sa_b", "sa_m", "sa_k", "sb_b", "sb_k", "sb_n",
+                                               "sc_b", "sc_m", "sc_n")]
+
+
 class GatherDesc(ctypes.Structure):
     _fields_ = [
         ("n_keep", ctypes.c_int32),
@@ -143,6 +148,9 @@ _SIGS = {
     "pgm_contract_workspace": ([ctypes.POINTER(ContractDesc), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_product_n": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, _P], ctypes.c_int),
+    "pgm_gemm": ([ctypes.POINTER(GemmDesc), _P, _P, _P, _P], ctypes.c_int),
+    "pgm_codes_select": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, ctypes.c_int64, _P, _P],
+                         ctypes.c_int),
     "pgm_graph_capture_begin": ([_P], ctypes.c_int),
     "pgm_graph_capture_end": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_graph_launch": ([_P, _P], ctypes.c_int),

@@ -25,7 +25,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 4
+#define PGM_ABI_VERSION 6
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -650,6 +650,85 @@ __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, ui
       if (out32) out32[r] = (int32_t)v;
     }
   }
+}
+
+// ----------------------------------------------------------------------------- dense pairwise step
+// C[b, m, n] = sum_k A[b, m, k] B[b, k, n], FP64 MFMA (v_mfma_f64_16x16x4_f64).  A 64x64 output
+// tile per workgroup, 4 waves in 2x2, each wave a 32x32 block = 2x2 MFMA tiles (4 independent
+// accumulators, 16 VGPRs).  K advances 16 at a time through LDS: A staged transposed (As[k][m])
+// so each MFMA operand read is 16 consecutive doubles per k row.  Operand maps (gfx950 f64):
+// lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15]; D[reg r] is row (l>>4)+4r, col l&15.
+struct GemmK {
+  int64_t batch, M, N, K;
+  int64_t sa_b, sa_m, sa_k, sb_b, sb_k, sb_n, sc_b, sc_m, sc_n;
+  uint32_t tiles_n, tiles_m;
+};
+
+__global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *__restrict__ A,
+                                                  const double *__restrict__ B, double *__restrict__ C) {
+  constexpr int BM = 64, BN = 64, BK = 16;
+  __shared__ double As[BK][BM + 2];
+  __shared__ double Bs[BK][BN + 2];
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wy = wave >> 1, wx = wave & 1;
+  // tile order: consecutive workgroups walk n fastest within an m row (A rows stay hot in L2)
+  const uint32_t t = blockIdx.x;
+  const int64_t n0 = (int64_t)(t % p.tiles_n) * BN, m0 = (int64_t)(t / p.tiles_n) * BM;
+  const int64_t b = blockIdx.y;
+  const double *Ab = A + b * p.sa_b;
+  const double *Bb = B + b * p.sb_b;
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // A tile: 64 m x 16 k, k fastest across threads
+      const int e = tid + 256 * i, mm = e >> 4, kk = e & 15;
+      const int64_t gm = m0 + mm, gk = k0 + kk;
+      As[kk][mm] = (gm < p.M && gk < p.K) ? Ab[gm * p.sa_m + gk * p.sa_k] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // B tile: 16 k x 64 n, n fastest across threads
+      const int e = tid + 256 * i, kk = e >> 6, nn = e & 63;
+      const int64_t gk = k0 + kk, gn = n0 + nn;
+      Bs[kk][nn] = (gk < p.K && gn < p.N) ? Bb[gk * p.sb_k + gn * p.sb_n] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      const int kq = 4 * s + (lane >> 4);
+      const double a0 = As[kq][32 * wy + (lane & 15)], a1 = As[kq][32 * wy + 16 + (lane & 15)];
+      const double b0 = Bs[kq][32 * wx + (lane & 15)], b1 = Bs[kq][32 * wx + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  double *Cb = C + b * p.sc_b;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + 32 * wy + 16 * i + (lane >> 4) + 4 * r;
+        const int64_t gn = n0 + 32 * wx + 16 * j + (lane & 15);
+        if (gm < p.M && gn < p.N) Cb[gm * p.sc_m + gn * p.sc_n] = acc[i][j][r];
+      }
+}
+
+// ----------------------------------------------------------------------------- evidence column select
+__global__ __launch_bounds__(256) void k_codes_select(const uint8_t *__restrict__ codes, int64_t ld, int64_t row0,
+                                                      const int32_t *__restrict__ cols, int64_t n_rows,
+                                                      uint8_t *__restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y;
+  if (r < n_rows) out[(int64_t)j * n_rows + r] = codes[(int64_t)cols[j] * ld + row0 + r];
 }
 
 // ----------------------------------------------------------------------------- fused row plan
@@ -1441,6 +1520,46 @@ int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, 
   uint64_t blocks = std::min<uint64_t>((threads + 255) / 256, 65535);
   hipLaunchKernelGGL(k_argmax, dim3((unsigned)blocks), dim3(256), 0, S(stream), X, (uint64_t)n_rows,
                      (uint32_t)row_len, s_row, s_elem, g, out_idx, out_idx32);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream) {
+  if (!d || !A || !B || !C) return fail(PGM_EINVAL, "gemm: null argument");
+  if (d->batch < 0 || d->m < 0 || d->n < 0 || d->k < 0) return fail(PGM_EINVAL, "gemm: negative extent");
+  if (d->batch == 0 || d->m == 0 || d->n == 0) return PGM_OK;
+  GemmK k;
+  k.batch = d->batch;
+  k.M = d->m;
+  k.N = d->n;
+  k.K = d->k;
+  k.sa_b = d->sa_b;
+  k.sa_m = d->sa_m;
+  k.sa_k = d->sa_k;
+  k.sb_b = d->sb_b;
+  k.sb_k = d->sb_k;
+  k.sb_n = d->sb_n;
+  k.sc_b = d->sc_b;
+  k.sc_m = d->sc_m;
+  k.sc_n = d->sc_n;
+  const uint64_t tn = ((uint64_t)d->n + 63) / 64, tm = ((uint64_t)d->m + 63) / 64;
+  if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
+  k.tiles_n = (uint32_t)tn;
+  k.tiles_m = (uint32_t)tm;
+  hipLaunchKernelGGL(k_gemm_f64, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32_t *cols, int32_t n_cols,
+                     int64_t n_rows, uint8_t *out, void *stream) {
+  if (n_cols <= 0 || n_rows <= 0) return PGM_OK;
+  if (!codes || !cols || !out) return fail(PGM_EINVAL, "codes_select: null argument");
+  if (n_cols > 65535) return fail(PGM_EINVAL, "codes_select: too many columns");
+  const uint64_t bx = ((uint64_t)n_rows + 255) / 256;
+  if (bx > 0x7fffffffull) return fail(PGM_EINVAL, "codes_select: too many rows");
+  hipLaunchKernelGGL(k_codes_select, dim3((unsigned)bx, (unsigned)n_cols), dim3(256), 0, S(stream), codes, ld, row0,
+                     cols, n_rows, out);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

@@ -140,6 +140,106 @@ def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
     return out
 
 
+GEMM_MIN_M = GEMM_MIN_N = 16
+GEMM_MIN_K = 8
+GEMM_MIN_FLOPS = 1 << 22
+
+
+def _group_stride(t, ls, group, card):
+    """One element stride for `group` (labels in that order) of tensor t[ls], or None if the
+    group's axes do not collapse into a single strided run."""
+    if not group:
+        return 0
+    strides = [int(t.stride(ls.index(l))) for l in group]
+    for i in range(len(group) - 1):
+        if strides[i] != strides[i + 1] * card[group[i + 1]]:
+            return None
+    return strides[-1]
+
+
+def gemm_shape(la, lb, keep, card, force=False):
+    """Classify the pairwise step sum_{(la|lb) - keep} A[la] B[lb] as a dense GEMM.
+
+    Returns (batch, M, N, K) label lists — batch: in both operands and kept; M: A only; N: B only;
+    K: in both, summed — or None when it is not GEMM-shaped (a label summed out of one operand
+    alone, M/N below 16 states, K below 8, or under 4 MFLOP unless force)."""
+    sa, sb, sk = set(la), set(lb), set(keep)
+    if len(sa) != len(la) or len(sb) != len(lb) or not sk <= (sa | sb):
+        return None
+    if any(l not in sk and l not in sb for l in la) or any(l not in sk and l not in sa for l in lb):
+        return None
+    batch = [l for l in la if l in sb and l in sk]
+    Ms = [l for l in la if l not in sb]
+    Ns = [l for l in lb if l not in sa]
+    Ks = [l for l in la if l in sb and l not in sk]
+
+    def prod(g):
+        p = 1
+        for l in g:
+            p *= int(card[l])
+        return p
+
+    nb, m, n, k = prod(batch), prod(Ms), prod(Ns), prod(Ks)
+    small = 2 * nb * m * n * k < GEMM_MIN_FLOPS and not force
+    if k < GEMM_MIN_K or m < GEMM_MIN_M or n < GEMM_MIN_N or small or nb > 65535:
+        return None
+    return batch, Ms, Ns, Ks
+
+
+def prepare_gemm(A, la, B, lb, shape, copy_fn=None):
+    """Descriptor for the dense step `shape` = (batch, M, N, K) of A[la] x B[lb] (gemm_shape).
+    Operands whose groups do not collapse into one stride each are packed with copy_fn
+    (default: an immediate contract copy).  Returns (desc, A, B, C, out_labels)."""
+    copy_fn = copy_fn or (lambda T, lt, lo: contract(T, lt, None, None, lo, combine="copy"))
+    la, lb = list(la), list(lb)
+    card = {l: int(A.shape[i]) for i, l in enumerate(la)}
+    for i, l in enumerate(lb):
+        if card.setdefault(l, int(B.shape[i])) != int(B.shape[i]):
+            raise ValueError(f"cardinality mismatch for {l!r}")
+    batch, Ms, Ns, Ks = shape
+
+    def prod(g):
+        p = 1
+        for l in g:
+            p *= card[l]
+        return p
+
+    nb, m, n, k = prod(batch), prod(Ms), prod(Ns), prod(Ks)
+    strides_a = [_group_stride(A, la, g, card) for g in (batch, Ms, Ks)]
+    if None in strides_a:
+        A = copy_fn(A, la, batch + Ms + Ks)
+        la = batch + Ms + Ks
+        strides_a = [_group_stride(A, la, g, card) for g in (batch, Ms, Ks)]
+    strides_b = [_group_stride(B, lb, g, card) for g in (batch, Ks, Ns)]
+    if None in strides_b:
+        B = copy_fn(B, lb, batch + Ks + Ns)
+        lb = batch + Ks + Ns
+        strides_b = [_group_stride(B, lb, g, card) for g in (batch, Ks, Ns)]
+    out_labels = batch + Ms + Ns
+    C = empty([card[l] for l in out_labels])
+    d = N.GemmDesc()
+    d.batch, d.m, d.n, d.k = nb, m, n, k
+    d.sa_b, d.sa_m, d.sa_k = strides_a
+    d.sb_b, d.sb_k, d.sb_n = strides_b
+    d.sc_b, d.sc_m, d.sc_n = m * n, n, 1
+    return d, A, B, C, out_labels
+
+
+def pair_gemm(A, la, B, lb, keep, force=False, shape=None):
+    """sum over (la | lb) - keep of A[la] * B[lb], on FP64 MFMA (pgm_gemm) when the step is a
+    dense GEMM (gemm_shape).  Returns (C, batch + M + N labels), C-order, or None for the
+    generic fused contraction.  force=True skips only the minimum-work threshold (tests)."""
+    if shape is None:
+        card = {l: int(A.shape[i]) for i, l in enumerate(la)}
+        card.update({l: int(B.shape[i]) for i, l in enumerate(lb)})
+        shape = gemm_shape(list(la), list(lb), keep, card, force)
+        if shape is None:
+            return None
+    d, A, B, C, out_labels = prepare_gemm(A, la, B, lb, shape)
+    N.check(N.lib().pgm_gemm(ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C), N.stream_handle()), "gemm")
+    return C, out_labels
+
+
 def prepare_product_n(operands, out_labels, out=None, kinds=None):
     """Descriptor for C[out_labels] = prod_i X_i (broadcast, no reduction), up to 8 operands.
 
@@ -227,14 +327,8 @@ def argmax_rows(A, la, row_label=None):
     return out
 
 
-def gather(A, la, evidence, out_labels, codes=None, ld=0, row0=0, n_rows=None, err=None):
-    """Evidence reduce.
-
-    evidence: {label: state} (static) or {label: column} with `codes` (uint8
-    device tensor [n_cols, ld]) giving per-row states; per-row gathers need
-    ROW in out_labels.  Labels of A that are in `evidence` are dropped."""
-    L = N.lib()
-    torch = _torch()
+def prepare_gather(A, la, evidence, out_labels, codes=None, ld=0, row0=0, n_rows=None):
+    """(desc, A pointer, out) for gather(); see there."""
     la = list(la)
     static = {l: s for l, s in evidence.items() if codes is None or not isinstance(s, tuple)}
     dynamic = {l: s[1] for l, s in evidence.items() if codes is not None and isinstance(s, tuple)}
@@ -265,10 +359,21 @@ def gather(A, la, evidence, out_labels, codes=None, ld=0, row0=0, n_rows=None, e
         d.ev_col[j] = int(col)
         d.ev_stride[j] = int(A.stride(la.index(l)))
         d.ev_card[j] = card[l]
+    return d, ctypes.c_void_p(A.data_ptr() + 8 * base), out
+
+
+def gather(A, la, evidence, out_labels, codes=None, ld=0, row0=0, n_rows=None, err=None):
+    """Evidence reduce.
+
+    evidence: {label: state} (static) or {label: column} with `codes` (uint8
+    device tensor [n_cols, ld]) giving per-row states; per-row gathers need
+    ROW in out_labels.  Labels of A that are in `evidence` are dropped."""
+    L = N.lib()
+    torch = _torch()
+    d, Aptr, out = prepare_gather(A, la, evidence, out_labels, codes, ld, row0, n_rows)
     own_err = err is None and d.n_ev > 0
     if own_err:
         err = torch.zeros(1, dtype=torch.int32, device=A.device)
-    Aptr = ctypes.c_void_p(A.data_ptr() + 8 * base)
     N.check(L.pgm_gather(ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err), N.stream_handle()), "gather")
     if own_err and int(err.item()) != 0:
         raise IndexError("evidence state code out of range for its variable")

@@ -27,6 +27,8 @@ def _is_scalar(x):
 class DiscreteFactor(BaseFactor, StateNameMixin):
     """Factor over discrete variables (DiscreteFactor.py:16-127)."""
 
+    _version = 0  # bumped whenever the values may change (compiled plans check it)
+
     def __init__(self, variables, cardinality, values, state_names={}):
         if isinstance(variables, str):
             raise TypeError("Variables: Expected type list or array like, got string")
@@ -58,16 +60,27 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
             self._host = E.to_host(self._dev)
         # the host array is handed out (callers may edit it in place): it becomes authoritative
         self._dev = None
+        self._version += 1
         return self._host
 
     @values.setter
     def values(self, v):
+        self._version += 1
         if _is_device(v):
             self._dev = v
             self._host = None
         else:
             self._host = np.asarray(v, dtype=np.float64)
             self._dev = None
+
+    def _values_readonly(self):
+        """Host values for internal readers (plan compilers): a read-only view, the device copy
+        stays valid and the version is unchanged."""
+        if self._host is None:
+            self._host = E.to_host(self._dev)
+        v = self._host.view()
+        v.flags.writeable = False
+        return v
 
     def _d(self):
         """Device tensor of the values (uploaded on first use)."""
@@ -77,6 +90,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         return self._dev
 
     def _set_d(self, t):
+        self._version += 1
         self._dev = t
         self._host = None
 

@@ -13,11 +13,14 @@ vendored) plans a greedy path; its published greedy strategy is restated here:
      smallest operands.
 
 Every pairwise step is ONE fused product+marginalize kernel (pgm_contract,
-combine=MUL, reduce=SUM): the broadcast product is never materialised.  A
+combine=MUL, reduce=SUM): the broadcast product is never materialised.  Steps
+that are dense GEMMs (shared summed variables of total cardinality >= 8, each
+side keeping >= 16 states) run on FP64 MFMA instead (pgm_gemm, engine.pair_gemm).  A
 ``ROW`` label (evidence rows) is just another kept label, so the same planner
 and executor run single queries (C2) and row batches.
 """
 import heapq
+from collections import OrderedDict
 from itertools import count
 
 import numpy as np
@@ -122,7 +125,7 @@ def plan_stats(operand_labels, out_labels, dims):
     steps, _ = greedy_path(operand_labels, out_labels, dims)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     nbytes = flops = 0
-    max_inter = 0
+    max_inter = sum_inter = 0
     for st in steps:
         if st[0] == "reduce":
             _, i, keep, nid = st
@@ -135,14 +138,52 @@ def plan_stats(operand_labels, out_labels, dims):
             flops += 2 * _size(union, dims)
         labels[nid] = keep
         max_inter = max(max_inter, _size(keep, dims))
-    return {"steps": len(steps), "bytes": nbytes, "flops": flops, "max_intermediate": max_inter}
+        sum_inter += _size(keep, dims)
+    return {"steps": len(steps), "bytes": nbytes, "flops": flops, "max_intermediate": max_inter,
+            "sum_intermediate": sum_inter}
 
 
-def contract_factors(operands, out_labels, reduce="sum"):
+_PATHS = OrderedDict()  # compiled paths, keyed on the operands' (label, cardinality) structure
+PATH_CACHE_SIZE = 256
+
+
+def compiled_path(operand_labels, out_labels, dims):
+    """greedy_path plus, per pairwise step, the dense-GEMM classification (engine.gemm_shape),
+    cached on the contraction's structure: repeated queries with the same query / evidence
+    variables (C2's pattern; every row batch of a predict pattern) re-plan nothing."""
+    key = (tuple(tuple((l, int(dims[l])) for l in ls) for ls in operand_labels), tuple(out_labels))
+    hit = _PATHS.get(key)
+    if hit is not None:
+        _PATHS.move_to_end(key)
+        return hit
+    steps, final_id = greedy_path(operand_labels, out_labels, dims)
+    labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    plan = []
+    for st in steps:
+        if st[0] == "reduce":
+            labels[st[3]] = st[2]
+            plan.append((st, None))
+            continue
+        _, i, j, keep, nid = st
+        shape = E.gemm_shape(labels[i], labels[j], keep, dims)
+        # a GEMM step's result is laid out batch + M + N; later steps see those labels
+        labels[nid] = (shape[0] + shape[1] + shape[2]) if shape is not None else keep
+        plan.append((st, shape))
+    hit = (plan, final_id)
+    _PATHS[key] = hit
+    if len(_PATHS) > PATH_CACHE_SIZE:
+        _PATHS.popitem(last=False)
+    return hit
+
+
+def contract_factors(operands, out_labels, reduce="sum", prog=None):
     """sum_{labels not in out} prod operands, on the device.
 
     operands: list of (device tensor, labels).  Returns a tensor over
-    out_labels (C-order).  reduce="max" gives the max-product variant."""
+    out_labels (C-order).  reduce="max" gives the max-product variant.  With a
+    pgmpy_amd.program.Program the launches are recorded (buffers preallocated)
+    instead of issued."""
+    run = prog if prog is not None else E
     if not operands:
         raise ValueError("nothing to contract")
     dims = {}
@@ -156,19 +197,23 @@ def contract_factors(operands, out_labels, reduce="sum"):
     for l in out_labels:
         if l not in dims:
             raise ValueError(f"output label {l!r} not in any operand")
-    steps, final_id = greedy_path([ls for _, ls in operands], out_labels, dims)
+    plan, final_id = compiled_path([ls for _, ls in operands], out_labels, dims)
     live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
-    for st in steps:
+    for st, shape in plan:
         if st[0] == "reduce":
             _, i, keep, nid = st
             t, ls = live.pop(i)
-            live[nid] = (E.contract(t, ls, None, None, keep, reduce=reduce, combine="copy"), keep)
+            live[nid] = (run.contract(t, ls, None, None, keep, reduce=reduce, combine="copy"), keep)
         else:
             _, i, j, keep, nid = st
             ti, li = live.pop(i)
             tj, lj = live.pop(j)
-            live[nid] = (E.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
+            if shape is not None and reduce == "sum":
+                live[nid] = (prog.pair_gemm(ti, li, tj, lj, shape) if prog is not None
+                             else E.pair_gemm(ti, li, tj, lj, keep, shape=shape))
+            else:
+                live[nid] = (run.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
     t, ls = live[final_id]
     if ls != list(out_labels):
-        t = E.contract(t, ls, None, None, list(out_labels), reduce=reduce, combine="copy")
+        t = run.contract(t, ls, None, None, list(out_labels), reduce=reduce, combine="copy")
     return t

@@ -201,7 +201,7 @@ class PatternPlan:
         """CPT values (C-order) of factor fi, packed into the plan (a copy, no arithmetic)."""
         cache = self.__dict__.setdefault("_vals_cache", {})
         if fi not in cache:
-            cache[fi] = np.ascontiguousarray(self.factors[fi][1].values, dtype=np.float64).reshape(-1)
+            cache[fi] = np.ascontiguousarray(self.factors[fi][1]._values_readonly(), dtype=np.float64).reshape(-1)
         return cache[fi]
 
     def _build_fused(self):
@@ -297,54 +297,109 @@ class PatternPlan:
             self._dev_cache = [(cpd._d(), vars_) for vars_, cpd in self.factors]
         return self._dev_cache
 
-    def max_intermediate_per_row(self):
-        labels, dims = [], dict(self.card)
-        dims[E.ROW] = 1
-        for vars_, _ in self.factors:
-            ls = [v for v in vars_ if v not in self.evidence_vars]
-            if any(v in self.evidence_vars for v in vars_):
-                ls = ls + [E.ROW]
-            labels.append(ls)
-        return max(1, plan_stats(labels, self.variables + [E.ROW], dims)["max_intermediate"])
+    def intermediates_per_row(self):
+        """(largest, total) intermediate entries per evidence row of the steps path."""
+        if not hasattr(self, "_inter"):
+            labels, dims = [], dict(self.card)
+            dims[E.ROW] = 1
+            for vars_, _ in self.factors:
+                ls = [v for v in vars_ if v not in self.evidence_vars]
+                if any(v in self.evidence_vars for v in vars_):
+                    ls = ls + [E.ROW]
+                labels.append(ls)
+            st = plan_stats(labels, self.variables + [E.ROW], dims)
+            self._inter = (max(1, st["max_intermediate"]), max(1, st["sum_intermediate"]))
+        return self._inter
 
-    def _run_steps(self, codes, ld, row0, n_rows, out, err):
-        """Batched greedy contraction with an evidence-row axis; rows chunked to bound memory."""
+    def max_intermediate_per_row(self):
+        return self.intermediates_per_row()[0]
+
+    def _steps_chunk(self, n_rows):
+        """Rows per compiled steps program: every intermediate is preallocated, so bound both the
+        largest one (2^26 entries) and their sum (2^28 entries = 2 GiB)."""
+        mx, tot = self.intermediates_per_row()
+        return max(1, min(n_rows, (1 << 26) // mx, (1 << 28) // tot))
+
+    def _steps_program(self, n, outs):
+        """The steps path for n rows compiled once: evidence gathers from the plan's own codes
+        buffer, the greedy contraction (dense steps on FP64 MFMA), normalisation and the requested
+        outputs into preallocated buffers, captured as one HIP graph."""
+        progs = self.__dict__.setdefault("_progs", {})
+        hit = progs.get((n, outs))
+        if hit is not None:
+            return hit
         import torch
 
-        L = N.lib()
+        from ..program import Program
+
+        dev = E.device()
+        prog = Program()
         ev_set = set(self.evidence_vars)
-        per_row = self.max_intermediate_per_row()
-        chunk = max(1, min(n_rows, (1 << 26) // per_row))
+        cols = list(self.ev_used)
+        local = {v: i for i, v in enumerate(cols)}
+        codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
+        perr = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops = []
+        for t, vars_ in self._dev_factors():
+            rem = [v for v in vars_ if v not in ev_set]
+            dyn = {v: (None, local[v]) for v in vars_ if v in ev_set}
+            if dyn:
+                g = prog.gather(t, vars_, dyn, rem + [E.ROW], codes_buf, n, 0, n, perr)
+                ops.append((g, rem + [E.ROW]))
+            else:
+                ops.append((t, list(vars_)))
+        outl = self.variables + [E.ROW]
+        if not any(E.ROW in ls for _, ls in ops):
+            # no evidence touches this pattern: broadcast one result over the rows
+            ops.append((E.to_device(np.ones(n)), [E.ROW]))
+        R = contract_factors(ops, outl, prog=prog)  # [Q..., ROW] C-order
+        Z = prog.contract(R, outl, None, None, [E.ROW], reduce="sum", combine="copy")
+        bufs = {}
+        if "marg" in outs:
+            bufs["marg"] = E.empty([self.n_acc, n])
+            for i, v in enumerate(self.variables):
+                a = self.acc_off[i]
+                m = prog.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
+                prog.contract(m, [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw",
+                              out=bufs["marg"][a:a + self.cards[i]])
+        if "map" in outs:
+            bufs["map"] = torch.empty(n, dtype=torch.int32, device=dev)
+            prog.argmax(R, n, self.P, 1, n, bufs["map"])
+        if "joint" in outs:
+            bufs["joint"] = E.empty([self.P, n])
+            prog.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw",
+                          out=bufs["joint"])
+        prog.capture()
+        cols_dev = torch.tensor([self.col_of[v] for v in cols], dtype=torch.int32, device=dev) if cols else None
+        hit = (prog, codes_buf, perr, bufs, cols_dev)
+        progs[(n, outs)] = hit
+        return hit
+
+    def _run_steps(self, codes, ld, row0, n_rows, out, err):
+        """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
+        replay of a compiled program (_steps_program)."""
+        L = N.lib()
+        s = N.stream_handle()
+        outs = frozenset(k for k in ("marg", "joint", "map") if k in out)
+        chunk = self._steps_chunk(n_rows)
         for c0 in range(0, n_rows, chunk):
             n = min(chunk, n_rows - c0)
-            ops = []
-            for t, vars_ in self._dev_factors():
-                rem = [v for v in vars_ if v not in ev_set]
-                dyn = {v: (None, self.col_of[v]) for v in vars_ if v in ev_set}
-                if dyn:
-                    g = E.gather(t, vars_, dyn, rem + [E.ROW], codes=codes, ld=ld, row0=row0 + c0, n_rows=n, err=err)
-                    ops.append((g, rem + [E.ROW]))
-                else:
-                    ops.append((t, list(vars_)))
-            outl = self.variables + [E.ROW]
-            if not any(E.ROW in ls for _, ls in ops):
-                # no evidence touches this pattern: broadcast one result over the rows
-                ones = E.to_device(np.ones(n))
-                ops.append((ones, [E.ROW]))
-            R = contract_factors(ops, outl)  # [Q..., ROW] C-order
-            Z = E.contract(R, outl, None, None, [E.ROW], reduce="sum", combine="copy")
+            prog, cbuf, perr, bufs, cols_dev = self._steps_program(n, outs)
+            if cols_dev is not None:
+                N.check(L.pgm_codes_select(N.ptr(codes), int(ld), int(row0 + c0), N.ptr(cols_dev), len(self.ev_used),
+                                           int(n), N.ptr(cbuf), s), "codes_select")
+            N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset")
+            prog.run()
             if "marg" in out:
-                for i, v in enumerate(self.variables):
-                    a = self.acc_off[i]
-                    view = out["marg"][a:a + self.cards[i], c0:c0 + n]
-                    m = E.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
-                    E.contract(m, [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw", out=view)
-            if "map" in out:
-                N.check(L.pgm_argmax(N.ptr(R), n, self.P, 1, n, None, N.ptr(out["map"][c0:c0 + n]),
-                                     N.stream_handle()), "argmax")
+                E.contract(bufs["marg"], ["a", E.ROW], None, None, ["a", E.ROW], combine="copy",
+                           out=out["marg"][:, c0:c0 + n])
             if "joint" in out:
-                jv = out["joint"][:, c0:c0 + n]
-                E.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw", out=jv)
+                E.contract(bufs["joint"], ["q", E.ROW], None, None, ["q", E.ROW], combine="copy",
+                           out=out["joint"][:, c0:c0 + n])
+            if "map" in out:
+                N.check(L.pgm_memcpy_d2d(N.ptr(out["map"][c0:c0 + n]), N.ptr(bufs["map"]), 4 * n, s), "memcpy")
+            if err is not None and int(perr.item()) != 0:
+                N.check(L.pgm_memset(N.ptr(err), 1, 4, s), "memset")
         return out
 
     # ------------------------------------------------------------------ accounting

@@ -52,6 +52,30 @@ class Program:
         self._steps.append(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"))
         return out
 
+    def gather(self, A, la, evidence, out_labels, codes, ld, row0, n_rows, err=None):
+        d, Aptr, out = E.prepare_gather(A, la, evidence, out_labels, codes, ld, row0, n_rows)
+        L = N.lib()
+        args = (ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err))
+        self._keep.extend([d, A, codes, out, err])
+        self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
+        return out
+
+    def pair_gemm(self, A, la, B, lb, shape):
+        """Recorded dense step (engine.prepare_gemm); packing copies are recorded too."""
+        d, A, B, C, out_labels = E.prepare_gemm(
+            A, la, B, lb, shape, copy_fn=lambda T, lt, lo: self.contract(T, lt, None, None, lo, combine="copy"))
+        L = N.lib()
+        args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C))
+        self._keep.extend([d, A, B, C])
+        self._steps.append(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"))
+        return C, out_labels
+
+    def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):
+        L = N.lib()
+        args = (N.ptr(X), int(n_rows), int(row_len), int(s_row), int(s_elem), None, N.ptr(out32))
+        self._keep.extend([X, out32])
+        self._steps.append(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"))
+
     # ------------------------------------------------------------------ execution
     def run(self, stream=None):
         s = N.stream_handle(stream)
