@@ -129,18 +129,21 @@ typedef struct {
 int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream);
 
 /* ---------------------------------------------------------------- dense pairwise step (FP64 MFMA)
- * C[b, m, n] = sum_k A[b, m, k] * B[b, k, n] with an element stride per group.  The greedy
- * contraction's pairwise steps that are genuine GEMMs — the two factors share summed-out
- * variables (k), each keeps its own (m, n), shared kept variables batch (b) — as in the
- * tensordot/BLAS calls opt_einsum makes for opt_einsum.contract(..., optimize="greedy")
+ * C[b, m, n] = sum_k A[b, m, k] * B[b, k, n] where each index is a GROUP of variables laid out in
+ * any order inside its tensor: the element offsets come from a DEVICE int64 table,
+ *   offsets = [A_b (batch) | B_b (batch) | C_b (batch) | A_m (m) | C_m (m) | A_k (k) | B_k (k) |
+ *              B_n (n) | C_n (n)]
+ * so A is read at A[A_b[b] + A_m[m] + A_k[k]] and C written at C[C_b[b] + C_m[m] + C_n[n]].
+ * These are the greedy contraction's pairwise steps that are genuine GEMMs — the two factors
+ * share summed-out variables (k), each keeps its own (m, n), shared kept variables batch (b) —
+ * as in the tensordot/BLAS calls opt_einsum makes for opt_einsum.contract(..., "greedy")
  * (pgmpy/inference/ExactInference.py:404-406, pgmpy/factors/base.py:106).  Exact fp64 products
- * (v_mfma_f64_16x16x4_f64); k-summation order differs from a sequential loop.
+ * (v_mfma_f64_16x16x4_f64); the k-summation order differs from a sequential loop.
  */
 typedef struct {
   int64_t batch, m, n, k;
-  int64_t sa_b, sa_m, sa_k;
-  int64_t sb_b, sb_k, sb_n;
-  int64_t sc_b, sc_m, sc_n;
+  const int64_t *offsets; /* device, 3*batch + 2*m + 2*k + 2*n entries */
+  int64_t stride[9];      /* per table part: >= 0 -> offset = index * stride (table not read), -1 -> table */
 } pgm_gemm_desc;
 
 int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream);

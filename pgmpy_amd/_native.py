@@ -79,8 +79,8 @@ class ProductNDesc(ctypes.Structure):
 
 
 class GemmDesc(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int64) for n in ("batch", "m", "n", "k", "sa_b", "sa_m", "sa_k", "sb_b", "sb_k", "sb_n",
-                                               "sc_b", "sc_m", "sc_n")]
+    _fields_ = [("batch", ctypes.c_int64), ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("k", ctypes.c_int64),
+                ("offsets", ctypes.c_void_p), ("stride", ctypes.c_int64 * 9)]
 
 
 class GatherDesc(ctypes.Structure):

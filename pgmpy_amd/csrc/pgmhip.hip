@@ -25,7 +25,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 6
+#define PGM_ABI_VERSION 7
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -653,17 +653,28 @@ __global__ __launch_bounds__(256) void k_argmax(const double *__restrict__ X, ui
 }
 
 // ----------------------------------------------------------------------------- dense pairwise step
-// C[b, m, n] = sum_k A[b, m, k] B[b, k, n], FP64 MFMA (v_mfma_f64_16x16x4_f64).  A 64x64 output
-// tile per workgroup, 4 waves in 2x2, each wave a 32x32 block = 2x2 MFMA tiles (4 independent
-// accumulators, 16 VGPRs).  K advances 16 at a time through LDS: A staged transposed (As[k][m])
-// so each MFMA operand read is 16 consecutive doubles per k row.  Operand maps (gfx950 f64):
-// lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15]; D[reg r] is row (l>>4)+4r, col l&15.
+// C[b, m, n] = sum_k A[b, m, k] B[b, k, n], FP64 MFMA (v_mfma_f64_16x16x4_f64), every index a
+// group of variables addressed through a per-index offset table (any label interleaving, no
+// packing copies; C written directly in the planner's label order).  A 64x64 output tile per
+// workgroup, 4 waves in 2x2, each wave a 32x32 block = 2x2 MFMA tiles (4 independent
+// accumulators).  K advances 16 at a time through LDS, A staged transposed (As[k][m]) so each
+// operand read is 16 consecutive doubles per k row; the next K tile's global loads are issued
+// before the current tile's MFMAs (register prefetch).  Operand maps (gfx950 f64): lane l holds
+// A[l&15][k=l>>4], B[k=l>>4][l&15]; D[reg r] is row (l>>4)+4r, col l&15.
 struct GemmK {
   int64_t batch, M, N, K;
-  int64_t sa_b, sa_m, sa_k, sb_b, sb_k, sb_n, sc_b, sc_m, sc_n;
-  uint32_t tiles_n, tiles_m;
+  const int64_t *a_b, *b_b, *c_b, *a_m, *c_m, *a_k, *b_k, *b_n, *c_n;
+  int64_t s_ab, s_bb, s_cb, s_am, s_cm, s_ak, s_bk, s_bn, s_cn;  // >= 0: strided group, -1: table
+  uint32_t tiles_n;
 };
+// offset of index i of a group: the table (TAB) or a single stride (every group collapses)
+template <bool TAB>
+__device__ __forceinline__ int64_t goff(int64_t s, const int64_t *tab, int64_t i) {
+  if constexpr (TAB) return tab[i];
+  else return i * s;
+}
 
+template <bool TAB>
 __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *__restrict__ A,
                                                   const double *__restrict__ B, double *__restrict__ C) {
   constexpr int BM = 64, BN = 64, BK = 16;
@@ -672,31 +683,56 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   typedef double d4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wy = wave >> 1, wx = wave & 1;
-  // tile order: consecutive workgroups walk n fastest within an m row (A rows stay hot in L2)
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = blockIdx.x;  // n fastest within an m row of tiles (A rows stay hot in L2)
   const int64_t n0 = (int64_t)(t % p.tiles_n) * BN, m0 = (int64_t)(t / p.tiles_n) * BM;
   const int64_t b = blockIdx.y;
-  const double *Ab = A + b * p.sa_b;
-  const double *Bb = B + b * p.sb_b;
+  const double *Ab = A + goff<TAB>(p.s_ab, p.a_b, b);
+  const double *Bb = B + goff<TAB>(p.s_bb, p.b_b, b);
+  // this thread's fixed tile rows (A: 4 m rows, k = tid & 15) and columns (B: 4 k rows, n = tid & 63)
+  int64_t arow[4];
+  bool aok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t gm = m0 + ((tid + 256 * i) >> 4);
+    aok[i] = gm < p.M;
+    arow[i] = aok[i] ? goff<TAB>(p.s_am, p.a_m, gm) : 0;
+  }
+  const int64_t gn = n0 + (tid & 63);
+  const bool bok = gn < p.N;
+  const int64_t bcol = bok ? goff<TAB>(p.s_bn, p.b_n, gn) : 0;
+  double ra[4], rb[4];
+  // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
+  auto load = [&](int64_t k0) {
+    const int64_t gka = k0 + (tid & 15);
+    const bool ka = gka < p.K;
+    const int64_t oka = goff<TAB>(p.s_ak, p.a_k, ka ? gka : p.K - 1);
+    double va[4], vb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) va[i] = Ab[arow[i] + oka];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t gkb = k0 + ((tid + 256 * i) >> 6);
+      vb[i] = Bb[goff<TAB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1) + bcol];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i] = (aok[i] && ka) ? va[i] : 0.0;
+      rb[i] = (bok && k0 + ((tid + 256 * i) >> 6) < p.K) ? vb[i] : 0.0;
+    }
+  };
   d4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  load(0);
   for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // A tile: 64 m x 16 k, k fastest across threads
-      const int e = tid + 256 * i, mm = e >> 4, kk = e & 15;
-      const int64_t gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < p.M && gk < p.K) ? Ab[gm * p.sa_m + gk * p.sa_k] : 0.0;
-    }
+    for (int i = 0; i < 4; ++i) As[tid & 15][(tid + 256 * i) >> 4] = ra[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // B tile: 16 k x 64 n, n fastest across threads
-      const int e = tid + 256 * i, kk = e >> 6, nn = e & 63;
-      const int64_t gk = k0 + kk, gn = n0 + nn;
-      Bs[kk][nn] = (gk < p.K && gn < p.N) ? Bb[gk * p.sb_k + gn * p.sb_n] : 0.0;
-    }
+    for (int i = 0; i < 4; ++i) Bs[(tid + 256 * i) >> 6][tid & 63] = rb[i];
     __syncthreads();
+    if (k0 + BK < p.K) load(k0 + BK);  // in flight during this tile's MFMAs
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int kq = 4 * s + (lane >> 4);
@@ -709,17 +745,20 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
     }
     __syncthreads();
   }
-  double *Cb = C + b * p.sc_b;
+  double *Cb = C + goff<TAB>(p.s_cb, p.c_b, b);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j) {
+    const int64_t cn = n0 + 32 * wx + 16 * j + (lane & 15);
+    if (cn >= p.N) continue;
+    const int64_t ocn = goff<TAB>(p.s_cn, p.c_n, cn);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t gm = m0 + 32 * wy + 16 * i + (lane >> 4) + 4 * r;
-        const int64_t gn = n0 + 32 * wx + 16 * j + (lane & 15);
-        if (gm < p.M && gn < p.N) Cb[gm * p.sc_m + gn * p.sc_n] = acc[i][j][r];
+        const int64_t cm = m0 + 32 * wy + 16 * i + (lane >> 4) + 4 * r;
+        if (cm < p.M) Cb[goff<TAB>(p.s_cm, p.c_m, cm) + ocn] = acc[i][j][r];
       }
+  }
 }
 
 // ----------------------------------------------------------------------------- evidence column select
@@ -1525,7 +1564,7 @@ int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, 
 }
 
 int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream) {
-  if (!d || !A || !B || !C) return fail(PGM_EINVAL, "gemm: null argument");
+  if (!d || !A || !B || !C || !d->offsets) return fail(PGM_EINVAL, "gemm: null argument");
   if (d->batch < 0 || d->m < 0 || d->n < 0 || d->k < 0) return fail(PGM_EINVAL, "gemm: negative extent");
   if (d->batch == 0 || d->m == 0 || d->n == 0) return PGM_OK;
   GemmK k;
@@ -1533,20 +1572,35 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   k.M = d->m;
   k.N = d->n;
   k.K = d->k;
-  k.sa_b = d->sa_b;
-  k.sa_m = d->sa_m;
-  k.sa_k = d->sa_k;
-  k.sb_b = d->sb_b;
-  k.sb_k = d->sb_k;
-  k.sb_n = d->sb_n;
-  k.sc_b = d->sc_b;
-  k.sc_m = d->sc_m;
-  k.sc_n = d->sc_n;
+  const int64_t *o = d->offsets;
+  k.a_b = o;
+  k.b_b = o + d->batch;
+  k.c_b = o + 2 * d->batch;
+  k.a_m = o + 3 * d->batch;
+  k.c_m = k.a_m + d->m;
+  k.a_k = k.c_m + d->m;
+  k.b_k = k.a_k + d->k;
+  k.b_n = k.b_k + d->k;
+  k.c_n = k.b_n + d->n;
+  k.s_ab = d->stride[0];
+  k.s_bb = d->stride[1];
+  k.s_cb = d->stride[2];
+  k.s_am = d->stride[3];
+  k.s_cm = d->stride[4];
+  k.s_ak = d->stride[5];
+  k.s_bk = d->stride[6];
+  k.s_bn = d->stride[7];
+  k.s_cn = d->stride[8];
   const uint64_t tn = ((uint64_t)d->n + 63) / 64, tm = ((uint64_t)d->m + 63) / 64;
   if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
-  k.tiles_m = (uint32_t)tm;
-  hipLaunchKernelGGL(k_gemm_f64, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
+  bool tab = false;
+  for (int i = 0; i < 9; ++i) tab |= d->stride[i] < 0;
+  if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
+  if (tab)
+    hipLaunchKernelGGL(k_gemm_f64<true>, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
+  else
+    hipLaunchKernelGGL(k_gemm_f64<false>, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

@@ -48,6 +48,17 @@ def to_device(arr):
     return t
 
 
+def to_device_i64(arr):
+    """Host int64 array -> device int64 tensor (descriptor tables)."""
+    torch = _torch()
+    a = np.ascontiguousarray(arr, dtype=np.int64)
+    t = torch.empty(a.shape, dtype=torch.int64, device=device())
+    if a.size:
+        N.check(N.lib().pgm_memcpy_h2d(N.ptr(t), a.ctypes.data_as(ctypes.c_void_p), a.nbytes, N.stream_handle()),
+                "memcpy_h2d")
+    return t
+
+
 def to_host(t):
     """Device tensor -> numpy (C-order copy of its logical contents)."""
     L = N.lib()
@@ -145,16 +156,17 @@ GEMM_MIN_K = 8
 GEMM_MIN_FLOPS = 1 << 22
 
 
-def _group_stride(t, ls, group, card):
-    """One element stride for `group` (labels in that order) of tensor t[ls], or None if the
-    group's axes do not collapse into a single strided run."""
-    if not group:
-        return 0
-    strides = [int(t.stride(ls.index(l))) for l in group]
-    for i in range(len(group) - 1):
-        if strides[i] != strides[i + 1] * card[group[i + 1]]:
-            return None
-    return strides[-1]
+def _group_offsets(t, ls, group, card):
+    """(offsets, stride): element offset of every index of `group` (labels, C-order over the group)
+    in tensor t[ls]; stride is the single element stride when the group collapses, else -1."""
+    off = np.zeros(1, dtype=np.int64)
+    for l in group:
+        st = int(t.stride(ls.index(l))) if l in ls else 0
+        off = (off[:, None] + np.arange(card[l], dtype=np.int64)[None, :] * st).reshape(-1)
+    if len(off) == 1:
+        return off, 0
+    d = np.diff(off)
+    return off, (int(d[0]) if d[0] >= 0 and np.all(d == d[0]) else -1)
 
 
 def gemm_shape(la, lb, keep, card, force=False):
@@ -186,58 +198,43 @@ def gemm_shape(la, lb, keep, card, force=False):
     return batch, Ms, Ns, Ks
 
 
-def prepare_gemm(A, la, B, lb, shape, copy_fn=None):
-    """Descriptor for the dense step `shape` = (batch, M, N, K) of A[la] x B[lb] (gemm_shape).
-    Operands whose groups do not collapse into one stride each are packed with copy_fn
-    (default: an immediate contract copy).  Returns (desc, A, B, C, out_labels)."""
-    copy_fn = copy_fn or (lambda T, lt, lo: contract(T, lt, None, None, lo, combine="copy"))
-    la, lb = list(la), list(lb)
+def prepare_gemm(A, la, B, lb, keep, shape):
+    """(desc, offset table, C) for the dense step `shape` = (batch, M, N, K) of A[la] x B[lb]
+    (gemm_shape), C allocated C-order over `keep`.  The offset table (pgm_gemm_desc) addresses
+    every operand layout directly."""
+    la, lb, keep = list(la), list(lb), list(keep)
     card = {l: int(A.shape[i]) for i, l in enumerate(la)}
     for i, l in enumerate(lb):
         if card.setdefault(l, int(B.shape[i])) != int(B.shape[i]):
             raise ValueError(f"cardinality mismatch for {l!r}")
     batch, Ms, Ns, Ks = shape
-
-    def prod(g):
-        p = 1
-        for l in g:
-            p *= card[l]
-        return p
-
-    nb, m, n, k = prod(batch), prod(Ms), prod(Ns), prod(Ks)
-    strides_a = [_group_stride(A, la, g, card) for g in (batch, Ms, Ks)]
-    if None in strides_a:
-        A = copy_fn(A, la, batch + Ms + Ks)
-        la = batch + Ms + Ks
-        strides_a = [_group_stride(A, la, g, card) for g in (batch, Ms, Ks)]
-    strides_b = [_group_stride(B, lb, g, card) for g in (batch, Ks, Ns)]
-    if None in strides_b:
-        B = copy_fn(B, lb, batch + Ks + Ns)
-        lb = batch + Ks + Ns
-        strides_b = [_group_stride(B, lb, g, card) for g in (batch, Ks, Ns)]
-    out_labels = batch + Ms + Ns
-    C = empty([card[l] for l in out_labels])
+    C = empty([card[l] for l in keep])
+    parts = [_group_offsets(A, la, batch, card), _group_offsets(B, lb, batch, card), _group_offsets(C, keep, batch, card),
+             _group_offsets(A, la, Ms, card), _group_offsets(C, keep, Ms, card),
+             _group_offsets(A, la, Ks, card), _group_offsets(B, lb, Ks, card),
+             _group_offsets(B, lb, Ns, card), _group_offsets(C, keep, Ns, card)]
+    table = to_device_i64(np.concatenate([o for o, _ in parts]))
     d = N.GemmDesc()
-    d.batch, d.m, d.n, d.k = nb, m, n, k
-    d.sa_b, d.sa_m, d.sa_k = strides_a
-    d.sb_b, d.sb_k, d.sb_n = strides_b
-    d.sc_b, d.sc_m, d.sc_n = m * n, n, 1
-    return d, A, B, C, out_labels
+    d.batch, d.m, d.n, d.k = len(parts[0][0]), len(parts[3][0]), len(parts[7][0]), len(parts[5][0])
+    d.offsets = table.data_ptr()
+    for i, (_, st) in enumerate(parts):
+        d.stride[i] = st
+    return d, table, C
 
 
 def pair_gemm(A, la, B, lb, keep, force=False, shape=None):
-    """sum over (la | lb) - keep of A[la] * B[lb], on FP64 MFMA (pgm_gemm) when the step is a
-    dense GEMM (gemm_shape).  Returns (C, batch + M + N labels), C-order, or None for the
-    generic fused contraction.  force=True skips only the minimum-work threshold (tests)."""
+    """sum over (la | lb) - keep of A[la] * B[lb] into a new C-order tensor over `keep`, on FP64
+    MFMA (pgm_gemm) when the step is a dense GEMM (gemm_shape); None otherwise (the caller uses
+    the generic fused contraction).  force=True skips only the minimum-work threshold (tests)."""
     if shape is None:
         card = {l: int(A.shape[i]) for i, l in enumerate(la)}
         card.update({l: int(B.shape[i]) for i, l in enumerate(lb)})
         shape = gemm_shape(list(la), list(lb), keep, card, force)
         if shape is None:
             return None
-    d, A, B, C, out_labels = prepare_gemm(A, la, B, lb, shape)
+    d, table, C = prepare_gemm(A, la, B, lb, keep, shape)
     N.check(N.lib().pgm_gemm(ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C), N.stream_handle()), "gemm")
-    return C, out_labels
+    return C
 
 
 def prepare_product_n(operands, out_labels, out=None, kinds=None):

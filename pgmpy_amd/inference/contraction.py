@@ -166,8 +166,7 @@ def compiled_path(operand_labels, out_labels, dims):
             continue
         _, i, j, keep, nid = st
         shape = E.gemm_shape(labels[i], labels[j], keep, dims)
-        # a GEMM step's result is laid out batch + M + N; later steps see those labels
-        labels[nid] = (shape[0] + shape[1] + shape[2]) if shape is not None else keep
+        labels[nid] = keep
         plan.append((st, shape))
     hit = (plan, final_id)
     _PATHS[key] = hit
@@ -209,8 +208,8 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
             ti, li = live.pop(i)
             tj, lj = live.pop(j)
             if shape is not None and reduce == "sum":
-                live[nid] = (prog.pair_gemm(ti, li, tj, lj, shape) if prog is not None
-                             else E.pair_gemm(ti, li, tj, lj, keep, shape=shape))
+                live[nid] = ((prog.pair_gemm(ti, li, tj, lj, keep, shape) if prog is not None
+                              else E.pair_gemm(ti, li, tj, lj, keep, shape=shape)), keep)
             else:
                 live[nid] = (run.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
     t, ls = live[final_id]

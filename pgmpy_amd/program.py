@@ -60,15 +60,14 @@ class Program:
         self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
         return out
 
-    def pair_gemm(self, A, la, B, lb, shape):
-        """Recorded dense step (engine.prepare_gemm); packing copies are recorded too."""
-        d, A, B, C, out_labels = E.prepare_gemm(
-            A, la, B, lb, shape, copy_fn=lambda T, lt, lo: self.contract(T, lt, None, None, lo, combine="copy"))
+    def pair_gemm(self, A, la, B, lb, keep, shape):
+        """Recorded dense step (engine.prepare_gemm): C over `keep`, offset table kept alive."""
+        d, table, C = E.prepare_gemm(A, la, B, lb, keep, shape)
         L = N.lib()
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C))
-        self._keep.extend([d, A, B, C])
+        self._keep.extend([d, table, A, B, C])
         self._steps.append(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"))
-        return C, out_labels
+        return C
 
     def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):
         L = N.lib()
