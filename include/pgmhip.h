@@ -204,6 +204,22 @@ int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *ou
 int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem,
                int64_t *out_idx, int32_t *out_idx32, void *stream);
 
+/* ---------------------------------------------------------------- batched small jobs
+ * Many INDEPENDENT small contractions / evidence gathers run as one launch (one level of a
+ * compiled greedy contraction path, ExactInference.py:404-406: every step whose inputs are ready;
+ * or all of a plan's per-factor evidence slices, ExactInference.py:352-365).  Jobs are planned on
+ * add (same descriptors and checks as pgm_contract / pgm_gather; contractions run in flat mode
+ * without split-K), uploaded once by finalize, and replayed by run (graph-capturable).  The
+ * caller guarantees that no job reads another job's output. */
+int pgm_batch_create(void **handle);
+int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const double *A, const double *B, double *C);
+int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
+                         int32_t *err_flag);
+int pgm_batch_finalize(void *handle);
+int pgm_batch_run(void *handle, void *stream);
+int pgm_batch_destroy(void *handle);
+
+
 /* ---------------------------------------------------------------- fused row plan
  * The batched-evidence hot path (DiscreteBayesianNetwork.predict /
  * predict_probability, DiscreteBayesianNetwork.py:731-989; the per-row

@@ -149,6 +149,12 @@ _SIGS = {
     "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_product_n": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, _P], ctypes.c_int),
     "pgm_gemm": ([ctypes.POINTER(GemmDesc), _P, _P, _P, _P], ctypes.c_int),
+    "pgm_batch_create": ([ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_batch_add_contract": ([_P, ctypes.POINTER(ContractDesc), _P, _P, _P], ctypes.c_int),
+    "pgm_batch_add_gather": ([_P, ctypes.POINTER(GatherDesc), _P, _P, _P, _P], ctypes.c_int),
+    "pgm_batch_finalize": ([_P], ctypes.c_int),
+    "pgm_batch_run": ([_P, _P], ctypes.c_int),
+    "pgm_batch_destroy": ([_P], ctypes.c_int),
     "pgm_codes_select": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, ctypes.c_int64, _P, _P],
                          ctypes.c_int),
     "pgm_graph_capture_begin": ([_P], ctypes.c_int),

@@ -25,7 +25,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 7
+#define PGM_ABI_VERSION 8
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -130,16 +130,16 @@ __device__ __forceinline__ void decode_ro(const ContractK &p, uint32_t ro, int64
 }
 
 // Flat mode: G lanes cooperate on one output (any keep layout); lanes stride the innermost
-// reduction dim, the reduction-outer index is walked wave-uniformly.
+// reduction dim, the reduction-outer index is walked wave-uniformly.  `tid` / `nthreads` are the
+// thread's index and the thread count of the launch (or of its job in a batched launch).
 template <int CMB, int RED>
-__global__ __launch_bounds__(256) void k_contract(const ContractK p, const double *__restrict__ A,
-                                                  const double *__restrict__ B, double *__restrict__ C,
-                                                  double *__restrict__ ws) {
+__device__ __forceinline__ void contract_flat(const ContractK &p, const double *__restrict__ A,
+                                              const double *__restrict__ B, double *__restrict__ C,
+                                              double *__restrict__ ws, uint64_t tid, uint64_t nthreads,
+                                              uint32_t split) {
   const uint32_t G = 1u << p.g_log2;
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane_g = (uint32_t)tid & (G - 1);
-  const uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) >> p.g_log2;
-  const uint32_t split = blockIdx.y;
+  const uint64_t ngroups = nthreads >> p.g_log2;
   const uint32_t r0 = split * p.red_chunk;
   const uint32_t r1 = min(p.n_ro, r0 + p.red_chunk);
   for (uint64_t out = tid >> p.g_log2; out < p.n_out; out += ngroups) {
@@ -178,6 +178,14 @@ __global__ __launch_bounds__(256) void k_contract(const ContractK p, const doubl
         ws[(uint64_t)split * p.n_out + out] = acc;
     }
   }
+}
+
+template <int CMB, int RED>
+__global__ __launch_bounds__(256) void k_contract(const ContractK p, const double *__restrict__ A,
+                                                  const double *__restrict__ B, double *__restrict__ C,
+                                                  double *__restrict__ ws) {
+  contract_flat<CMB, RED>(p, A, B, C, ws, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                          (uint64_t)gridDim.x * blockDim.x, blockIdx.y);
 }
 
 // Row mode: the innermost keep dim runs across the lanes (coalesced when it is innermost in the
@@ -565,11 +573,10 @@ struct GatherK {
   int32_t ev_card[PGM_MAX_DIMS];
 };
 
-__global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *__restrict__ A,
-                                                const uint8_t *__restrict__ codes, double *__restrict__ C,
-                                                int32_t *__restrict__ err) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t out = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; out < p.n_out; out += stride) {
+__device__ __forceinline__ void gather_body(const GatherK &p, const double *__restrict__ A,
+                                            const uint8_t *__restrict__ codes, double *__restrict__ C,
+                                            int32_t *__restrict__ err, uint64_t tid, uint64_t nthreads) {
+  for (uint64_t out = tid; out < p.n_out; out += nthreads) {
     int64_t oa = 0, oc = 0, row = 0;
     uint32_t idx = (uint32_t)out;
     for (int k = p.nk - 1; k >= 0; --k) {
@@ -589,6 +596,56 @@ __global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *_
       oa += (int64_t)c * p.ev_stride[j];
     }
     C[oc] = A[oa];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *__restrict__ A,
+                                                const uint8_t *__restrict__ codes, double *__restrict__ C,
+                                                int32_t *__restrict__ err) {
+  gather_body(p, A, codes, C, err, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
+}
+
+// ----------------------------------------------------------------------------- batched small jobs
+// Many independent small contractions / evidence gathers in ONE launch: workgroup -> job through a
+// block map, each job runs the flat-mode contraction (or the gather) over its own blocks.  One
+// level of a compiled contraction path (all steps whose inputs are ready) is one launch instead
+// of one launch per step.
+struct BatchJob {
+  int32_t kind, cmb, red, _pad;  // kind 0: contraction, 1: gather
+  uint32_t block0, nblocks;
+  const double *A, *B;
+  double *C;
+  const uint8_t *codes;
+  int32_t *err;
+  ContractK c;
+  GatherK g;
+};
+
+template <int CMB>
+__device__ __forceinline__ void batch_contract_c(const BatchJob &J, uint64_t tid, uint64_t n) {
+  switch (J.red) {
+    case PGM_RED_NONE: contract_flat<CMB, PGM_RED_NONE>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+    case PGM_RED_SUM: contract_flat<CMB, PGM_RED_SUM>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+    default: contract_flat<CMB, PGM_RED_MAX>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs,
+                                               const uint32_t *__restrict__ block_job) {
+  const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[blockIdx.x]);
+  const BatchJob &J = jobs[j];
+  const uint64_t tid = (uint64_t)(blockIdx.x - J.block0) * blockDim.x + threadIdx.x;
+  const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
+  if (J.kind == 1) {
+    gather_body(J.g, J.A, J.codes, J.C, J.err, tid, n);
+    return;
+  }
+  switch (J.cmb) {
+    case PGM_COMBINE_MUL: batch_contract_c<PGM_COMBINE_MUL>(J, tid, n); break;
+    case PGM_COMBINE_ADD: batch_contract_c<PGM_COMBINE_ADD>(J, tid, n); break;
+    case PGM_COMBINE_DIV: batch_contract_c<PGM_COMBINE_DIV>(J, tid, n); break;
+    case PGM_COMBINE_DIV_RAW: batch_contract_c<PGM_COMBINE_DIV_RAW>(J, tid, n); break;
+    default: batch_contract_c<PGM_COMBINE_COPY>(J, tid, n); break;
   }
 }
 
@@ -1500,14 +1557,12 @@ int pgm_graph_destroy(void *graph_exec) {
   return PGM_OK;
 }
 
-int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C, int32_t *err_flag,
-               void *stream) {
-  if (!d || !A || !C) return fail(PGM_EINVAL, "gather: null argument");
+}  // extern "C"
+
+static int plan_gather(const pgm_gather_desc *d, GatherK &k) {
   if (d->n_keep < 0 || d->n_keep > KMAX || d->n_ev < 0 || d->n_ev > PGM_MAX_DIMS)
     return fail(PGM_EINVAL, "gather: n_keep %d (limit %d) / n_ev %d", d->n_keep, KMAX, d->n_ev);
-  if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "gather: null codes");
   if (d->batch_dim >= d->n_keep) return fail(PGM_EINVAL, "gather: batch_dim out of range");
-  GatherK k;
   memset(&k, 0, sizeof k);
   k.nk = d->n_keep;
   k.n_ev = d->n_ev;
@@ -1529,10 +1584,135 @@ int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, 
     k.ev_card[j] = (int32_t)d->ev_card[j];
   }
   k.n_out = (uint32_t)n_out;
-  if (n_out == 0) return PGM_OK;
-  uint64_t blocks = std::min<uint64_t>((n_out + 255) / 256, 65535);
+  return PGM_OK;
+}
+
+struct BatchHandle {
+  std::vector<BatchJob> jobs;
+  std::vector<uint32_t> block_job;
+  BatchJob *d_jobs = nullptr;
+  uint32_t *d_map = nullptr;
+};
+
+static const uint32_t kBatchMaxBlocksPerJob = 256;
+
+extern "C" {
+
+int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C, int32_t *err_flag,
+               void *stream) {
+  if (!d || !A || !C) return fail(PGM_EINVAL, "gather: null argument");
+  if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "gather: null codes");
+  GatherK k;
+  int rc = plan_gather(d, k);
+  if (rc != PGM_OK) return rc;
+  if (k.n_out == 0) return PGM_OK;
+  uint64_t blocks = std::min<uint64_t>((k.n_out + 255) / 256, 65535);
   hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(256), 0, S(stream), k, A, codes, C, err_flag);
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_batch_create(void **handle) {
+  if (!handle) return fail(PGM_EINVAL, "batch_create: null handle");
+  *handle = new (std::nothrow) BatchHandle;
+  return *handle ? PGM_OK : fail(PGM_ENOMEM, "batch_create: host allocation");
+}
+
+static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads) {
+  if (h->d_jobs) return fail(PGM_EINVAL, "batch: already finalized");
+  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), kBatchMaxBlocksPerJob);
+  if (h->block_job.size() + nb > 0x7fffffffull) return fail(PGM_EINVAL, "batch: too many blocks");
+  J.block0 = (uint32_t)h->block_job.size();
+  J.nblocks = (uint32_t)nb;
+  h->block_job.insert(h->block_job.end(), nb, (uint32_t)h->jobs.size());
+  h->jobs.push_back(J);
+  return PGM_OK;
+}
+
+int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const double *A, const double *B, double *C) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !A || !C) return fail(PGM_EINVAL, "batch_add_contract: null argument");
+  if (d && d->combine != PGM_COMBINE_COPY && !B) return fail(PGM_EINVAL, "batch_add_contract: null B");
+  ContractLaunch L;
+  int rc = plan_contract(d, L);
+  if (rc != PGM_OK) return rc;
+  if (L.empty) return PGM_OK;
+  BatchJob J;
+  memset(&J, 0, sizeof J);
+  J.kind = 0;
+  J.cmb = d->combine;
+  J.red = d->reduce;
+  J.A = A;
+  J.B = B;
+  J.C = C;
+  J.c = L.k;
+  // flat mode, no split: lanes per output grow while the job is small and the reduction long
+  ContractK &k = J.c;
+  k.row_mode = 0;
+  k.n_split = 1;
+  k.red_chunk = k.n_ro;
+  int g = 0;
+  if (d->reduce != PGM_RED_NONE && (uint64_t)k.n_ro * k.ri_card > 1)
+    while (g < 6 && ((uint64_t)k.n_out << g) < 4096 && (1u << (g + 1)) <= k.ri_card) ++g;
+  k.g_log2 = g;
+  return batch_append(h, J, (uint64_t)k.n_out << g);
+}
+
+int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
+                         int32_t *err_flag) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !d || !A || !C) return fail(PGM_EINVAL, "batch_add_gather: null argument");
+  if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "batch_add_gather: null codes");
+  BatchJob J;
+  memset(&J, 0, sizeof J);
+  int rc = plan_gather(d, J.g);
+  if (rc != PGM_OK) return rc;
+  if (J.g.n_out == 0) return PGM_OK;
+  J.kind = 1;
+  J.A = A;
+  J.C = C;
+  J.codes = codes;
+  J.err = err_flag;
+  return batch_append(h, J, J.g.n_out);
+}
+
+int pgm_batch_finalize(void *handle) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "batch_finalize: null handle");
+  if (h->d_jobs || h->jobs.empty()) return PGM_OK;
+  hipError_t e = hipMalloc((void **)&h->d_jobs, sizeof(BatchJob) * h->jobs.size());
+  if (e == hipSuccess) e = hipMalloc((void **)&h->d_map, sizeof(uint32_t) * h->block_job.size());
+  if (e == hipSuccess)
+    e = hipMemcpy(h->d_jobs, h->jobs.data(), sizeof(BatchJob) * h->jobs.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(h->d_map, h->block_job.data(), sizeof(uint32_t) * h->block_job.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    if (h->d_jobs) (void)hipFree(h->d_jobs);
+    if (h->d_map) (void)hipFree(h->d_map);
+    h->d_jobs = nullptr;
+    h->d_map = nullptr;
+    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "batch_finalize: %s", hipGetErrorString(e));
+  }
+  return PGM_OK;
+}
+
+int pgm_batch_run(void *handle, void *stream) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "batch_run: null handle");
+  if (h->jobs.empty()) return PGM_OK;
+  if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
+  hipLaunchKernelGGL(k_batch, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_batch_destroy(void *handle) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return PGM_OK;
+  if (h->d_jobs) (void)hipFree(h->d_jobs);
+  if (h->d_map) (void)hipFree(h->d_map);
+  delete h;
   return PGM_OK;
 }
 

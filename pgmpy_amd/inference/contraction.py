@@ -168,7 +168,17 @@ def compiled_path(operand_labels, out_labels, dims):
         shape = E.gemm_shape(labels[i], labels[j], keep, dims)
         labels[nid] = keep
         plan.append((st, shape))
-    hit = (plan, final_id)
+    # levels: step k runs at 1 + the deepest level among its inputs (inputs are level 0)
+    depth = {i: 0 for i in range(len(operand_labels))}
+    levels = []
+    for k, (st, _) in enumerate(plan):
+        ins = (st[1],) if st[0] == "reduce" else (st[1], st[2])
+        d = 1 + max(depth[i] for i in ins)
+        depth[st[-1]] = d
+        while len(levels) < d:
+            levels.append([])
+        levels[d - 1].append(k)
+    hit = (plan, final_id, levels)
     _PATHS[key] = hit
     if len(_PATHS) > PATH_CACHE_SIZE:
         _PATHS.popitem(last=False)
@@ -196,9 +206,10 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
     for l in out_labels:
         if l not in dims:
             raise ValueError(f"output label {l!r} not in any operand")
-    plan, final_id = compiled_path([ls for _, ls in operands], out_labels, dims)
+    plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims)
     live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
-    for st, shape in plan:
+
+    def step(st, shape):
         if st[0] == "reduce":
             _, i, keep, nid = st
             t, ls = live.pop(i)
@@ -212,6 +223,17 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
                               else E.pair_gemm(ti, li, tj, lj, keep, shape=shape)), keep)
             else:
                 live[nid] = (run.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
+
+    if prog is None:
+        for st, shape in plan:
+            step(st, shape)
+    else:
+        # recorded: one launch per level of the path (steps whose inputs are all ready)
+        for lvl in levels:
+            prog.begin_batch()
+            for k in lvl:
+                step(*plan[k])
+            prog.end_batch()
     t, ls = live[final_id]
     if ls != list(out_labels):
         t = run.contract(t, ls, None, None, list(out_labels), reduce=reduce, combine="copy")

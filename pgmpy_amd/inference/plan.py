@@ -340,6 +340,7 @@ class PatternPlan:
         codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
         perr = torch.zeros(1, dtype=torch.int32, device=dev)
         ops = []
+        prog.begin_batch()  # every factor's evidence slice: one launch
         for t, vars_ in self._dev_factors():
             rem = [v for v in vars_ if v not in ev_set]
             dyn = {v: (None, local[v]) for v in vars_ if v in ev_set}
@@ -348,6 +349,7 @@ class PatternPlan:
                 ops.append((g, rem + [E.ROW]))
             else:
                 ops.append((t, list(vars_)))
+        prog.end_batch()
         outl = self.variables + [E.ROW]
         if not any(E.ROW in ls for _, ls in ops):
             # no evidence touches this pattern: broadcast one result over the rows

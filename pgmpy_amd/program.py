@@ -12,19 +12,68 @@ from . import _native as N
 from . import engine as E
 
 
+BATCH_MAX_WORK = 1 << 22  # index-space size (outputs x reduction) up to which a step joins a batch
+BATCH_SPLIT_WORK = 1 << 16  # a step the planner would split (few outputs, long reduction) joins only this small
+
+
+class _Batch:
+    """Independent small jobs collected between Program.begin_batch() and end_batch()."""
+
+    def __init__(self):
+        self.jobs = []  # (kind, batch args, plain-launch args)
+
+
 class Program:
     def __init__(self):
         self._steps = []
         self._keep = []
         self._graph = None
         self._stream = None
+        self._batch = None
+        self._handles = []
+
+    # ------------------------------------------------------------------ batching
+    def begin_batch(self):
+        """Small contractions / gathers recorded until end_batch() become ONE launch
+        (pgm_batch_*); the caller guarantees they are independent of each other."""
+        if self._batch is not None:
+            raise RuntimeError("batch already open")
+        self._batch = _Batch()
+
+    def end_batch(self):
+        b, self._batch = self._batch, None
+        if b is None or not b.jobs:
+            return
+        L = N.lib()
+        if len(b.jobs) == 1:  # a batch of one is just the job (with its own planner's launch)
+            kind, _, args = b.jobs[0]
+            if kind == "contract":
+                self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
+            else:
+                self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
+            return
+        h = ctypes.c_void_p()
+        N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
+        self._handles.append(h)
+        for kind, args, _ in b.jobs:
+            if kind == "contract":
+                N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
+            else:
+                N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
+        N.check(L.pgm_batch_finalize(h), "batch_finalize")
+        self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
 
     # ------------------------------------------------------------------ recording
     def contract(self, A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
         d, out, ws, wsb = E.prepare_contract(A, la, B, lb, out_labels, reduce, combine, out)
-        args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
         self._keep.extend([d, A, B, out, ws])
         L = N.lib()
+        w = _work(d) if self._batch is not None else 0
+        if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
+            self._batch.jobs.append(("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)),
+                                     (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)))
+            return out
+        args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
         self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
         return out
 
@@ -57,6 +106,9 @@ class Program:
         L = N.lib()
         args = (ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err))
         self._keep.extend([d, A, codes, out, err])
+        if self._batch is not None and out.numel() <= BATCH_MAX_WORK:
+            self._batch.jobs.append(("gather", args, args))
+            return out
         self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
         return out
 
@@ -108,8 +160,21 @@ class Program:
 
     def __del__(self):
         g = getattr(self, "_graph", None)
-        if g is not None and g.value:
-            try:
-                N.load_library().pgm_graph_destroy(g)
-            except Exception:
-                pass
+        try:
+            L = N.load_library()
+            if g is not None and g.value:
+                L.pgm_graph_destroy(g)
+            for h in getattr(self, "_handles", []):
+                L.pgm_batch_destroy(h)
+        except Exception:
+            pass
+
+
+def _work(d):
+    """Index-space size of a contraction descriptor (outputs x reduction)."""
+    w = 1
+    for i in range(d.n_keep):
+        w *= int(d.keep_card[i])
+    for i in range(d.n_red):
+        w *= int(d.red_card[i])
+    return w

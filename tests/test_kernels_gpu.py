@@ -329,3 +329,52 @@ def test_contract_factors_gemm_steps_match_numpy(gpu):
         args += [x, [sym[l] for l in ls]]
     ref = np.einsum(*args, [sym["a"], sym["d"]])
     np.testing.assert_allclose(got, ref, rtol=1e-12)
+
+
+def test_program_batch_matches_eager(gpu):
+    """Independent small contractions and gathers recorded in one batch (pgm_batch_*: one launch)
+    give the same results as individual launches, replayed directly and from a HIP graph."""
+    import ctypes
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd import engine as E
+    from pgmpy_amd.program import Program
+
+    rng = np.random.default_rng(3)
+    jobs = [
+        (rng.random((3, 4, 5)), ["a", "b", "c"], rng.random((5, 6)), ["c", "d"], ["a", "d"], "sum", "mul"),
+        (rng.random((7, 2)), ["x", "y"], None, None, ["y"], "max", "copy"),
+        (rng.random((4, 9)), ["p", "q"], rng.random((9,)) + 0.5, ["q"], ["p", "q"], None, "div"),
+        (rng.random((2, 3, 4)), ["u", "v", "w"], None, None, ["w", "u", "v"], None, "copy"),
+        (rng.random((300, 40)), ["m", "k"], rng.random((40, 50)), ["k", "n"], ["m", "n"], "sum", "mul"),
+        (rng.random((6,)), ["s"], rng.random((5,)), ["t"], ["t", "s"], None, "add"),
+    ]
+    dev = [(E.to_device(A), la, None if B is None else E.to_device(B), lb, out, red, cmb)
+           for A, la, B, lb, out, red, cmb in jobs]
+    expect = [E.to_host(E.contract(A, la, B, lb, out, reduce=red, combine=cmb)) for A, la, B, lb, out, red, cmb in dev]
+    G = E.to_device(rng.random((4, 5, 6)))
+    gexp = E.to_host(E.gather(G, ["a", "b", "c"], {"b": 3}, ["c", "a"]))
+    for graph in (False, True):
+        prog = Program()
+        prog.begin_batch()
+        outs = [prog.contract(A, la, B, lb, out, reduce=red, combine=cmb) for A, la, B, lb, out, red, cmb in dev]
+        gd, Aptr, gout = E.prepare_gather(G, ["a", "b", "c"], {"b": 3}, ["c", "a"])
+        prog._keep.extend([gd, G, gout])
+        ga = (ctypes.byref(gd), Aptr, None, N.ptr(gout), None)
+        prog._batch.jobs.append(("gather", ga, ga))
+        prog.end_batch()
+        assert len(prog) == 1  # all seven jobs are small: one launch
+        if graph:
+            prog.capture()
+        prog.run()
+        for got, exp in zip(outs, expect):
+            np.testing.assert_allclose(E.to_host(got), exp, rtol=1e-13, atol=0)
+        np.testing.assert_array_equal(E.to_host(gout), gexp)
+    # a batch of one is recorded as the plain launch
+    prog = Program()
+    prog.begin_batch()
+    A, la, B, lb, out, red, cmb = dev[0]
+    o = prog.contract(A, la, B, lb, out, reduce=red, combine=cmb)
+    prog.end_batch()
+    prog.run()
+    np.testing.assert_allclose(E.to_host(o), expect[0], rtol=1e-13)
