@@ -52,6 +52,35 @@ class BatchedCalibration:
         return dict(self._marg)
 
 
+def _aggregate(prog, small, clique_labels, scope_size):
+    """Multiply the findings / messages entering a clique bottom-up over their scopes.
+
+    Operands with the same scope are multiplied at that scope; each scope's product is folded
+    into the smallest containing scope among the operands' scopes (still separator-sized), so the
+    clique-sized product reads only the maximal scopes' aggregates (pathfinder's root: 57 child
+    messages, 46 of them over one variable -> 3 operands).  Returns [(tensor, labels)]."""
+    R = E.ROW
+    groups = {}
+    for t, labels in small:
+        sc = tuple(v for v in clique_labels if v in labels)
+        groups.setdefault(sc, []).append((t, list(labels)))
+    order = sorted(groups, key=lambda sc: (scope_size(sc), len(sc)))
+    folded = {sc: [] for sc in order}
+    top = []
+    for i, sc in enumerate(order):
+        items = groups[sc] + folded[sc]
+        if len(items) == 1:
+            agg = items[0]
+        else:
+            agg = (prog.product_n(items, list(sc) + [R]), list(sc) + [R])
+        bigger = [t for t in order[i + 1:] if set(sc) < set(t)]
+        if bigger:
+            folded[min(bigger, key=lambda t: (scope_size(t), len(t)))].append(agg)
+        else:
+            top.append(agg)
+    return top
+
+
 class BPSchedule:
     """A compiled batched calibration for fixed (n_rows, evidence columns, operation)."""
 
@@ -76,15 +105,21 @@ class BPSchedule:
             children[p].append(c)
             parent[c] = p
         beliefs, msgs, seps = {}, {}, {}
+        size = {v: bjt.card[v] for v in bjt.card}
+
+        def scope_size(sc):
+            return int(np.prod([size[v] for v in sc])) if sc else 1
+
         # collect: post-order (children before parents)
         post = [c for _, c in reversed(bjt.order)] + [bjt.root]
         for c in post:
             t, ls = bjt.pot[c]
-            ops = [(t, ls)]
+            small = []  # (tensor, labels incl. R): findings and child messages, all over subsets of c
             for j, v in ev_by_clique.get(c, []):
-                ops.append((prog.indicator(self.codes[j], bjt.card[v], n_rows, err=self.err), [v, R]))
+                small.append((prog.indicator(self.codes[j], bjt.card[v], n_rows, err=self.err), [v, R]))
             for k in children[c]:
-                ops.append(msgs[k])
+                small.append(msgs[k])
+            ops = [(t, ls)] + _aggregate(prog, small, ls, scope_size)
             if len(ops) == 1:
                 ops.append((E.to_device(np.ones(n_rows)), [R]))  # broadcast psi over the rows
             beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
@@ -92,16 +127,31 @@ class BPSchedule:
                 sep = [v for v in ls if v in parent[c]]
                 msgs[c] = (prog.contract(beliefs[c][0], ls + [R], None, None, sep + [R], reduce=red,
                                          combine="copy"), sep + [R])
-        # distribute: root -> leaves
+        # distribute: root -> leaves; one sigma per distinct separator scope of a parent, each
+        # marginalised from the smallest already-computed containing scope (or the belief)
+        kids = {}
         for p, c in bjt.order:
+            kids.setdefault(p, []).append(c)
+        for p in [bjt.root] + [c for _, c in bjt.order]:
+            if p not in kids:
+                continue
             tp, lp = beliefs[p]
-            tc, lc = beliefs[c]
-            mu, sl = msgs[c]
-            sigma = prog.contract(tp, lp + [R], None, None, sl, reduce=red, combine="copy")
-            # beta_c *= sigma / mu (0/0 -> 0) in one pass
-            prog.product_n([(tc, lc + [R]), (sigma, sl), (mu, sl)], lc + [R], out=tc,
-                           kinds=[N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN])
-            seps[(p, c)] = (sigma, sl[:-1])
+            scopes = {}
+            for c in kids[p]:
+                scopes.setdefault(tuple(msgs[c][1][:-1]), []).append(c)
+            have = {tuple(lp): tp}
+            for sc in sorted(scopes, key=lambda x: -scope_size(x)):
+                src = min((h for h in have if set(sc) <= set(h)), key=scope_size)
+                sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
+                                      combine="copy")
+                have[sc] = sigma
+                for c in scopes[sc]:
+                    tc, lc = beliefs[c]
+                    mu, sl = msgs[c]
+                    # beta_c *= sigma / mu (0/0 -> 0) in one pass
+                    prog.product_n([(tc, lc + [R]), (sigma, sl), (mu, sl)], lc + [R], out=tc,
+                                   kinds=[N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN])
+                    seps[(p, c)] = (sigma, sl[:-1])
         marg = {}
         if marginals:
             for var in bjt.variables:
