@@ -486,13 +486,37 @@ struct ProdNK {
   const double *ops[PMAX];
 };
 
+// all operand values first (unused slots alias operand 0 with stride 0, so every load is valid and
+// no load sits behind a branch), then the product with the per-operand kinds (uniform branches)
+template <int NOPS>
+__device__ __forceinline__ double prodn_combine(const ProdNK &p, const double (&v)[NOPS]) {
+  double prod = 1.0;
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i) {
+    if (i < p.n_ops) {
+      if (p.kind[i] == PGM_PRODN_MUL) {
+        prod *= v[i];
+      } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
+        const double r = v[i] / v[i + 1];
+        prod *= (r != r) ? 0.0 : r;
+      }
+    }
+  }
+  return prod;
+}
+
 template <int NOPS>
 __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__restrict__ C) {
   if (p.row_mode) {
+    constexpr int U = NOPS <= 4 ? 4 : 2;  // rows in flight per thread
     const int kx = p.nk - 1;
     const uint32_t NX = p.kdiv[kx].d;
     const uint32_t n_outer = p.n_out / NX;
     const uint32_t xstep = gridDim.x * blockDim.x;
+    int64_t sx[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) sx[i] = p.ks[i][kx];
+    const int64_t scx = p.ksc[kx];
     for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
       // outer decode once per block and outer index (wave-uniform), reused for all rows
       int64_t off[NOPS];
@@ -510,22 +534,21 @@ __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__rest
       }
       const double *op[NOPS];
 #pragma unroll
-      for (int i = 0; i < NOPS; ++i) op[i] = i < p.n_ops ? p.ops[i] + off[i] : nullptr;
-      for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < NX; x += xstep) {
-        double prod = 1.0;
+      for (int i = 0; i < NOPS; ++i) op[i] = p.ops[i] + off[i];
+      for (uint32_t x0 = blockIdx.x * blockDim.x + threadIdx.x; x0 < NX; x0 += U * xstep) {
+        double v[U][NOPS];
 #pragma unroll
-        for (int i = 0; i < NOPS; ++i) {
-          if (i < p.n_ops) {
-            const double v = op[i][(int64_t)x * p.ks[i][kx]];
-            if (p.kind[i] == PGM_PRODN_MUL) {
-              prod *= v;
-            } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
-              const double r = v / op[i + 1][(int64_t)x * p.ks[i + 1][kx]];
-              prod *= (r != r) ? 0.0 : r;
-            }
-          }
+        for (int u = 0; u < U; ++u) {
+          const uint32_t x = x0 + u * xstep;
+          const int64_t xc = x < NX ? x : NX - 1;
+#pragma unroll
+          for (int i = 0; i < NOPS; ++i) v[u][i] = op[i][xc * sx[i]];
         }
-        C[oc + (int64_t)x * p.ksc[kx]] = prod;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t x = x0 + u * xstep;
+          if (x < NX) C[oc + (int64_t)x * scx] = prodn_combine<NOPS>(p, v[u]);
+        }
       }
     }
     return;
@@ -545,20 +568,10 @@ __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__rest
       oc += (int64_t)dg * p.ksc[k];
       idx = q;
     }
-    double prod = 1.0;
+    double v[NOPS];
 #pragma unroll
-    for (int i = 0; i < NOPS; ++i) {
-      if (i < p.n_ops) {
-        const double v = p.ops[i][off[i]];
-        if (p.kind[i] == PGM_PRODN_MUL) {
-          prod *= v;
-        } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
-          const double r = v / p.ops[i + 1][off[i + 1]];
-          prod *= (r != r) ? 0.0 : r;
-        }
-      }
-    }
-    C[oc] = prod;
+    for (int i = 0; i < NOPS; ++i) v[i] = p.ops[i][off[i]];
+    C[oc] = prodn_combine<NOPS>(p, v);
   }
 }
 
@@ -1503,6 +1516,11 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
       return fail(PGM_EINVAL, "product_n: a RATIO operand must be followed by its DEN operand");
     if (d->op_kind[t] == PGM_PRODN_DEN && (t == 0 || d->op_kind[t - 1] != PGM_PRODN_RATIO))
       return fail(PGM_EINVAL, "product_n: a DEN operand must follow a RATIO operand");
+  }
+  for (int t = d->n_ops; t < PMAX; ++t) {  // unused slots alias operand 0 with stride 0 (valid loads)
+    k.ops[t] = k.ops[0];
+    k.kind[t] = PGM_PRODN_MUL;
+    for (int i = 0; i < n; ++i) k.ks[t][i] = 0;
   }
   const uint64_t NX = n > 0 ? (uint64_t)card[n - 1] : 1;
   k.row_mode = (n > 0 && NX >= 64) ? 1 : 0;

@@ -31,6 +31,7 @@ class Program:
         self._stream = None
         self._batch = None
         self._handles = []
+        self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
     def begin_batch(self):
@@ -51,6 +52,7 @@ class Program:
                 self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
             else:
                 self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
+            self.notes.append(f"{kind} (batch of one)")
             return
         h = ctypes.c_void_p()
         N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
@@ -62,6 +64,7 @@ class Program:
                 N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
         self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+        self.notes.append(f"batch of {len(b.jobs)}")
 
     # ------------------------------------------------------------------ recording
     def contract(self, A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
@@ -75,6 +78,7 @@ class Program:
             return out
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
         self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
+        self.notes.append(f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}")
         return out
 
     def product_n(self, operands, out_labels, out=None, kinds=None):
@@ -90,6 +94,8 @@ class Program:
         self._keep.extend([d, ptrs, out] + [t for t, _ in ops])
         args = (ctypes.byref(d), ptrs, N.ptr(out))
         self._steps.append(lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n"))
+        self.notes.append(f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
+                          f"-> {list(out_labels)}{tuple(out.shape)}")
         return out
 
     def indicator(self, codes_col, card, n_rows, err=None):
@@ -99,6 +105,7 @@ class Program:
                 N.ptr(err))
         self._keep.extend([codes_col, out, err])
         self._steps.append(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"))
+        self.notes.append(f"indicator card {card}")
         return out
 
     def gather(self, A, la, evidence, out_labels, codes, ld, row0, n_rows, err=None):
@@ -110,6 +117,7 @@ class Program:
             self._batch.jobs.append(("gather", args, args))
             return out
         self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
+        self.notes.append(f"gather {list(la)} -> {list(out_labels)}")
         return out
 
     def pair_gemm(self, A, la, B, lb, keep, shape):
@@ -119,6 +127,7 @@ class Program:
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C))
         self._keep.extend([d, table, A, B, C])
         self._steps.append(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"))
+        self.notes.append(f"gemm b{d.batch} m{d.m} n{d.n} k{d.k}")
         return C
 
     def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):
@@ -126,6 +135,30 @@ class Program:
         args = (N.ptr(X), int(n_rows), int(row_len), int(s_row), int(s_elem), None, N.ptr(out32))
         self._keep.extend([X, out32])
         self._steps.append(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"))
+        self.notes.append("argmax")
+
+    def time_steps(self, reps=3):
+        """[(us, note)] per recorded step, each replayed alone (profiling aid; not graph-replayed)."""
+        import ctypes as C
+
+        L = N.lib()
+        s = N.stream_handle()
+        a, b = C.c_void_p(), C.c_void_p()
+        N.check(L.pgm_event_create(C.byref(a)))
+        N.check(L.pgm_event_create(C.byref(b)))
+        out = []
+        for step, note in zip(self._steps, self.notes):
+            step(s)
+            N.check(L.pgm_event_record(a, s))
+            for _ in range(reps):
+                step(s)
+            N.check(L.pgm_event_record(b, s))
+            ms = C.c_float()
+            N.check(L.pgm_event_elapsed_ms(a, b, C.byref(ms)))
+            out.append((ms.value * 1e3 / reps, note))
+        L.pgm_event_destroy(a)
+        L.pgm_event_destroy(b)
+        return out
 
     # ------------------------------------------------------------------ execution
     def run(self, stream=None):

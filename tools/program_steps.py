@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Time every step of a compiled program alone and list the slowest (profiling aid).
+
+    python tools/program_steps.py c4 [rows]      # batched BP schedule on pathfinder
+    python tools/program_steps.py c2             # munin C2 query plan
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "c4"
+    if what == "c4":
+        from pgmpy_amd.inference.bp_batch import BatchedJunctionTree
+        from pgmpy_amd.inference.EliminationOrder import junction_tree_from_model
+        from pgmpy_amd.utils import get_example_model
+
+        n = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
+        m = get_example_model("pathfinder")
+        bjt = BatchedJunctionTree(junction_tree_from_model(m))
+        leaves = sorted(v for v in m.nodes() if m.out_degree(v) == 0)
+        sch = bjt.schedule(n, leaves, graph=False, marginals=False)
+        prog = sch.prog
+    else:
+        import random
+
+        from pgmpy_amd.inference import VariableElimination
+        from pgmpy_amd.utils import get_example_model
+
+        m = get_example_model("munin")
+        leaves = sorted(v for v in m.nodes() if m.out_degree(v) == 0)
+        roots = sorted(v for v in m.nodes() if m.in_degree(v) == 0)
+        rng = random.Random(100000)
+        E = rng.sample(leaves, 100)
+        q = [rng.choice(roots)]
+        ev = {v: m.states[v][0] for v in E}
+        ve = VariableElimination(m)
+        ve.query(q, ev, show_progress=False)
+        (plan, _), = ve._compiled.values()
+        (prog, *_), = plan._progs.values()
+    res = prog.time_steps()
+    tot = sum(us for us, _ in res)
+    print(f"{len(res)} steps, {tot / 1e3:.2f} ms summed")
+    for us, note in sorted(res, key=lambda r: -r[0])[:25]:
+        print(f"{us:9.1f} us  {note[:220]}")
+
+
+if __name__ == "__main__":
+    main()
