@@ -283,6 +283,61 @@ __global__ __launch_bounds__(256) void k_contract_rows(const ContractK p, const 
   }
 }
 
+// Row mode, short reduction (n_red <= 512, no split): every reduction offset is decoded once per
+// block into LDS, then each row sums flat over them with 8 loads and 8 accumulators in flight
+// (a BP separator marginal: a few clique variables summed for every (separator state, row)).
+#define RTAB_MAX 512
+template <int CMB, int RED>
+__global__ __launch_bounds__(256) void k_contract_rows_tab(const ContractK p, const double *__restrict__ A,
+                                                           const double *__restrict__ B, double *__restrict__ C) {
+  __shared__ int64_t sra[RTAB_MAX], srb[RTAB_MAX];
+  const uint32_t NR = p.n_red;
+  for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+    const uint32_t ro = j / p.ri_card, ri = j - ro * p.ri_card;
+    int64_t ra, rb;
+    decode_ro(p, ro, ra, rb);
+    sra[j] = ra + (int64_t)ri * p.ri_sa;
+    srb[j] = rb + (int64_t)ri * p.ri_sb;
+  }
+  __syncthreads();
+  const int kx = p.nk - 1;
+  const uint32_t NX = p.kdiv[kx].d;
+  const int64_t sxa = p.ksa[kx], sxb = p.ksb[kx], sxc = p.ksc[kx];
+  const uint32_t n_outer = p.n_out / NX;
+  const uint32_t xstep = gridDim.x * blockDim.x;
+  for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+    int64_t oa = 0, ob = 0, oc = 0;
+    uint32_t idx = o;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      if constexpr (CMB != PGM_COMBINE_COPY) ob += (int64_t)dg * p.ksb[k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < NX; x += xstep) {
+      const double *a = A + oa + (int64_t)x * sxa;
+      const double *b = B + ob + (int64_t)x * sxb;
+      double acc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] = red_init<RED>();
+      uint32_t j = 0;
+      for (; j + 8 <= NR; j += 8) {
+        double w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = ld_combine<CMB>(a, b, sra[j + u], srb[j + u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] = red_op<RED>(acc[u], w[u]);
+      }
+      for (; j < NR; ++j) acc[0] = red_op<RED>(acc[0], ld_combine<CMB>(a, b, sra[j], srb[j]));
+#pragma unroll
+      for (int u = 1; u < 8; ++u) acc[0] = red_op<RED>(acc[0], acc[u]);
+      C[oc + (int64_t)x * sxc] = acc[0];
+    }
+  }
+}
+
 template <int RED>
 __global__ __launch_bounds__(256) void k_contract_final(const ContractK p, const double *__restrict__ ws,
                                                         double *__restrict__ C) {
@@ -453,7 +508,9 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
 template <int CMB, int RED>
 static void launch_contract_t(const ContractLaunch &L, const double *A, const double *B, double *C, double *ws,
                               hipStream_t s) {
-  if (L.k.row_mode)
+  if (L.k.row_mode && RED != PGM_RED_NONE && L.k.n_split == 1 && L.k.ri_nb == 1 && L.k.n_red <= RTAB_MAX)
+    hipLaunchKernelGGL((k_contract_rows_tab<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C);
+  else if (L.k.row_mode)
     hipLaunchKernelGGL((k_contract_rows<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
   else
     hipLaunchKernelGGL((k_contract<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
