@@ -143,6 +143,53 @@ def cpu_baseline_c3(model, missing, codes_host, nodes, seconds):
                       f"(prune + greedy einsum contraction + normalize + marginals), {dt:.1f} s"}
 
 
+def _cpu_worker(job):
+    """One host worker of the all-core CPU baseline: rows w, w+W, ... of the sample until the budget."""
+    missing, codes_host, nodes, w, W, seconds = job
+    from oracle import ve as OVE
+    from oracle.network import load_network
+
+    net = load_network("munin")
+    pos = {v: i for i, v in enumerate(nodes)}
+    obs = [v for v in nodes if v not in missing]
+    t0 = time.perf_counter()
+    n = 0
+    for r in range(w, codes_host.shape[1], W):
+        ev = {v: net.states[v][codes_host[pos[v], r]] for v in obs}
+        OVE.query(net, list(missing), ev, joint_out=False)
+        n += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    return n
+
+
+def cpu_baseline_c3_allcore(missing, codes_host, nodes, seconds):
+    """The same oracle on every host core we are given (fork pool, before any GPU use)."""
+    import multiprocessing as mp
+
+    W = max(1, min(16, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(W) as pool:
+        counts = pool.map(_cpu_worker, [(list(missing), codes_host, nodes, w, W, seconds) for w in range(W)])
+    dt = time.perf_counter() - t0
+    return {"value": sum(counts) / dt, "unit": "queries/s", "cores": W, "kind": "port",
+            "sample": f"{sum(counts)} rows of the same synthetic munin sample, numpy oracle per row, "
+                      f"{W} worker processes, {dt:.1f} s wall (upper bound: pgmpy's predict is GIL-bound)"}
+
+
+def cpu_baselines_c3(args):
+    """Both C3 CPU baselines, computed before the GPU is touched (the all-core pool forks)."""
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    model = get_example_model("munin")
+    missing = set(random.Random(0).sample(sorted(model.nodes()), 3))
+    codes_all, nodes = forward_sample_codes(model, args.rows, seed=42)
+    single = cpu_baseline_c3(model, missing, codes_all, nodes, args.cpu_seconds)
+    allcore = cpu_baseline_c3_allcore(missing, codes_all, nodes, min(10.0, args.cpu_seconds))
+    return single, allcore
+
+
 def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64):
     """First rows of the device output against the oracle (1e-6 relative, BASELINE.json)."""
     from oracle import ve as OVE
@@ -256,8 +303,8 @@ def bench_c3(args, dist, rank, world):
     }
     if rank == 0:
         result["parity"] = parity_spot_check(model, missing, plan, out, codes_all, nodes)
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline_c3(model, missing, codes_all, nodes, args.cpu_seconds)
+        if world == 1 and args.cpu_pre is not None:
+            result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
     if dist is not None and args.gather:
         from pgmpy_amd.distributed import gather_rows
@@ -303,11 +350,66 @@ def bench_c2(args):
         r = ve.query(q, evidence, show_progress=False)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    (plan, _), = ve._compiled.values()
+    ps = plan.path_stats(1)
     return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
-            "higher_is_better": False, "steps": args.steps, "first_query_s": t_cold,
+            "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
+            "plan": {"kind": plan.kind, **ps},
+            "achieved": {"GB/s": ps["bytes"] / dt / 1e9, "TFLOP/s": ps["flops"] / dt / 1e12,
+                         "note": "algorithmic bytes / flops of the executed greedy plan (SURVEY §8(d) C2) per query"},
+            "reference": {"value": 52.7, "unit": "s/query", "note": "pgmpy numpy path, survey container (not this host)"},
             "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
                     "same query/evidence variables); first_query_s includes pruning, planning and graph capture",
             "result": list(np.asarray(r.values))}
+
+
+def bench_c1(args):
+    """C1: alarm VariableElimination.query, single evidence rows (50 seeded patterns: 3 query vars,
+    5 evidence vars), device path (compiled per pattern) vs the numpy oracle on the host."""
+    import torch
+
+    from pgmpy_amd.inference import VariableElimination
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("alarm")
+    nodes_sorted = sorted(m.nodes())
+    rng = random.Random(1)
+    codes, nodes = forward_sample_codes(m, 50, seed=1)
+    pos = {v: i for i, v in enumerate(nodes)}
+    pats = []
+    for r in range(50):
+        pick = rng.sample(nodes_sorted, 8)
+        q, e = pick[:3], pick[3:]
+        pats.append((q, {v: m.states[v][codes[pos[v], r]] for v in e}))
+    ve = VariableElimination(m)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for q, e in pats:
+        ve.query(q, e, show_progress=False)
+    torch.cuda.synchronize()
+    cold = (time.perf_counter() - t0) / len(pats)
+    t0 = time.perf_counter()
+    reps = max(1, args.steps // 10)
+    for _ in range(reps):
+        for q, e in pats:
+            r = ve.query(q, e, show_progress=False)
+    torch.cuda.synchronize()
+    warm = (time.perf_counter() - t0) / (reps * len(pats))
+    out = {"metric": "alarm single-row query latency (C1)", "value": warm, "unit": "s/query",
+           "higher_is_better": False, "patterns": len(pats), "first_query_s": cold,
+           "note": "value: compiled pattern plans cached (same query/evidence variables, new values)"}
+    if not args.no_cpu_baseline:
+        from oracle import ve as OVE
+        from oracle.network import load_network
+
+        net = load_network("alarm")
+        t0 = time.perf_counter()
+        for q, e in pats:
+            OVE.query(net, q, e)
+        out["cpu_baseline"] = {"value": (time.perf_counter() - t0) / len(pats), "unit": "s/query", "cores": 1,
+                               "kind": "port", "sample": "the same 50 patterns, numpy oracle"}
+    return out
 
 
 def bench_c4(args):
@@ -354,7 +456,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rows", type=int, default=None)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c1", "c2", "c4"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="after timing, gather marginals to rank 0 (RCCL)")
@@ -365,11 +467,17 @@ def main():
     from pgmpy_amd.build import build
 
     build(verbose=False)
+    args.cpu_pre = None
+    single_process = int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if args.workload == "c3" and single_process and not args.no_cpu_baseline:
+        args.cpu_pre = cpu_baselines_c3(args)  # before dist_setup: no GPU state in the forked workers
     dist, rank, world = dist_setup(args.gpus, args.dist_backend)
     if args.workload == "c3":
         res = bench_c3(args, dist, rank, world)
     elif args.workload == "c2":
         res = bench_c2(args)
+    elif args.workload == "c1":
+        res = bench_c1(args)
     else:
         res = bench_c4(args)
     if rank == 0:

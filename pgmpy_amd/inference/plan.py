@@ -311,6 +311,25 @@ class PatternPlan:
             self._inter = (max(1, st["max_intermediate"]), max(1, st["sum_intermediate"]))
         return self._inter
 
+    def path_stats(self, n_rows=1):
+        """SURVEY.md §8(d) C2 accounting of the steps path for n_rows rows: pairwise steps,
+        algorithmic bytes (sum of 8 (|A| + |B| + |C|)), flops (2 |index space|), max intermediate;
+        plus how many steps run as dense FP64 MFMA GEMMs."""
+        from .contraction import compiled_path
+
+        labels, dims = [], dict(self.card)
+        dims[E.ROW] = n_rows
+        for vars_, _ in self.factors:
+            ls = [v for v in vars_ if v not in self.evidence_vars]
+            if any(v in self.evidence_vars for v in vars_):
+                ls = ls + [E.ROW]
+            labels.append(ls)
+        st = plan_stats(labels, self.variables + [E.ROW], dims)
+        plan, _, levels = compiled_path(labels, self.variables + [E.ROW], dims)
+        st["gemm_steps"] = sum(1 for _, shape in plan if shape is not None)
+        st["levels"] = len(levels)
+        return st
+
     def max_intermediate_per_row(self):
         return self.intermediates_per_row()[0]
 
