@@ -390,7 +390,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
             return False
         if set(self.scope()) != set(other.scope()):
             return False
-        ovals = np.asarray(other.values)
+        ovals = np.asarray(other._values_readonly())
         perm = [other.variables.index(v) for v in self.variables]
         ovals = ovals.transpose(perm) if ovals.ndim else ovals
         ocard = np.array(other.cardinality)[perm] if len(perm) else np.array(other.cardinality)
@@ -402,7 +402,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
                 sl = [slice(None)] * len(self.variables)
                 sl[axis] = ref_index
                 ovals = ovals[tuple(sl)]
-        svals = np.asarray(self.values)
+        svals = np.asarray(self._values_readonly())
         if ovals.shape != svals.shape:
             return False
         if not np.allclose(ovals, svals, atol=atol):
@@ -418,7 +418,8 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         # DiscreteFactor.py:1089-1110 (axes sorted by variable hash)
         variable_hashes = [hash(v) for v in self.variables]
         order = sorted(range(len(variable_hashes)), key=lambda i: variable_hashes[i])
-        vals = np.asarray(self.values).transpose(order) if order else np.asarray(self.values)
+        vals = np.asarray(self._values_readonly())
+        vals = vals.transpose(order) if order else vals
         card = np.array(self.cardinality)[order] if order else np.array(self.cardinality)
         return hash(str(sorted(variable_hashes)) + str(hash(np.ascontiguousarray(vals).tobytes()))
                     + str(hash(np.ascontiguousarray(card).tobytes())) + str(hash(frozenset(self.state_names))))

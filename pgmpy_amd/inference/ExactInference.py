@@ -452,3 +452,127 @@ class BeliefPropagation(Inference):
         from .bp_batch import BatchedJunctionTree
 
         return BatchedJunctionTree(self.junction_tree).calibrate_frame(evidence, operation=operation)
+
+
+class BeliefPropagationWithMessagePassing(Inference):
+    """Belief propagation by recursive message passing on a loop-free FactorGraph (mirror of
+    pgmpy/inference/ExactInference.py:1320-1681; Algorithm 2.1 of Winn, "Model-Based Machine
+    Learning").
+
+    Same recursion, message cache keys ("['B', 'A'] -> B", "A -> ['B', 'A']"), evidence as point
+    masses at an integer state index, virtual evidence as extra variable-node messages, and the
+    reference's normalisation conventions: a variable node with exactly one incoming message
+    passes it on unnormalised; factor messages (sum over the other variables of the factor times
+    their incoming messages, the reference's chained matmul L1659-1681) are normalised.  Every
+    product / reduction is a device contraction; messages are handed back as numpy arrays, as the
+    reference returns them."""
+
+    def __init__(self, model, check_model=True):
+        from ..models.FactorGraph import FactorGraph
+
+        assert isinstance(model, FactorGraph), "Model must be an instance of FactorGraph"
+        if check_model:
+            model.check_model()
+        self.model = model
+
+    class _RecursiveMessageSchedulingQuery:
+        # ExactInference.py:1349-1507
+        def __init__(self, bp, variables, evidence, virtual_evidence, get_messages, precomp_messages):
+            self.bp = bp
+            self.variables = variables
+            self.evidence = evidence
+            self.virtual_evidence = virtual_evidence
+            self.get_messages = get_messages
+            self.all_messages = (precomp_messages.copy() if precomp_messages is not None
+                                 else {} if get_messages or len(variables) > 1 else None)
+
+        def run(self):
+            agg_res = {}
+            for variable in self.variables:
+                res = self.schedule_variable_node_messages(variable, from_factor=None)
+                agg_res[variable] = DiscreteFactor([variable], [len(res)], res)
+            if self.get_messages:
+                return agg_res, self.all_messages
+            return agg_res
+
+        def schedule_variable_node_messages(self, variable, from_factor):
+            if self.evidence is not None and variable in self.evidence.keys():
+                return self.bp.model.get_point_mass_message(variable, self.evidence[variable])
+            virtual_messages = []
+            if (self.virtual_evidence is not None
+                    and variable in self.bp._get_virtual_evidence_var_list(self.virtual_evidence)):
+                virtual_messages = [np.asarray(cpd.values).reshape(-1) for cpd in self.virtual_evidence
+                                    if cpd.variables[0] == variable]
+            incoming_factors = [f for f in list(self.bp.model.neighbors(variable)) if f != from_factor]
+            if len(incoming_factors) == 0:
+                message = self.bp.model.get_uniform_message(variable)
+                return self.bp.calc_variable_node_message(variable, [message] + virtual_messages)
+            incoming_messages = []
+            for factor in incoming_factors:
+                key = f"{factor.variables} -> {variable}"
+                if self.all_messages is not None and key in self.all_messages:
+                    msg = self.all_messages[key]
+                else:
+                    msg = self.schedule_factor_node_messages(factor, variable)
+                    if self.all_messages is not None:
+                        self.all_messages[key] = msg
+                incoming_messages.append(msg)
+            return self.bp.calc_variable_node_message(variable, incoming_messages + virtual_messages)
+
+        def schedule_factor_node_messages(self, factor, from_variable):
+            incoming_vars = [var for var in factor.variables if var != from_variable]
+            if len(incoming_vars) == 0:
+                return self.bp.calc_factor_node_message(factor, [], from_variable)
+            incoming_messages = []
+            for var in incoming_vars:
+                key = f"{var} -> {factor.variables}"
+                if self.all_messages is not None and key in self.all_messages:
+                    msg = self.all_messages[key]
+                else:
+                    msg = self.schedule_variable_node_messages(var, factor)
+                    if self.all_messages is not None:
+                        self.all_messages[key] = msg
+                incoming_messages.append(msg)
+            return self.bp.calc_factor_node_message(factor, incoming_messages, from_variable)
+
+    def query(self, variables, evidence=None, virtual_evidence=None, get_messages=False, precomp_messages=None):
+        # ExactInference.py:1509-1627
+        common_vars = set(evidence if evidence is not None else []).intersection(set(variables))
+        if common_vars:
+            raise ValueError(f"Can't have the same variables in both `variables` and `evidence`. "
+                             f"Found in both: {common_vars}")
+        if evidence is not None and virtual_evidence is not None:
+            self._check_virtual_evidence(virtual_evidence)
+            ve_names = self._get_virtual_evidence_var_list(virtual_evidence)
+            common_vars = set(evidence).intersection(set(ve_names))
+            if common_vars:
+                raise ValueError(f"Can't have the same variables in both `evidence` and `virtual_evidence`. "
+                                 f"Found in both: {common_vars}")
+        return self._RecursiveMessageSchedulingQuery(self, variables, evidence, virtual_evidence, get_messages,
+                                                     precomp_messages).run()
+
+    def calc_variable_node_message(self, variable, incoming_messages):
+        """ExactInference.py:1629-1657: one message passes through; several are multiplied and
+        normalised (on the device)."""
+        if len(incoming_messages) == 1:
+            return incoming_messages[0]
+        ops = [(E.to_device(np.asarray(m, dtype=np.float64).reshape(-1)), ["v"]) for m in incoming_messages]
+        prod = E.product_n(ops, ["v"]) if len(ops) > 1 else ops[0][0]
+        total = E.contract(prod, ["v"], None, None, [], reduce="sum", combine="copy")
+        return E.to_host(E.contract(prod, ["v"], total, [], ["v"], combine="div_raw"))
+
+    @staticmethod
+    def calc_factor_node_message(factor, incoming_messages, target_var):
+        """ExactInference.py:1659-1681: sum over the factor's other variables of the factor times
+        their incoming messages (the reference's chained matmul), normalised; a factor with no other
+        variable sends its values."""
+        if len(incoming_messages) != len(factor.variables) - 1:
+            raise AssertionError(f"Error computing factor node message for {target_var}. ")
+        if len(incoming_messages) == 0:
+            return np.asarray(factor._values_readonly()).copy()
+        others = [v for v in factor.variables if v != target_var]
+        ops = [(factor._d(), list(factor.variables))]
+        ops += [(E.to_device(np.asarray(m, dtype=np.float64).reshape(-1)), [v]) for v, m in zip(others, incoming_messages)]
+        msg = contract_factors(ops, [target_var])
+        total = E.contract(msg, [target_var], None, None, [], reduce="sum", combine="copy")
+        return E.to_host(E.contract(msg, [target_var], total, [], [target_var], combine="div_raw"))

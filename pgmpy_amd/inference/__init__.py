@@ -1,4 +1,4 @@
 from .base import Inference
-from .ExactInference import BeliefPropagation, VariableElimination
+from .ExactInference import BeliefPropagation, BeliefPropagationWithMessagePassing, VariableElimination
 
-__all__ = ["Inference", "VariableElimination", "BeliefPropagation"]
+__all__ = ["Inference", "VariableElimination", "BeliefPropagation", "BeliefPropagationWithMessagePassing"]
