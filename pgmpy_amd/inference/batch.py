@@ -18,8 +18,28 @@ from .plan import PatternPlan
 MISSING = N.PGM_EV_MISSING
 
 
+def _lookup_codes(values, st):
+    """int64 state numbers of an object array against the state list, -1 where not found: one pass of
+    pandas' C object hash table (1.7 ms per 100k cells) instead of isna + Categorical (6+ ms)."""
+    try:
+        from pandas._libs import hashtable as ht
+
+        table = ht.PyObjectHashTable(max(len(st), 1))
+        table.map_locations(np.asarray(st, dtype=object))
+        return np.asarray(table.lookup(values), dtype=np.int64)
+    except Exception:  # private API moved: the public path
+        import pandas as pd
+
+        return np.asarray(pd.Categorical(values, categories=st).codes, dtype=np.int64)
+
+
 def encode_frame(model, data, columns=None):
-    """[n_cols, n_rows] uint8 codes of `data` (state names -> state numbers, NaN -> 255)."""
+    """[n_cols, n_rows] uint8 codes of `data` (state names -> state numbers, NaN -> 255).
+
+    Evidence ingestion: categorical columns remap their category codes
+    (O(n) integer work); other columns take one hash-table lookup per cell against the variable's
+    state names, and only the cells it misses are examined again (NaN -> 255; the reference's
+    fallback from an unknown state name to the str() match, DiscreteFactor.py:589-597)."""
     import pandas as pd
 
     columns = list(data.columns) if columns is None else list(columns)
@@ -31,20 +51,31 @@ def encode_frame(model, data, columns=None):
         if len(st) >= MISSING:
             raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
         v = data[col]
-        isna = v.isna().to_numpy()
-        cat = pd.Categorical(v, categories=st)
-        c = np.asarray(cat.codes, dtype=np.int64)
-        bad = (c < 0) & ~isna
-        if bad.any():
-            # retry through str(): numeric frames against string state names (and vice versa)
-            sm = {str(s): i for i, s in enumerate(st)}
-            vals = v.to_numpy(object)
-            for i in np.nonzero(bad)[0]:
-                k = sm.get(str(vals[i]))
-                if k is None:
-                    raise KeyError(f"state: {vals[i]} is an unknown for variable: {col}. It must be one of {st}")
-                c[i] = k
-        c[isna] = MISSING
+        if isinstance(v.dtype, pd.CategoricalDtype):
+            cats = list(v.cat.categories)
+            lut = _lookup_codes(np.asarray(cats, dtype=object), st) if cats else np.zeros(0, dtype=np.int64)
+            cc = np.asarray(v.cat.codes, dtype=np.int64)
+            c = np.where(cc >= 0, lut[np.maximum(cc, 0)] if len(lut) else -1, -1)
+            vals = None
+        else:
+            vals = v.to_numpy(dtype=object)
+            c = _lookup_codes(vals, st)
+        miss = np.nonzero(c < 0)[0]
+        if len(miss):
+            if vals is None:
+                vals = v.to_numpy(dtype=object)
+            sub = vals[miss]
+            na = pd.isna(sub)
+            c[miss[na]] = MISSING
+            rest = miss[~na]
+            if len(rest):
+                # retry through str(): numeric frames against string state names (and vice versa)
+                sm = {str(x): i for i, x in enumerate(st)}
+                for i in rest:
+                    k = sm.get(str(vals[i]))
+                    if k is None:
+                        raise KeyError(f"state: {vals[i]} is an unknown for variable: {col}. It must be one of {st}")
+                    c[i] = k
         codes[j] = c.astype(np.uint8)
     return codes
 
@@ -159,9 +190,9 @@ def predict_frame(model, data):
 
     missing_variables = set(model.nodes()) - set(data.columns)
     order = list(missing_variables)
-    all_columns = data.columns.tolist() + [col for col in missing_variables]
-    result = data.reindex(columns=all_columns).astype(object)
-    vals = {c: result[c].to_numpy(object).copy() for c in all_columns}
+    vals = {c: np.full(len(data), np.nan, dtype=object) for c in order}
+    base = data.astype(object, copy=False)  # no copy when every column already holds objects
+    filled = {}  # observed columns whose NaN cells receive MAP states, as in the reference
     for plan, rows, host in _run_groups(model, data, order, False, True, True):
         idx = host["map"].astype(np.int64)
         # decode the flat index (C-order over plan.variables, last fastest)
@@ -169,9 +200,20 @@ def predict_frame(model, data):
             var = plan.variables[i]
             c = plan.cards[i]
             st = np.array(plan.states[var], dtype=object)
-            vals[var][rows] = st[idx % c]
+            if var in vals:
+                vals[var][rows] = st[idx % c]
+            else:
+                if var not in filled:
+                    filled[var] = base[var].to_numpy(object).copy()
+                filled[var][rows] = st[idx % c]
             idx = idx // c
-    out = pd.DataFrame(vals, index=data.index, columns=all_columns)
+    if filled:
+        base = base.assign(**filled)  # a new frame: the caller's data is not modified
+    # the observed columns (object, as the reference's merge leaves them), then the MAP columns in the
+    # reference's set order, rows sorted by index (DiscreteBayesianNetwork.py:895-910)
+    out = pd.concat([base, pd.DataFrame(vals, index=data.index, columns=order)], axis=1)
+    if out.index.is_monotonic_increasing:
+        return out
     return out.sort_index()
 
 

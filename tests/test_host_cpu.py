@@ -113,3 +113,30 @@ def test_encode_and_group_patterns():
     assert sorted(len(r) for _, r in groups) == [1, 1, 2]
     with pytest.raises(KeyError):
         encode_frame(m, pd.DataFrame({"asia": ["maybe"]}))
+
+
+def test_encode_frame_categorical_numeric_and_nan():
+    """Evidence ingestion fast paths (f-4): categorical columns, NaN in either form, numeric cells
+    matching string state names through str() (DiscreteFactor.py:589-597), unknown states."""
+    from pgmpy_amd.inference.batch import encode_frame
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("asia")
+    st = list(m.states["asia"])
+    obj = pd.DataFrame({"asia": ["no", "yes", np.nan, "no", None]})
+    cat = obj.astype({"asia": pd.CategoricalDtype(categories=["yes", "no", "unused"])})
+    want = [st.index("no"), st.index("yes"), 255, st.index("no"), 255]
+    assert list(encode_frame(m, obj)[0]) == want
+    assert list(encode_frame(m, cat)[0]) == want
+    with pytest.raises(KeyError):
+        encode_frame(m, pd.DataFrame({"asia": pd.Categorical(["yes", "maybe"])}))
+
+    from pgmpy_amd.factors.discrete import TabularCPD
+    from pgmpy_amd.models import DiscreteBayesianNetwork
+
+    bn = DiscreteBayesianNetwork([("a", "b")])
+    bn.add_cpds(TabularCPD("a", 2, [[0.5], [0.5]], state_names={"a": ["0", "1"]}),
+                TabularCPD("b", 2, [[0.3, 0.6], [0.7, 0.4]], evidence=["a"], evidence_card=[2],
+                           state_names={"b": [0, 1], "a": ["0", "1"]}))
+    codes = encode_frame(bn, pd.DataFrame({"a": [1, 0, 1], "b": ["1", "0", 1]}))
+    assert codes.tolist() == [[1, 0, 1], [1, 0, 1]]
