@@ -426,6 +426,27 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
                 (unsigned long long)n_out, (unsigned long long)n_red);
   coalesce(kd, 3);
   coalesce(rd, 2);
+  // few outputs (flat mode) and one long reduction run: cut the run into (outer x chunk) so the
+  // split-K below has reduction-outer indices to distribute (a batched dot product over a packed
+  // operand pair would otherwise leave 64 lanes per output walking the whole run)
+  if (d->reduce != PGM_RED_NONE && rd.n > 0 && rd.n < KMAX && kd.n <= KMAX && n_out <= 4096 &&
+      !(kd.n > 0 && kd.card[kd.n - 1] >= 64)) {
+    const int64_t ri = rd.card[rd.n - 1];
+    if (ri >= 8192 && n_red / (uint64_t)ri < 256) {
+      for (int64_t c = 4096; c >= 256; c >>= 1) {
+        if (ri % c) continue;
+        const int last = rd.n - 1;
+        rd.card[rd.n] = c;
+        rd.s[0][rd.n] = rd.s[0][last];
+        rd.s[1][rd.n] = rd.s[1][last];
+        rd.card[last] = ri / c;
+        rd.s[0][last] *= c;
+        rd.s[1][last] *= c;
+        ++rd.n;
+        break;
+      }
+    }
+  }
   if (kd.n > KMAX || rd.n > KMAX)
     return fail(PGM_EINVAL, "contract: %d keep / %d reduce dims after coalescing (limit %d)", kd.n, rd.n, KMAX);
   ContractK &k = L.k;
@@ -794,14 +815,15 @@ struct GemmK {
   int64_t s_ab, s_bb, s_cb, s_am, s_cm, s_ak, s_bk, s_bn, s_cn;  // >= 0: strided group, -1: table
   uint32_t tiles_n;
 };
-// offset of index i of a group: the table (TAB) or a single stride (every group collapses)
+// offset of index i of a group: the table (TAB) or a single stride (the group collapses)
 template <bool TAB>
 __device__ __forceinline__ int64_t goff(int64_t s, const int64_t *tab, int64_t i) {
   if constexpr (TAB) return tab[i];
   else return i * s;
 }
 
-template <bool TAB>
+// TA / TB / TC: operand A, B, C addressed through its offset tables (some group does not collapse)
+template <bool TA, bool TB, bool TC>
 __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *__restrict__ A,
                                                   const double *__restrict__ B, double *__restrict__ C) {
   constexpr int BM = 64, BN = 64, BK = 16;
@@ -813,8 +835,8 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   const uint32_t t = blockIdx.x;  // n fastest within an m row of tiles (A rows stay hot in L2)
   const int64_t n0 = (int64_t)(t % p.tiles_n) * BN, m0 = (int64_t)(t / p.tiles_n) * BM;
   const int64_t b = blockIdx.y;
-  const double *Ab = A + goff<TAB>(p.s_ab, p.a_b, b);
-  const double *Bb = B + goff<TAB>(p.s_bb, p.b_b, b);
+  const double *Ab = A + goff<TA>(p.s_ab, p.a_b, b);
+  const double *Bb = B + goff<TB>(p.s_bb, p.b_b, b);
   // this thread's fixed tile rows (A: 4 m rows, k = tid & 15) and columns (B: 4 k rows, n = tid & 63)
   int64_t arow[4];
   bool aok[4];
@@ -822,24 +844,24 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   for (int i = 0; i < 4; ++i) {
     const int64_t gm = m0 + ((tid + 256 * i) >> 4);
     aok[i] = gm < p.M;
-    arow[i] = aok[i] ? goff<TAB>(p.s_am, p.a_m, gm) : 0;
+    arow[i] = aok[i] ? goff<TA>(p.s_am, p.a_m, gm) : 0;
   }
   const int64_t gn = n0 + (tid & 63);
   const bool bok = gn < p.N;
-  const int64_t bcol = bok ? goff<TAB>(p.s_bn, p.b_n, gn) : 0;
+  const int64_t bcol = bok ? goff<TB>(p.s_bn, p.b_n, gn) : 0;
   double ra[4], rb[4];
   // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
   auto load = [&](int64_t k0) {
     const int64_t gka = k0 + (tid & 15);
     const bool ka = gka < p.K;
-    const int64_t oka = goff<TAB>(p.s_ak, p.a_k, ka ? gka : p.K - 1);
+    const int64_t oka = goff<TA>(p.s_ak, p.a_k, ka ? gka : p.K - 1);
     double va[4], vb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) va[i] = Ab[arow[i] + oka];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t gkb = k0 + ((tid + 256 * i) >> 6);
-      vb[i] = Bb[goff<TAB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1) + bcol];
+      vb[i] = Bb[goff<TB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1) + bcol];
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -872,18 +894,18 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
     }
     __syncthreads();
   }
-  double *Cb = C + goff<TAB>(p.s_cb, p.c_b, b);
+  double *Cb = C + goff<TC>(p.s_cb, p.c_b, b);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t cn = n0 + 32 * wx + 16 * j + (lane & 15);
     if (cn >= p.N) continue;
-    const int64_t ocn = goff<TAB>(p.s_cn, p.c_n, cn);
+    const int64_t ocn = goff<TC>(p.s_cn, p.c_n, cn);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t cm = m0 + 32 * wy + 16 * i + (lane >> 4) + 4 * r;
-        if (cm < p.M) Cb[goff<TAB>(p.s_cm, p.c_m, cm) + ocn] = acc[i][j][r];
+        if (cm < p.M) Cb[goff<TC>(p.s_cm, p.c_m, cm) + ocn] = acc[i][j][r];
       }
   }
 }
@@ -1849,13 +1871,22 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   const uint64_t tn = ((uint64_t)d->n + 63) / 64, tm = ((uint64_t)d->m + 63) / 64;
   if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
-  bool tab = false;
-  for (int i = 0; i < 9; ++i) tab |= d->stride[i] < 0;
   if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
-  if (tab)
-    hipLaunchKernelGGL(k_gemm_f64<true>, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
-  else
-    hipLaunchKernelGGL(k_gemm_f64<false>, dim3((unsigned)(tn * tm), (unsigned)d->batch), dim3(256), 0, S(stream), k, A, B, C);
+  const bool ta = d->stride[0] < 0 || d->stride[3] < 0 || d->stride[5] < 0;
+  const bool tb = d->stride[1] < 0 || d->stride[6] < 0 || d->stride[7] < 0;
+  const bool tc = d->stride[2] < 0 || d->stride[4] < 0 || d->stride[8] < 0;
+  const dim3 g((unsigned)(tn * tm), (unsigned)d->batch), b(256);
+  hipStream_t s = S(stream);
+  switch ((ta ? 4 : 0) | (tb ? 2 : 0) | (tc ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((k_gemm_f64<false, false, false>), g, b, 0, s, k, A, B, C); break;
+    case 1: hipLaunchKernelGGL((k_gemm_f64<false, false, true>), g, b, 0, s, k, A, B, C); break;
+    case 2: hipLaunchKernelGGL((k_gemm_f64<false, true, false>), g, b, 0, s, k, A, B, C); break;
+    case 3: hipLaunchKernelGGL((k_gemm_f64<false, true, true>), g, b, 0, s, k, A, B, C); break;
+    case 4: hipLaunchKernelGGL((k_gemm_f64<true, false, false>), g, b, 0, s, k, A, B, C); break;
+    case 5: hipLaunchKernelGGL((k_gemm_f64<true, false, true>), g, b, 0, s, k, A, B, C); break;
+    case 6: hipLaunchKernelGGL((k_gemm_f64<true, true, false>), g, b, 0, s, k, A, B, C); break;
+    default: hipLaunchKernelGGL((k_gemm_f64<true, true, true>), g, b, 0, s, k, A, B, C); break;
+  }
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

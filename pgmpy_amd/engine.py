@@ -152,7 +152,7 @@ def contract(A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
 
 
 GEMM_MIN_M = GEMM_MIN_N = 16
-GEMM_MIN_K = 8
+GEMM_MIN_K = 1  # outer-product-like steps (few shared states) still write C as coalesced tiles
 GEMM_MIN_FLOPS = 1 << 22
 
 
@@ -196,6 +196,20 @@ def gemm_shape(la, lb, keep, card, force=False):
     if k < GEMM_MIN_K or m < GEMM_MIN_M or n < GEMM_MIN_N or small or nb > 65535:
         return None
     return batch, Ms, Ns, Ks
+
+
+def gemm_orient(la, lb, shape):
+    """Plan-time choice for a dense step of C-order operands A[la], B[lb]: which operand is the
+    kernel's A (its K group is read along the lanes' k) and the output label order (batch + M + N,
+    so C's innermost variable lies along the lanes).  Returns (swap, out_labels, shape') with shape'
+    expressed for the kernel's (A, B)."""
+    batch, Ms, Ns, Ks = shape
+    score = (la[-1] in Ks) + (lb[-1] in Ns)
+    score_sw = (lb[-1] in Ks) + (la[-1] in Ms)
+    if score_sw > score:
+        kset = set(Ks)
+        return True, batch + Ns + Ms, (batch, Ns, Ms, [l for l in lb if l in kset])
+    return False, batch + Ms + Ns, shape
 
 
 def prepare_gemm(A, la, B, lb, keep, shape):

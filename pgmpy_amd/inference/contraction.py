@@ -144,6 +144,8 @@ def plan_stats(operand_labels, out_labels, dims):
 
 
 _PATHS = OrderedDict()  # compiled paths, keyed on the operands' (label, cardinality) structure
+PACK_MAX_OUT = 4096       # pack the operands of non-GEMM steps with at most this many outputs ...
+PACK_MIN_WORK = 1 << 20   # ... and at least this large an index space
 PATH_CACHE_SIZE = 256
 
 
@@ -166,6 +168,15 @@ def compiled_path(operand_labels, out_labels, dims):
             continue
         _, i, j, keep, nid = st
         shape = E.gemm_shape(labels[i], labels[j], keep, dims)
+        if shape is not None:
+            # operand roles and the output layout chosen for coalescing; later steps see that layout
+            swap, keep, shape = E.gemm_orient(labels[i], labels[j], shape)
+            st = ("pair", j, i, keep, nid) if swap else ("pair", i, j, keep, nid)
+        elif _size(keep, dims) <= PACK_MAX_OUT and _size(list(dict.fromkeys(labels[i] + labels[j])), dims) >= PACK_MIN_WORK:
+            # a long reduction to few outputs (a batched dot product): both operands are first copied to
+            # [kept..., summed...] with the summed variables in one shared order, so the reduction is one
+            # contiguous run (lanes + split-K) instead of a strided walk with a digit decode per step
+            shape = "pack"
         labels[nid] = keep
         plan.append((st, shape))
     # levels: step k runs at 1 + the deepest level among its inputs (inputs are level 0)
@@ -209,6 +220,8 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
     plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims)
     live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
 
+    after = []  # contractions that read operands packed in the same level (recorded after its batch)
+
     def step(st, shape):
         if st[0] == "reduce":
             _, i, keep, nid = st
@@ -218,7 +231,17 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
             _, i, j, keep, nid = st
             ti, li = live.pop(i)
             tj, lj = live.pop(j)
-            if shape is not None and reduce == "sum":
+            if shape == "pack":
+                red = [l for l in dict.fromkeys(li + lj) if l not in keep]
+                pa = [l for l in keep if l in li] + [l for l in red if l in li]
+                pb = [l for l in keep if l in lj] + [l for l in red if l in lj]
+                ti, li = run.contract(ti, li, None, None, pa, combine="copy"), pa
+                tj, lj = run.contract(tj, lj, None, None, pb, combine="copy"), pb
+                if prog is None:
+                    live[nid] = (E.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
+                else:
+                    after.append((nid, ti, li, tj, lj, keep))
+            elif shape is not None and reduce == "sum":
                 live[nid] = ((prog.pair_gemm(ti, li, tj, lj, keep, shape) if prog is not None
                               else E.pair_gemm(ti, li, tj, lj, keep, shape=shape)), keep)
             else:
@@ -228,12 +251,16 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
         for st, shape in plan:
             step(st, shape)
     else:
-        # recorded: one launch per level of the path (steps whose inputs are all ready)
+        # recorded: one launch per level of the path (steps whose inputs are all ready); a packed
+        # step's contraction follows its level's batch (it reads the copies made inside it)
         for lvl in levels:
             prog.begin_batch()
             for k in lvl:
                 step(*plan[k])
             prog.end_batch()
+            for nid, ti, li, tj, lj, keep in after:
+                live[nid] = (prog.contract(ti, li, tj, lj, keep, reduce=reduce, combine="mul"), keep)
+            after.clear()
     t, ls = live[final_id]
     if ls != list(out_labels):
         t = run.contract(t, ls, None, None, list(out_labels), reduce=reduce, combine="copy")

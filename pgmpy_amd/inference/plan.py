@@ -326,7 +326,8 @@ class PatternPlan:
             labels.append(ls)
         st = plan_stats(labels, self.variables + [E.ROW], dims)
         plan, _, levels = compiled_path(labels, self.variables + [E.ROW], dims)
-        st["gemm_steps"] = sum(1 for _, shape in plan if shape is not None)
+        st["gemm_steps"] = sum(1 for _, shape in plan if shape is not None and shape != "pack")
+        st["packed_steps"] = sum(1 for _, shape in plan if shape == "pack")
         st["levels"] = len(levels)
         return st
 

@@ -378,3 +378,17 @@ def test_program_batch_matches_eager(gpu):
     prog.end_batch()
     prog.run()
     np.testing.assert_allclose(E.to_host(o), expect[0], rtol=1e-13)
+
+
+@pytest.mark.parametrize("red", [614400, 3 * 4099])
+def test_long_contiguous_reduction_few_outputs(gpu, red):
+    """A batched dot product (5 outputs, one long contiguous reduction — a packed greedy step):
+    the planner cuts the run into chunks for split-K; sums match numpy to fp64 rounding."""
+    from pgmpy_amd import engine as E
+
+    rng = np.random.default_rng(9)
+    A = rng.random((5, red))
+    B = rng.random(red)
+    got = E.to_host(E.contract(E.to_device(A), ["m", "k"], E.to_device(B), ["k"], ["m"], reduce="sum",
+                               combine="mul"))
+    np.testing.assert_allclose(got, A @ B, rtol=1e-12)

@@ -45,7 +45,7 @@ def main():
     tot = sum(us for us, _ in res)
     print(f"{len(res)} steps, {tot / 1e3:.2f} ms summed")
     for us, note in sorted(res, key=lambda r: -r[0])[:25]:
-        print(f"{us:9.1f} us  {note[:220]}")
+        print(f"{us:9.1f} us  {note[:220] if len(sys.argv) < 4 else note}")
 
 
 if __name__ == "__main__":
