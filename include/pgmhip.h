@@ -253,7 +253,8 @@ enum pgm_rows_mode {
   PGM_ROWS_MAPGAP = 8,    /* also (best - second best) / best of the joint, for tie screening */
   PGM_ROWS_VALUES_GLOBAL = 16, /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
   PGM_ROWS_ONE_GROUP = 32,     /* tuning: one 64-row group per workgroup (no staging amortisation) */
-  PGM_ROWS_GENERIC = 64        /* tuning: table-driven kernel even for all-affine plans (testing)  */
+  PGM_ROWS_GENERIC = 64,       /* tuning: table-driven kernel even for all-affine plans (testing)  */
+  PGM_ROWS_PLAIN_STORE = 128   /* tuning: ordinary (cached) stores of the marginals instead of nontemporal */
 };
 
 typedef struct {

@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -338,6 +339,67 @@ __global__ __launch_bounds__(256) void k_contract_rows_tab(const ContractK p, co
   }
 }
 
+// k_contract_rows_tab for a plain marginal (COPY), two rows per lane with 16-B loads/stores.
+// Host-checked: even row count, row stride 1 in A and C, every other A/C stride even, bases 16-B aligned.
+template <int RED>
+__global__ __launch_bounds__(256) void k_contract_rows_tab2(const ContractK p, const double *__restrict__ A,
+                                                            double *__restrict__ C) {
+  __shared__ int64_t sra[RTAB_MAX];
+  const uint32_t NR = p.n_red;
+  for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+    const uint32_t ro = j / p.ri_card, ri = j - ro * p.ri_card;
+    int64_t ra, rb;
+    decode_ro(p, ro, ra, rb);
+    sra[j] = (ra + (int64_t)ri * p.ri_sa) >> 1;  // in double2 units
+  }
+  __syncthreads();
+  const int kx = p.nk - 1;
+  const uint32_t NP = p.kdiv[kx].d >> 1;
+  const uint32_t n_outer = p.n_out / p.kdiv[kx].d;
+  const uint32_t xstep = gridDim.x * blockDim.x;
+  for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+    int64_t oa = 0, oc = 0;
+    uint32_t idx = o;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    const double2 *a2 = (const double2 *)(A + oa);
+    double2 *c2 = (double2 *)(C + oc);
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < NP; x += xstep) {
+      const double2 *a = a2 + x;
+      double2 acc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] = make_double2(red_init<RED>(), red_init<RED>());
+      uint32_t j = 0;
+      for (; j + 8 <= NR; j += 8) {
+        double2 w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = a[sra[j + u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc[u].x = red_op<RED>(acc[u].x, w[u].x);
+          acc[u].y = red_op<RED>(acc[u].y, w[u].y);
+        }
+      }
+      for (; j < NR; ++j) {
+        const double2 w = a[sra[j]];
+        acc[0].x = red_op<RED>(acc[0].x, w.x);
+        acc[0].y = red_op<RED>(acc[0].y, w.y);
+      }
+#pragma unroll
+      for (int u = 1; u < 8; ++u) {
+        acc[0].x = red_op<RED>(acc[0].x, acc[u].x);
+        acc[0].y = red_op<RED>(acc[0].y, acc[u].y);
+      }
+      c2[x] = acc[0];
+    }
+  }
+}
+
 template <int RED>
 __global__ __launch_bounds__(256) void k_contract_final(const ContractK p, const double *__restrict__ ws,
                                                         double *__restrict__ C) {
@@ -384,6 +446,8 @@ static void coalesce(Dims &d, int nops) {
   }
   d = o;
 }
+
+static const bool g_no_rows2 = getenv("PGM_NO_ROWS2") != nullptr;  // tuning/testing: 8-B row paths only
 
 static const uint64_t kTargetThreads = 256ull * 2048;  // 256 CUs x 32 waves x 64 lanes
 
@@ -526,11 +590,31 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
   return PGM_OK;
 }
 
+// two-rows-per-lane eligibility of a row-mode COPY contraction (A read, C written)
+static bool rows2_ok(const ContractK &k, const double *A, const double *C) {
+  if (g_no_rows2 || !k.row_mode || k.nk < 1) return false;
+  const int kx = k.nk - 1;
+  if (k.kdiv[kx].d % 2 || k.ksa[kx] != 1 || k.ksc[kx] != 1) return false;
+  if (((uintptr_t)A & 15) || ((uintptr_t)C & 15)) return false;
+  for (int i = 0; i < kx; ++i)
+    if (k.ksa[i] % 2 || k.ksc[i] % 2) return false;
+  for (int i = 0; i < k.nr; ++i)
+    if (k.rsa[i] % 2) return false;
+  return k.nr == 0 || k.ri_sa % 2 == 0;
+}
+
 template <int CMB, int RED>
 static void launch_contract_t(const ContractLaunch &L, const double *A, const double *B, double *C, double *ws,
                               hipStream_t s) {
-  if (L.k.row_mode && RED != PGM_RED_NONE && L.k.n_split == 1 && L.k.ri_nb == 1 && L.k.n_red <= RTAB_MAX)
-    hipLaunchKernelGGL((k_contract_rows_tab<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C);
+  if (L.k.row_mode && RED != PGM_RED_NONE && L.k.n_split == 1 && L.k.ri_nb == 1 && L.k.n_red <= RTAB_MAX) {
+    if (CMB == PGM_COMBINE_COPY && rows2_ok(L.k, A, C)) {
+      dim3 g = L.grid;
+      g.x = (unsigned)std::max<uint64_t>(1, (g.x + 1) / 2);
+      hipLaunchKernelGGL((k_contract_rows_tab2<RED>), g, dim3(256), 0, s, L.k, A, C);
+    } else {
+      hipLaunchKernelGGL((k_contract_rows_tab<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C);
+    }
+  }
   else if (L.k.row_mode)
     hipLaunchKernelGGL((k_contract_rows<CMB, RED>), L.grid, dim3(256), 0, s, L.k, A, B, C, ws);
   else
@@ -650,6 +734,68 @@ __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__rest
 #pragma unroll
     for (int i = 0; i < NOPS; ++i) v[i] = p.ops[i][off[i]];
     C[oc] = prodn_combine<NOPS>(p, v);
+  }
+}
+
+// Row mode, two rows per lane (16-B loads/stores; the 8-B form runs at 0.54-0.70x the 16-B rate on
+// gfx950).  Host-checked: even row count, output row stride 1, every operand's row stride 0 (broadcast,
+// one scalar per outer index) or 1, every base 16-B aligned (all outer strides even).
+template <int NOPS>
+__global__ __launch_bounds__(256) void k_productn_rows2(const ProdNK p, double *__restrict__ C) {
+  constexpr int U = NOPS <= 4 ? 2 : 1;  // row pairs in flight per thread
+  const int kx = p.nk - 1;
+  const uint32_t NP = p.kdiv[kx].d >> 1;
+  const uint32_t n_outer = p.n_out / p.kdiv[kx].d;
+  const uint32_t xstep = gridDim.x * blockDim.x;
+  bool vec[NOPS];
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i) vec[i] = p.ks[i][kx] != 0;
+  for (uint32_t o = blockIdx.y; o < n_outer; o += gridDim.y) {
+    int64_t off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    int64_t oc = 0;
+    uint32_t idx = o;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    const double *op[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) op[i] = p.ops[i] + off[i];
+    double2 *c2 = (double2 *)(C + oc);
+    for (uint32_t x0 = blockIdx.x * blockDim.x + threadIdx.x; x0 < NP; x0 += U * xstep) {
+      double2 v[U][NOPS];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t x = x0 + u * xstep;
+        const uint32_t xc = x < NP ? x : NP - 1;
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          if (vec[i]) {
+            v[u][i] = ((const double2 *)op[i])[xc];
+          } else {
+            const double b = op[i][0];
+            v[u][i] = make_double2(b, b);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t x = x0 + u * xstep;
+        double lo[NOPS], hi[NOPS];
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          lo[i] = v[u][i].x;
+          hi[i] = v[u][i].y;
+        }
+        if (x < NP) c2[x] = make_double2(prodn_combine<NOPS>(p, lo), prodn_combine<NOPS>(p, hi));
+      }
+    }
   }
 }
 
@@ -1207,17 +1353,23 @@ template <bool VL, int NF, int NT, bool MAP>
 __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
     const RowsK p, const double *__restrict__ gvals, const int32_t *__restrict__ desc,
     const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode, int32_t RG,
-    double *__restrict__ marg, int64_t ld_out, int32_t *__restrict__ map, double *__restrict__ gap,
+    int32_t W, double *__restrict__ marg, int64_t ld_out, int32_t *__restrict__ map, double *__restrict__ gap,
     int32_t *__restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int32_t dbg = W >> 8;  // DEBUG strip mask (tools only)
+  W &= 255;
   const int lane = threadIdx.x & 63;
-  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NC = p.n_comp;
+  // wave w = (row wave rw, component c): W row groups side by side, one wave per component each
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rw = w / NC;
+  const int c = w - rw * NC;
   const RowsComp &cd = ((const RowsComp *)desc)[c];
   double *svals = lds;
-  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0);  // [NC][64]
-  double *xgap = xmass + NC * 64;                              // [NC][64]
-  int32_t *xmap = (int32_t *)(xgap + NC * 64);                 // [NC][64]
+  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0) + rw * NC * 64;  // [W][NC][64]
+  double *xgap = lds + (VL ? ((p.n_values + 1) & ~1) : 0) + W * NC * 64 + rw * NC * 64;
+  int32_t *xmap = (int32_t *)(lds + (VL ? ((p.n_values + 1) & ~1) : 0) + 2 * W * NC * 64) + rw * NC * 64;
+  const bool plain_store = (mode & PGM_ROWS_PLAIN_STORE) != 0;
   const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
   // descriptor -> registers (wave-uniform)
   int32_t fb[NF], fs[NF], S[NT][NF];
@@ -1240,25 +1392,30 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
   const int32_t ms = cd.mstride;
   double *mrow = marg + (int64_t)cd.marg0 * ld_out;
   auto val = [&](int32_t i) -> double {
-    if constexpr (VL) return svals[i];
-    else return gvals[i];
+    if constexpr (VL) {
+      if (dbg & 2) return gvals[i];
+      return svals[i];
+    } else return gvals[i];
   };
-  if constexpr (VL) {
+  // every wave stages its own component's values: the W waves of one component write identical
+  // values to the same LDS words, so no wave waits on another (no barrier)
+  if (VL && !(dbg & 2)) {
     if (lane == 0) svals[p.one_idx] = 1.0;
     for (int i = cd.val_lo + lane; i < cd.val_hi; i += 64) svals[i] = gvals[i];
   }
+  auto row_of = [&](int g) -> int64_t { return (((int64_t)blockIdx.x * RG + g) * W + rw) * 64 + lane; };
   auto load_codes = [&](int g, uint32_t (&code)[NT]) {
-    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const int64_t r = row_of(g);
     const uint8_t *crow = codes + (r < n_rows ? r : 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) code[j] = crow[cofs[j]];
+    for (int j = 0; j < NT; ++j) code[j] = (dbg & 8) ? (uint32_t)(lane & 1) : crow[cofs[j]];
   };
   uint32_t nx[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) nx[j] = 0;
   if (nt > 0) load_codes(0, nx);
   for (int g = 0; g < RG; ++g) {
-    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
+    const int64_t r = row_of(g);
     const bool live = r < n_rows;
     uint32_t code[NT];
 #pragma unroll
@@ -1283,9 +1440,14 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
 #pragma unroll
     for (int qs = 0; qs < RC; ++qs) {
       const int32_t q = qs < plast ? qs : plast;
-      double prod = val(cb[0] + q * fs[0]);
+      double prod;
+      if (dbg & 4) {
+        prod = (double)(cb[0] + q);
+      } else {
+        prod = val(cb[0] + q * fs[0]);
 #pragma unroll
-      for (int k = 1; k < NF; ++k) prod *= val(cb[k] + q * fs[k]);
+        for (int k = 1; k < NF; ++k) prod *= val(cb[k] + q * fs[k]);
+      }
       pc[qs] = prod;
     }
     double mass = 0.0, best = -1.0, second = -1.0;
@@ -1316,16 +1478,20 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
       double *out = mrow + r;
 #pragma unroll
       for (int qs = 0; qs < RC; ++qs)
-        if ((uint32_t)qs < P) __builtin_nontemporal_store(pc[qs] * inv, out + (int64_t)qs * ld_out);
+        if ((uint32_t)qs < P) {
+          if (plain_store) out[(int64_t)qs * ld_out] = pc[qs] * inv;
+          else __builtin_nontemporal_store(pc[qs] * inv, out + (int64_t)qs * ld_out);
+        }
       for (uint32_t qs = RC; qs < P; ++qs) {
         double prod = val(cb[0] + (int32_t)qs * fs[0]);
 #pragma unroll
         for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
-        __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
+        if (plain_store) out[(int64_t)qs * ld_out] = prod * inv;
+        else __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
       }
     }
     double z = mass;
-    if (NC > 1) {
+    if (NC > 1 && !(dbg & 1)) {
       xmass[c * 64 + lane] = mass;
       if constexpr (MAP) {
         xmap[c * 64 + lane] = best_s * ms;
@@ -1356,27 +1522,27 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
         if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : mg;
       }
     }
-    if (NC > 1 && g + 1 < RG) __syncthreads();  // the exchange slots are reused by the next row group
+    if (NC > 1 && g + 1 < RG && !(dbg & 1)) __syncthreads();  // the exchange slots are reused by the next row group
   }
 }
 
 template <bool VL, int NF, int NT>
 static void launch_affine_m(bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
                             const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0,
-                            int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo, int32_t *map, double *gap,
-                            int32_t *err) {
+                            int64_t n, int32_t mode, int32_t RG, int32_t W, double *marg, int64_t ldo, int32_t *map,
+                            double *gap, int32_t *err) {
   if (do_map)
-    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, true>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, true>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err);
   else
-    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, false>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, false>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err);
 }
 
 template <bool VL>
 static void launch_affine(int max_nf, int max_nt, bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s,
                           const RowsK &k, const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc,
-                          int64_t row0, int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo, int32_t *map,
-                          double *gap, int32_t *err) {
-#define PGM_AFF(NF, NT) launch_affine_m<VL, NF, NT>(do_map, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err)
+                          int64_t row0, int64_t n, int32_t mode, int32_t RG, int32_t W, double *marg, int64_t ldo,
+                          int32_t *map, double *gap, int32_t *err) {
+#define PGM_AFF(NF, NT) launch_affine_m<VL, NF, NT>(do_map, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err)
   if (max_nt <= 4) {
     if (max_nf <= 1) PGM_AFF(1, 4);
     else if (max_nf <= 2) PGM_AFF(2, 4);
@@ -1603,7 +1769,30 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
   }
   const uint64_t NX = n > 0 ? (uint64_t)card[n - 1] : 1;
   k.row_mode = (n > 0 && NX >= 64) ? 1 : 0;
+  // two rows per lane when every access is 16-B aligned (batched BP: rows innermost, even count)
+  bool rows2 = k.row_mode && (NX % 2 == 0) && sc[n - 1] == 1 && ((uintptr_t)C & 15) == 0 && !g_no_rows2;
+  for (int i = 0; rows2 && i < n - 1; ++i) rows2 = (sc[i] % 2) == 0;
+  for (int t = 0; rows2 && t < d->n_ops; ++t) {
+    const int64_t sx = so[t][n - 1];
+    rows2 = sx == 0 || (sx == 1 && ((uintptr_t)ops[t] & 15) == 0);
+    for (int i = 0; rows2 && sx == 1 && i < n - 1; ++i) rows2 = (so[t][i] % 2) == 0;
+  }
   dim3 grid;
+  if (rows2) {
+    const uint64_t NP = NX / 2, n_outer = n_out / NX;
+    const uint64_t bs = std::min<uint64_t>(256, (NP + 63) / 64 * 64);
+    const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
+    const uint64_t gx = std::min<uint64_t>((NP + bs - 1) / bs, std::max<uint64_t>(1, 2048 / gy));
+    hipStream_t s = S(stream);
+    const dim3 g2((unsigned)gx, (unsigned)gy, 1), b2((unsigned)bs);
+    switch (d->n_ops <= 2 ? 2 : d->n_ops <= 4 ? 4 : 8) {
+      case 2: hipLaunchKernelGGL((k_productn_rows2<2>), g2, b2, 0, s, k, C); break;
+      case 4: hipLaunchKernelGGL((k_productn_rows2<4>), g2, b2, 0, s, k, C); break;
+      default: hipLaunchKernelGGL((k_productn_rows2<8>), g2, b2, 0, s, k, C); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return PGM_OK;
+  }
   if (k.row_mode) {
     const uint64_t xchunks = (NX + 255) / 256, n_outer = n_out / NX;
     const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
@@ -2148,19 +2337,37 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   // amortise the LDS staging of the CPT values over several row groups once the grid is large
   int32_t RG = 1;
   if (vals_lds && !(mode & PGM_ROWS_ONE_GROUP)) RG = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, groups / 4096));
-  const uint64_t blocks = (groups + RG - 1) / RG;
-  if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
-  const dim3 g((unsigned)blocks), b(64 * k.n_waves);
   hipStream_t s = S(stream);
   const double *v = h->d_values;
   const int32_t *t = h->d_desc;
   if (h->all_affine && !(mode & PGM_ROWS_JOINT) && !(mode & PGM_ROWS_GENERIC)) {
+    // W row groups side by side per workgroup (W x n_comp waves)
+    static const int envW = getenv("PGM_ROWS_W") ? atoi(getenv("PGM_ROWS_W")) : 0;
+    static const int envRG = getenv("PGM_ROWS_RG") ? atoi(getenv("PGM_ROWS_RG")) : 0;
+    static const int envDbg = getenv("PGM_ROWS_DBG") ? atoi(getenv("PGM_ROWS_DBG")) : 0;
+    int32_t W = envW > 0 ? envW : 1;
+    W = std::max(1, std::min<int32_t>(W, PGM_ROWS_MAX_COMP / k.n_comp));
+    RG = 1;
+    if (vals_lds && !(mode & PGM_ROWS_ONE_GROUP))
+      RG = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, groups / (4096ull * W)));
+    if (envRG > 0) RG = envRG;
+    const uint64_t ablocks = (groups + (uint64_t)RG * W - 1) / ((uint64_t)RG * W);
+    if (ablocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
+    const size_t alds = vals_bytes + x_bytes * W;
+    const dim3 ag((unsigned)ablocks), ab(64 * k.n_comp * W);
     const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
+    const int32_t Wd = W | (envDbg << 8);
     if (vals_lds)
-      launch_affine<true>(h->max_nf, h->max_nt, do_map, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
+      launch_affine<true>(h->max_nf, h->max_nt, do_map, ag, ab, alds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, Wd, marg, ld_out, map, gap, err_flag);
     else
-      launch_affine<false>(h->max_nf, h->max_nt, do_map, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
-  } else if (vals_lds && acc_lds)
+      launch_affine<false>(h->max_nf, h->max_nt, do_map, ag, ab, alds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, Wd, marg, ld_out, map, gap, err_flag);
+    HIP_TRY(hipGetLastError());
+    return PGM_OK;
+  }
+  const uint64_t blocks = (groups + RG - 1) / RG;
+  if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
+  const dim3 g((unsigned)blocks), b(64 * k.n_waves);
+  if (vals_lds && acc_lds)
     launch_rows_f<true, true>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   else if (vals_lds)
     launch_rows_f<true, false>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);

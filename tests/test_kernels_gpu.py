@@ -392,3 +392,47 @@ def test_long_contiguous_reduction_few_outputs(gpu, red):
     got = E.to_host(E.contract(E.to_device(A), ["m", "k"], E.to_device(B), ["k"], ["m"], reduce="sum",
                                combine="mul"))
     np.testing.assert_allclose(got, A @ B, rtol=1e-12)
+
+
+@pytest.mark.parametrize("rows", [64, 66, 1000, 1001])
+def test_rows2_product_and_marginal_paths(gpu, rows):
+    """Batched-BP shapes (rows innermost): even row counts take the 16-B two-rows-per-lane kernels
+    (k_productn_rows2, k_contract_rows_tab2), odd counts and misaligned views the 8-B ones."""
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    rng = np.random.default_rng(rows)
+    psi = rng.random((4, 2, 3, 5))                      # no row axis (broadcast over rows)
+    m1 = rng.random((4, 5, rows))
+    m2 = rng.random((2, 3, rows))
+    m2[0, 0, :7] = 0.0
+    den = rng.random((2, 3, rows))
+    den[0, 0, :7] = 0.0                                 # 0/0 -> 0
+    den[1, 2, :3] = 0.0                                 # x/0 -> inf
+    ops = [(E.to_device(psi), ["a", "b", "c", "d"]), (E.to_device(m1), ["a", "d", "r"]),
+           (E.to_device(m2), ["b", "c", "r"]), (E.to_device(den), ["b", "c", "r"])]
+    got = E.to_host(E.product_n(ops, ["a", "b", "c", "d", "r"],
+                                kinds=[NN.PRODN_MUL, NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN]))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = m2 / den
+    q[np.isnan(q)] = 0
+    ref = np.einsum("abcd,adr,bcr->abcdr", psi, m1, q)
+    np.testing.assert_allclose(got, ref, rtol=1e-14)
+    # separator marginals of the product (short reductions) and a misaligned (offset) view
+    B = E.to_device(ref)
+    for keep, red in ((["b", "d", "r"], "sum"), (["a", "r"], "max"), (["c", "r"], "sum")):
+        idx = {l: i for i, l in enumerate("abcdr")}
+        full = ref.copy()
+        full[~np.isfinite(full)] = 0.0
+        Bf = E.to_device(full)
+        axes = tuple(i for l, i in idx.items() if l not in keep)
+        exp = full.sum(axis=axes) if red == "sum" else full.max(axis=axes)
+        got = E.to_host(E.contract(Bf, list("abcdr"), None, None, keep, reduce=red, combine="copy"))
+        np.testing.assert_allclose(got, exp, rtol=1e-13)
+    import torch
+
+    flat = torch.zeros(full.size + 1, dtype=torch.float64, device=B.device)
+    view = flat[1:].view(full.shape)                    # 8-B aligned only: the 8-B kernels
+    view.copy_(E.to_device(full))
+    got = E.to_host(E.contract(view, list("abcdr"), None, None, ["b", "d", "r"], reduce="sum", combine="copy"))
+    np.testing.assert_allclose(got, full.sum(axis=(0, 2)), rtol=1e-13)

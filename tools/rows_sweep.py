@@ -56,6 +56,7 @@ def main():
             del mt
         for name, extra, outs in (("lds_values", 0, dict(marginals=True)),
                                   ("lds_one_group", N.ROWS_ONE_GROUP, dict(marginals=True)),
+                                  ("plain_store", N.ROWS_PLAIN_STORE, dict(marginals=True)),
                                   ("generic_kernel", N.ROWS_GENERIC, dict(marginals=True)),
                                   ("global_values", N.ROWS_VALUES_GLOBAL, dict(marginals=True)),
                                   ("map_only", 0, dict(marginals=False, map_=True))):
