@@ -14,7 +14,7 @@ marginals to HBM.
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, rows sharded: weak scaling)
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel
-(k_rows_affine for the C3 template; achieved = algorithmic bytes per launch / HIP-event launch time) and a
+(pgm_rows_jit, the plan-specialised kernel, for the C3 template; achieved = algorithmic bytes per launch / HIP-event launch time) and a
 CPU baseline (the numpy oracle's per-row predict_probability, single core,
 bounded sample) timed on this host.
 Other workloads for DESIGN.md numbers: --workload c2 (single munin query,
@@ -240,8 +240,12 @@ def bench_c3(args, dist, rank, world):
     d_codes = upload_codes(codes_ev)
     out = plan.alloc_outputs(rows, marginals=True)
     err = torch.zeros(1, dtype=torch.int32, device=d_codes.device)
+    # one step = one pass of the fused row plan over the resident batch, launched through the
+    # prepared (bound) C-ABI entry: validated and marshalled once, one argument-free call per step
+    bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
     for _ in range(args.warmup):
-        plan.run(d_codes, rows, 0, rows, out, err=err)
+        bound.run()
+    torch.cuda.synchronize()
     barrier(dist)
     # HIP events on the launch stream bracketing the timed region: average launch duration
     # (includes the ~1 us gap between back-to-back launches that rocprofv3's kernel time omits)
@@ -249,7 +253,7 @@ def bench_c3(args, dist, rank, world):
     timer.start()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        plan.run(d_codes, rows, 0, rows, out, err=err)
+        bound.run()
     kern_ms_total = timer.stop_ms()
     torch.cuda.synchronize()
     t_end = time.perf_counter()
@@ -280,7 +284,7 @@ def bench_c3(args, dist, rank, world):
         "data": "synthetic (forward-sampled munin evidence rows, seed 42+rank)",
         "config": {
             "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, "
-                        "fused row plan (pgm_rows_plan_run)",
+                        "fused row plan (pgm_rows_plan_bind / pgm_rows_bound_run)",
             "network": "munin",
             "missing": variables,
             "rows_per_gpu_per_step": rows,

@@ -254,7 +254,7 @@ enum pgm_rows_mode {
   PGM_ROWS_VALUES_GLOBAL = 16, /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
   PGM_ROWS_ONE_GROUP = 32,     /* tuning: one 64-row group per workgroup (no staging amortisation) */
   PGM_ROWS_GENERIC = 64,       /* tuning: table-driven kernel even for all-affine plans (testing)  */
-  PGM_ROWS_PLAIN_STORE = 128   /* tuning: ordinary (cached) stores of the marginals instead of nontemporal */
+  PGM_ROWS_NO_JIT = 128        /* testing: skip the plan-specialised (hipRTC) kernel, run the AOT ones */
 };
 
 typedef struct {
@@ -285,12 +285,26 @@ typedef struct {
 
 int pgm_rows_plan_create(const pgm_rows_plan *plan, const double *host_values, void **handle);
 int pgm_rows_plan_destroy(void *handle);
+/* Source of the plan-specialised row kernel (hipRTC, compiled for gfx950 on the first run of an
+ * all-affine plan: one query variable and no hidden variable per component).  Writes at most len
+ * bytes (NUL-terminated) and the full size + 1 to *needed.  No device needed (tests, inspection). */
+int pgm_rows_plan_source(const pgm_rows_plan *plan, char *buf, size_t len, size_t *needed);
 /* Rows [row0, row0 + n_rows) of codes.  Outputs are column-major with leading dim ld_out (>= n_rows) and
  * row r written at column r (not row0 + r); any may be NULL unless its mode bit is set:
  *   marg [n_marg][ld_out] f64   joint [n_joint][ld_out] f64   map [n_rows] int32   gap [n_rows] f64 */
 int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
                       int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map,
                       double *gap, int32_t *err_flag, void *stream);
+
+/* Prepared launch: validates the same arguments as pgm_rows_plan_run once and binds them; each
+ * pgm_rows_bound_run then launches that pass (same result as the unbound call).  The buffers and the
+ * plan handle must outlive the bound handle.  Replaces the per-batch Python call of predict()'s
+ * inner loop (pgmpy/models/DiscreteBayesianNetwork.py:867-910) for repeated batches. */
+int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
+                       int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map,
+                       double *gap, int32_t *err_flag, void *stream, void **bound);
+int pgm_rows_bound_run(void *bound);
+int pgm_rows_bound_destroy(void *bound);
 
 #ifdef __cplusplus
 }

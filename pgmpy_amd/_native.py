@@ -16,7 +16,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libpgmhip.so")
+LIB_PATH = os.environ.get("PGM_LIB_PATH") or os.path.join(HERE, "lib", "libpgmhip.so")  # override: tools only
 
 PGM_OK = 0
 PGM_EINVAL = -1
@@ -35,7 +35,7 @@ ROWS_MAX_EV = 48
 ROWS_MAX_COMP = 12
 ROWS_MAX_MARG = 192
 ROWS_MARGINALS, ROWS_JOINT, ROWS_MAP, ROWS_MAPGAP, ROWS_VALUES_GLOBAL = 1, 2, 4, 8, 16
-ROWS_ONE_GROUP, ROWS_GENERIC, ROWS_PLAIN_STORE = 32, 64, 128
+ROWS_ONE_GROUP, ROWS_GENERIC, ROWS_NO_JIT = 32, 64, 128
 
 
 class NativeUnavailable(RuntimeError):
@@ -169,6 +169,12 @@ _SIGS = {
     "pgm_rows_plan_destroy": ([_P], ctypes.c_int),
     "pgm_rows_plan_run": ([_P, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P,
                            ctypes.c_int64, _P, _P, _P, _P], ctypes.c_int),
+    "pgm_rows_plan_bind": ([_P, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _P, _P,
+                            ctypes.c_int64, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "pgm_rows_bound_run": ([_P], ctypes.c_int),
+    "pgm_rows_plan_source": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                             ctypes.c_int),
+    "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

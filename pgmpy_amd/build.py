@@ -24,21 +24,26 @@ def hipcc():
     return "hipcc"
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, out=OUT, defines=()):
+    """defines: extra -D macros (tools only, e.g. PGM_ROWS_TIMELINE into lib/libpgmhip_timeline.so)."""
     deps = [SRC, os.path.join(INC, "pgmhip.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-I", INC, "-o", tmp, SRC]
+           "-Wno-unused-result", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", tmp, SRC, "-lhiprtc"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
+
+TIMELINE_OUT = os.path.join(HERE, "lib", "libpgmhip_timeline.so")
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    print(OUT)
+    if "--timeline" in sys.argv:  # per-wave timestamps in the affine row kernel (tools/rows_timeline.py)
+        print(build(force=True, out=TIMELINE_OUT, defines=("PGM_ROWS_TIMELINE",)))
+    else:
+        print(build(force="--force" in sys.argv))

@@ -13,6 +13,7 @@
 //   k_rows                         fused per-row plan: reduce -> sum-product -> normalize ->
 //                                  marginals / joint / MAP, one lane per evidence row
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -20,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -1106,6 +1108,12 @@ struct RowsHandle {
   bool any_table, all_affine;
   double *d_values;
   int32_t *d_desc;
+  // plan-specialised kernel (hipRTC): generated at create for all-affine plans, compiled on first use
+  std::string jit_src;
+  std::mutex jit_mu;
+  int jit_state = 0;  // 0 not compiled, 1 ready, -1 unavailable (the AOT kernels run instead)
+  hipModule_t jit_mod = nullptr;
+  hipFunction_t jit_fn = nullptr;
 };
 
 template <bool VL, bool AL, int MAXFC, int MAXT>
@@ -1345,31 +1353,38 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows(
   }
 }
 
+// workgroup barrier for LDS-only exchanges: waits for this wave's LDS traffic, not for its global
+// loads/stores (__syncthreads' release fence would wait for every outstanding store to be acked)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // All-affine plans (every component one query dim, no hidden dim, <= 4 factors, <= 8 evidence
 // terms: the common batched-predict shape, e.g. munin C3).  Same work split as k_rows, but each
 // wave loads its component's descriptor into registers once, folds evidence with multiply-adds
 // against host-precomputed per-slot strides, and carries the MAP bookkeeping only when asked.
+// Latency shape (one row group per wave at 100k rows): descriptor -> {codes, CPT staging} in
+// flight together (staging issues every load before any LDS write) -> products -> LDS-only
+// exchange of component masses -> stores.  PGM_ROWS_TIMELINE builds add per-wave s_memrealtime
+// stamps (tools/rows_timeline.py).
 template <bool VL, int NF, int NT, bool MAP>
 __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
     const RowsK p, const double *__restrict__ gvals, const int32_t *__restrict__ desc,
     const uint8_t *__restrict__ codes, int64_t ld_codes, int64_t row0, int64_t n_rows, int32_t mode, int32_t RG,
-    int32_t W, double *__restrict__ marg, int64_t ld_out, int32_t *__restrict__ map, double *__restrict__ gap,
+    double *__restrict__ marg, int64_t ld_out, int32_t *__restrict__ map, double *__restrict__ gap,
     int32_t *__restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int32_t dbg = W >> 8;  // DEBUG strip mask (tools only)
-  W &= 255;
+#ifdef PGM_ROWS_TIMELINE
+  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   const int lane = threadIdx.x & 63;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // this wave's component
   const int NC = p.n_comp;
-  // wave w = (row wave rw, component c): W row groups side by side, one wave per component each
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int rw = w / NC;
-  const int c = w - rw * NC;
   const RowsComp &cd = ((const RowsComp *)desc)[c];
   double *svals = lds;
-  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0) + rw * NC * 64;  // [W][NC][64]
-  double *xgap = lds + (VL ? ((p.n_values + 1) & ~1) : 0) + W * NC * 64 + rw * NC * 64;
-  int32_t *xmap = (int32_t *)(lds + (VL ? ((p.n_values + 1) & ~1) : 0) + 2 * W * NC * 64) + rw * NC * 64;
-  const bool plain_store = (mode & PGM_ROWS_PLAIN_STORE) != 0;
+  double *xmass = lds + (VL ? ((p.n_values + 1) & ~1) : 0);  // [NC][64]
+  double *xgap = xmass + NC * 64;                              // [NC][64] (MAP only)
+  int32_t *xmap = (int32_t *)(xgap + NC * 64);                 // [NC][64] (MAP only)
   const bool do_marg = (mode & PGM_ROWS_MARGINALS) != 0;
   // descriptor -> registers (wave-uniform)
   int32_t fb[NF], fs[NF], S[NT][NF];
@@ -1392,30 +1407,57 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
   const int32_t ms = cd.mstride;
   double *mrow = marg + (int64_t)cd.marg0 * ld_out;
   auto val = [&](int32_t i) -> double {
-    if constexpr (VL) {
-      if (dbg & 2) return gvals[i];
-      return svals[i];
-    } else return gvals[i];
+    if constexpr (VL) return svals[i];
+    else return gvals[i];
   };
-  // every wave stages its own component's values: the W waves of one component write identical
-  // values to the same LDS words, so no wave waits on another (no barrier)
-  if (VL && !(dbg & 2)) {
-    if (lane == 0) svals[p.one_idx] = 1.0;
-    for (int i = cd.val_lo + lane; i < cd.val_hi; i += 64) svals[i] = gvals[i];
-  }
-  auto row_of = [&](int g) -> int64_t { return (((int64_t)blockIdx.x * RG + g) * W + rw) * 64 + lane; };
   auto load_codes = [&](int g, uint32_t (&code)[NT]) {
-    const int64_t r = row_of(g);
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
     const uint8_t *crow = codes + (r < n_rows ? r : 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) code[j] = (dbg & 8) ? (uint32_t)(lane & 1) : crow[cofs[j]];
+    for (int j = 0; j < NT; ++j) code[j] = crow[cofs[j]];
   };
+  // this wave's first 256 CPT values, then the first row group's codes, all in flight before the
+  // LDS writes (vmcnt is in order: the writes wait only for the value loads); larger components
+  // stage the rest in further 256-value batches
   uint32_t nx[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) nx[j] = 0;
+  const int vlo = cd.val_lo, vhi = cd.val_hi;
+  double t[4];
+  if constexpr (VL) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = vlo + u * 64 + lane;
+      t[u] = gvals[i < vhi ? i : vhi - 1];
+    }
+  }
   if (nt > 0) load_codes(0, nx);
+  if constexpr (VL) {
+    if (lane == 0) svals[p.one_idx] = 1.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // clamped lanes rewrite the last value with itself: no branches
+      const int i = vlo + u * 64 + lane;
+      svals[i < vhi ? i : vhi - 1] = t[u];
+    }
+    for (int base = vlo + 256; base < vhi; base += 256) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 64 + lane;
+        t[u] = gvals[i < vhi ? i : vhi - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 64 + lane;
+        if (i < vhi) svals[i] = t[u];
+      }
+    }
+  }
+#ifdef PGM_ROWS_TIMELINE
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const uint64_t t_ready = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int g = 0; g < RG; ++g) {
-    const int64_t r = row_of(g);
+    const int64_t r = ((int64_t)blockIdx.x * RG + g) * 64 + lane;
     const bool live = r < n_rows;
     uint32_t code[NT];
 #pragma unroll
@@ -1440,14 +1482,9 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
 #pragma unroll
     for (int qs = 0; qs < RC; ++qs) {
       const int32_t q = qs < plast ? qs : plast;
-      double prod;
-      if (dbg & 4) {
-        prod = (double)(cb[0] + q);
-      } else {
-        prod = val(cb[0] + q * fs[0]);
+      double prod = val(cb[0] + q * fs[0]);
 #pragma unroll
-        for (int k = 1; k < NF; ++k) prod *= val(cb[k] + q * fs[k]);
-      }
+      for (int k = 1; k < NF; ++k) prod *= val(cb[k] + q * fs[k]);
       pc[qs] = prod;
     }
     double mass = 0.0, best = -1.0, second = -1.0;
@@ -1473,38 +1510,33 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
       for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
       visit(qs, prod);
     }
-    if (do_marg && live) {  // normalised marginal streamed straight to HBM
-      const double inv = 1.0 / mass;
-      double *out = mrow + r;
-#pragma unroll
-      for (int qs = 0; qs < RC; ++qs)
-        if ((uint32_t)qs < P) {
-          if (plain_store) out[(int64_t)qs * ld_out] = pc[qs] * inv;
-          else __builtin_nontemporal_store(pc[qs] * inv, out + (int64_t)qs * ld_out);
-        }
-      for (uint32_t qs = RC; qs < P; ++qs) {
-        double prod = val(cb[0] + (int32_t)qs * fs[0]);
-#pragma unroll
-        for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
-        if (plain_store) out[(int64_t)qs * ld_out] = prod * inv;
-        else __builtin_nontemporal_store(prod * inv, out + (int64_t)qs * ld_out);
-      }
-    }
+    // the component waves of a row group meet BEFORE any store, through an LDS-only barrier
+    // (no wait for global stores to be acknowledged, as __syncthreads' release fence would)
     double z = mass;
-    if (NC > 1 && !(dbg & 1)) {
+    if (NC > 1) {
       xmass[c * 64 + lane] = mass;
       if constexpr (MAP) {
         xmap[c * 64 + lane] = best_s * ms;
         xgap[c * 64 + lane] = (P > 1) ? (best > 0.0 ? (best - (second < 0.0 ? 0.0 : second)) / best : 0.0) : 1.0;
       }
-      __syncthreads();
+      lds_barrier();
       z = 1.0;
       for (int c2 = 0; c2 < NC; ++c2) z *= xmass[c2 * 64 + lane];
     }
     // impossible evidence (zero total mass): every marginal is 0/0 = NaN and np.argmax gives 0
     const bool dead = !(z > 0.0);
-    if (live && do_marg && dead) {
-      for (uint32_t qs = 0; qs < P; ++qs) mrow[(int64_t)qs * ld_out + r] = __builtin_nan("");
+    if (do_marg && live) {  // normalised marginal streamed straight to HBM
+      const double inv = dead ? __builtin_nan("") : 1.0 / mass;
+      double *out = mrow + r;
+#pragma unroll
+      for (int qs = 0; qs < RC; ++qs)
+        if ((uint32_t)qs < P) out[(int64_t)qs * ld_out] = pc[qs] * inv;
+      for (uint32_t qs = RC; qs < P; ++qs) {
+        double prod = val(cb[0] + (int32_t)qs * fs[0]);
+#pragma unroll
+        for (int k = 1; k < NF; ++k) prod *= val(cb[k] + (int32_t)qs * fs[k]);
+        out[(int64_t)qs * ld_out] = prod * inv;
+      }
     }
     if constexpr (MAP) {
       if (live && c == 0) {
@@ -1522,27 +1554,43 @@ __global__ __launch_bounds__(64 * PGM_ROWS_MAX_COMP) void k_rows_affine(
         if (gap && (mode & PGM_ROWS_MAPGAP)) gap[r] = dead ? 0.0 : mg;
       }
     }
-    if (NC > 1 && g + 1 < RG && !(dbg & 1)) __syncthreads();  // the exchange slots are reused by the next row group
+    if (NC > 1 && g + 1 < RG) lds_barrier();  // the exchange slots are reused by the next row group
   }
+#ifdef PGM_ROWS_TIMELINE
+  {  // [entry, ready, stores issued, stores acked, HW_ID, XCC_ID] per wave into `gap`
+    const uint64_t t_issued = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const uint64_t t_done = __builtin_amdgcn_s_memrealtime();
+    if (gap && !(mode & PGM_ROWS_MAPGAP) && lane == 0) {
+      double *tl = gap + ((int64_t)blockIdx.x * (blockDim.x >> 6) + c) * 6;
+      tl[0] = (double)t_entry;
+      tl[1] = (double)t_ready;
+      tl[2] = (double)t_issued;
+      tl[3] = (double)t_done;
+      tl[4] = (double)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+      tl[5] = (double)__builtin_amdgcn_s_getreg(20 | (15 << 11));
+    }
+  }
+#endif
 }
 
 template <bool VL, int NF, int NT>
 static void launch_affine_m(bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s, const RowsK &k,
                             const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc, int64_t row0,
-                            int64_t n, int32_t mode, int32_t RG, int32_t W, double *marg, int64_t ldo, int32_t *map,
+                            int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo, int32_t *map,
                             double *gap, int32_t *err) {
   if (do_map)
-    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, true>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, true>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
   else
-    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, false>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err);
+    hipLaunchKernelGGL((k_rows_affine<VL, NF, NT, false>), g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err);
 }
 
 template <bool VL>
 static void launch_affine(int max_nf, int max_nt, bool do_map, dim3 g, dim3 b, size_t lds, hipStream_t s,
                           const RowsK &k, const double *v, const int32_t *t, const uint8_t *codes, int64_t ldc,
-                          int64_t row0, int64_t n, int32_t mode, int32_t RG, int32_t W, double *marg, int64_t ldo,
+                          int64_t row0, int64_t n, int32_t mode, int32_t RG, double *marg, int64_t ldo,
                           int32_t *map, double *gap, int32_t *err) {
-#define PGM_AFF(NF, NT) launch_affine_m<VL, NF, NT>(do_map, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, W, marg, ldo, map, gap, err)
+#define PGM_AFF(NF, NT) launch_affine_m<VL, NF, NT>(do_map, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, ldo, map, gap, err)
   if (max_nt <= 4) {
     if (max_nf <= 1) PGM_AFF(1, 4);
     else if (max_nf <= 2) PGM_AFF(2, 4);
@@ -1580,6 +1628,158 @@ static void launch_rows_f(int max_nt, int max_nf, dim3 g, dim3 b, size_t lds, hi
     launch_rows_t<VL, AL, 8>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
   else
     launch_rows_t<VL, AL, PGM_ROWS_MAX_EV>(max_nf, g, b, lds, s, k, v, t, codes, ldc, row0, n, mode, RG, marg, joint, ldo, map, gap, err);
+}
+
+// ----------------------------------------------------------------------------- plan-specialised row kernel
+// For plans whose components each have one query variable and no hidden variable (the batched
+// predict shape, munin C3), pgm_rows_plan_create also writes a kernel source with every column,
+// stride, base offset and cardinality as a literal; hipRTC compiles it for gfx950 on first use.
+// One thread per evidence row, 256-row workgroups: the CPT values are staged in LDS with every
+// load issued before any LDS write, all evidence codes are loaded once per distinct column, and
+// each component's products stay in registers between the mass and the stores.  No descriptor
+// loads, no inter-wave exchange, a few hundred bytes of code.  Arithmetic order is exactly the
+// generic kernels' (factor products left to right, masses summed in state order, components'
+// masses multiplied in order), so results are bit-identical to k_rows_affine / k_rows.
+static void appendf(std::string &o, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  o += buf;
+}
+
+static std::string rows_jit_source(const pgm_rows_plan *pl) {
+  const int NV = pl->n_values + 1;  // + trailing 1.0
+  const bool lds = NV * 8 <= 48 * 1024;
+  std::string o;
+  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_rows_jit(const double *__restrict__ V, "
+       "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, double *__restrict__ M, "
+       "long long ldo, int *__restrict__ MP, double *__restrict__ G, int *__restrict__ E, int mode) {\n";
+  o += "  const int t = threadIdx.x;\n  const long long r = (long long)blockIdx.x * 256 + t;\n";
+  o += "  const long long rc = r < n ? r : n - 1;\n";
+  const int K = (NV + 255) / 256;
+  if (lds) {
+    appendf(o, "  __shared__ double S[%d];\n", K * 256);
+    for (int i = 0; i < K; ++i) appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, 256 * i, NV, 256 * i, NV - 1);
+  }
+  // distinct evidence columns, each loaded once
+  std::vector<int> cols;
+  for (int j = 0; j < pl->n_ev; ++j)
+    if (std::find(cols.begin(), cols.end(), pl->ev_col[j]) == cols.end()) cols.push_back(pl->ev_col[j]);
+  if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + rc;\n";
+  for (size_t i = 0; i < cols.size(); ++i) appendf(o, "  const unsigned e%zu = cr[%dLL * ldc];\n", i, cols[i]);
+  if (lds) {
+    for (int i = 0; i < K; ++i) appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", 256 * i, NV, 256 * i, NV - 1, i);
+    o += "  __syncthreads();\n#define VAL(i) S[i]\n";
+  } else {
+    o += "#define VAL(i) V[i]\n";
+  }
+  o += "  unsigned bad = 0u;\n";
+  const int NC = pl->n_comp;
+  for (int c = 0; c < NC; ++c) {
+    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
+    const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
+    const int P = nq == 1 ? pl->loop_card[lb] : 1;
+    for (int f = fb; f < fe; ++f) {
+      appendf(o, "  int o%d_%d = %d;\n", c, f - fb, pl->fac_base[f]);
+      for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) {
+        const int ci = (int)(std::find(cols.begin(), cols.end(), pl->ev_col[j]) - cols.begin());
+        appendf(o, "  { const unsigned x = e%d; bad |= (unsigned)(x >= %uu); o%d_%d += (x >= %uu ? 0 : (int)x) * %d; }\n", ci,
+                (unsigned)pl->ev_card[j], c, f - fb, (unsigned)pl->ev_card[j], pl->ev_stride[j]);
+      }
+    }
+    for (int q = 0; q < P; ++q) {
+      appendf(o, "  const double p%d_%d = ", c, q);
+      if (fe == fb) o += "1.0";
+      for (int f = fb; f < fe; ++f) {
+        const int qs = nq == 1 ? pl->fac_stride[f][lb] : 0;
+        appendf(o, "%sVAL(o%d_%d + %d)", f > fb ? " * " : "", c, f - fb, q * qs);
+      }
+      o += ";\n";
+    }
+    appendf(o, "  const double m%d = p%d_0", c, c);
+    for (int q = 1; q < P; ++q) appendf(o, " + p%d_%d", c, q);
+    o += ";\n";
+  }
+  o += "  const double z = ";
+  if (NC == 1) o += "m0";
+  else {
+    o += "1.0";
+    for (int c = 0; c < NC; ++c) appendf(o, " * m%d", c);
+  }
+  o += ";\n  const bool dead = !(z > 0.0);\n";
+  o += "  if (bad && r < n && E) atomicOr(E, 1);\n  if (r >= n) return;\n";
+  o += "  if (mode & 1) {\n";
+  for (int c = 0; c < NC; ++c) {
+    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
+    if (nq != 1) continue;
+    appendf(o, "    { const double iv = dead ? __builtin_nan(\"\") : 1.0 / m%d;\n", c);
+    for (int q = 0; q < pl->loop_card[lb]; ++q)
+      appendf(o, "      M[%dLL * ldo + r] = p%d_%d * iv;\n", pl->loop_marg_off[lb] + q, c, q);
+    o += "    }\n";
+  }
+  o += "  }\n  if (mode & 12) {\n    int m = 0;\n    double mg = 1.0;\n";
+  for (int c = 0; c < NC; ++c) {
+    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
+    const int P = nq == 1 ? pl->loop_card[lb] : 1;
+    const int ms = nq == 1 ? pl->loop_map_stride[lb] : 0;
+    appendf(o, "    { double b = -1.0, s = -1.0; int bs = 0;\n");
+    for (int q = 0; q < P; ++q)
+      appendf(o, "      if (p%d_%d > b) { s = b; b = p%d_%d; bs = %d; } else if (p%d_%d > s) { s = p%d_%d; }\n", c, q, c, q,
+              q, c, q, c, q);
+    appendf(o, "      m += bs * %d;\n", ms);
+    if (P > 1)
+      o += "      const double g = b > 0.0 ? (b - (s < 0.0 ? 0.0 : s)) / b : 0.0;\n";
+    else
+      o += "      const double g = 1.0;\n";
+    o += NC == 1 ? "      mg = g; }\n" : "      mg = fmin(mg, g); }\n";
+  }
+  o += "    if (MP) MP[r] = dead ? 0 : m;\n    if ((mode & 8) && G) G[r] = dead ? 0.0 : mg;\n  }\n}\n";
+  return o;
+}
+
+static std::mutex g_rtc_mu;  // hipRTC program creation is serialised (one compile at a time)
+
+// compile + load the handle's specialised kernel once; false when unavailable (AOT kernels run)
+static bool rows_jit_ready(RowsHandle *h) {
+  if (h->jit_src.empty()) return false;
+  std::lock_guard<std::mutex> lk(h->jit_mu);
+  if (h->jit_state != 0) return h->jit_state > 0;
+  h->jit_state = -1;
+  static const bool disabled = getenv("PGM_NO_JIT") != nullptr;  // testing: AOT kernels only
+  if (disabled) return false;
+  std::lock_guard<std::mutex> lk2(g_rtc_mu);
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, h->jit_src.c_str(), "pgm_rows_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    return false;
+  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 2, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    fprintf(stderr, "pgmhip: specialised row kernel did not compile (generic kernels used):\n%s\n", log.c_str());
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t sz = 0;
+  hiprtcGetCodeSize(prog, &sz);
+  std::vector<char> code(sz);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  if (hipModuleLoadData(&h->jit_mod, code.data()) != hipSuccess) {
+    (void)hipGetLastError();
+    h->jit_mod = nullptr;
+    return false;
+  }
+  if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  h->jit_state = 1;
+  return true;
 }
 
 // ============================================================================= C-ABI
@@ -2277,6 +2477,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   h->all_affine = !any_table && max_nf <= 4 && max_nt <= 8;
   h->d_values = nullptr;
   h->d_desc = nullptr;
+  if (!any_table) h->jit_src = rows_jit_source(pl);
   hipError_t e = hipSuccess;
   e = hipMalloc((void **)&h->d_values, sizeof(double) * (pl->n_values + 1));
   if (e == hipSuccess && pl->n_values > 0)
@@ -2298,18 +2499,41 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   return PGM_OK;
 }
 
+int pgm_rows_plan_source(const pgm_rows_plan *pl, char *buf, size_t len, size_t *needed) {
+  if (!pl) return fail(PGM_EINVAL, "rows_plan_source: null plan");
+  if (pl->n_comp < 1 || pl->n_comp > PGM_ROWS_MAX_COMP || pl->n_fac < 0 || pl->n_fac > PGM_ROWS_MAX_FAC ||
+      pl->n_ev < 0 || pl->n_ev > PGM_ROWS_MAX_EV || pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP)
+    return fail(PGM_EINVAL, "rows_plan_source: plan out of range");
+  for (int c = 0; c < pl->n_comp; ++c)
+    if (pl->comp_n_query[c] > 1 || pl->comp_loop_end[c] - pl->comp_loop_begin[c] != pl->comp_n_query[c])
+      return fail(PGM_EINVAL, "rows_plan_source: component %d is not specialisable (query dims %d, loop dims %d)", c,
+                  pl->comp_n_query[c], pl->comp_loop_end[c] - pl->comp_loop_begin[c]);
+  const std::string src = rows_jit_source(pl);
+  if (needed) *needed = src.size() + 1;
+  if (buf && len > 0) {
+    const size_t n = std::min(len - 1, src.size());
+    memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
+  return PGM_OK;
+}
+
 int pgm_rows_plan_destroy(void *handle) {
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
   if (h->d_values) (void)hipFree(h->d_values);
   if (h->d_desc) (void)hipFree(h->d_desc);
+  if (h->jit_mod) (void)hipModuleUnload(h->jit_mod);
   delete h;
   return PGM_OK;
 }
 
-int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
-                      double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap, int32_t *err_flag,
-                      void *stream) {
+}  // extern "C"
+
+// dry: validate and size the launch only (pgm_rows_plan_bind)
+static int rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
+                         int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap,
+                         int32_t *err_flag, void *stream, bool dry) {
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "rows_plan_run: null handle");
   if (n_rows <= 0) return PGM_OK;
@@ -2340,33 +2564,42 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   hipStream_t s = S(stream);
   const double *v = h->d_values;
   const int32_t *t = h->d_desc;
+  if (!(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP)) &&
+      rows_jit_ready(h)) {
+    const uint64_t jblocks = ((uint64_t)n_rows + 255) / 256;
+    if (jblocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
+    if (dry) return PGM_OK;
+    const uint8_t *cp = codes;
+    int64_t ldc = ld_codes, r0 = row0, nr = n_rows, ldo = ld_out;
+    double *mg = marg, *gp = gap;
+    int32_t *mp = map, *ef = err_flag;
+    int32_t md = mode;
+    void *args[] = {(void *)&v, (void *)&cp, &ldc, &r0, &nr, (void *)&mg, &ldo, (void *)&mp, (void *)&gp, (void *)&ef, &md};
+    HIP_TRY(hipModuleLaunchKernel(h->jit_fn, (unsigned)jblocks, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+    return PGM_OK;
+  }
   if (h->all_affine && !(mode & PGM_ROWS_JOINT) && !(mode & PGM_ROWS_GENERIC)) {
-    // W row groups side by side per workgroup (W x n_comp waves)
-    static const int envW = getenv("PGM_ROWS_W") ? atoi(getenv("PGM_ROWS_W")) : 0;
-    static const int envRG = getenv("PGM_ROWS_RG") ? atoi(getenv("PGM_ROWS_RG")) : 0;
-    static const int envDbg = getenv("PGM_ROWS_DBG") ? atoi(getenv("PGM_ROWS_DBG")) : 0;
-    int32_t W = envW > 0 ? envW : 1;
-    W = std::max(1, std::min<int32_t>(W, PGM_ROWS_MAX_COMP / k.n_comp));
     RG = 1;
     if (vals_lds && !(mode & PGM_ROWS_ONE_GROUP))
-      RG = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, groups / (4096ull * W)));
-    if (envRG > 0) RG = envRG;
-    const uint64_t ablocks = (groups + (uint64_t)RG * W - 1) / ((uint64_t)RG * W);
+      RG = (int32_t)std::max<uint64_t>(1, std::min<uint64_t>(8, groups / 4096));
+    const uint64_t ablocks = (groups + RG - 1) / RG;
     if (ablocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
-    const size_t alds = vals_bytes + x_bytes * W;
-    const dim3 ag((unsigned)ablocks), ab(64 * k.n_comp * W);
     const bool do_map = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) != 0;
-    const int32_t Wd = W | (envDbg << 8);
+    // exchange slots: masses only, unless MAP digits / gaps are combined too
+    const size_t x_aff = k.n_comp > 1 ? (size_t)k.n_comp * 64 * (do_map ? 2 * sizeof(double) + sizeof(int32_t) : sizeof(double)) : 0;
+    const dim3 ag((unsigned)ablocks), ab(64 * k.n_comp);
+    if (dry) return PGM_OK;
     if (vals_lds)
-      launch_affine<true>(h->max_nf, h->max_nt, do_map, ag, ab, alds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, Wd, marg, ld_out, map, gap, err_flag);
+      launch_affine<true>(h->max_nf, h->max_nt, do_map, ag, ab, vals_bytes + x_aff, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
     else
-      launch_affine<false>(h->max_nf, h->max_nt, do_map, ag, ab, alds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, Wd, marg, ld_out, map, gap, err_flag);
+      launch_affine<false>(h->max_nf, h->max_nt, do_map, ag, ab, vals_bytes + x_aff, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, ld_out, map, gap, err_flag);
     HIP_TRY(hipGetLastError());
     return PGM_OK;
   }
   const uint64_t blocks = (groups + RG - 1) / RG;
   if (blocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
   const dim3 g((unsigned)blocks), b(64 * k.n_waves);
+  if (dry) return PGM_OK;
   if (vals_lds && acc_lds)
     launch_rows_f<true, true>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   else if (vals_lds)
@@ -2376,6 +2609,57 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
   else
     launch_rows_f<false, false>(h->max_nt, h->max_nf, g, b, lds, s, k, v, t, codes, ld_codes, row0, n_rows, mode, RG, marg, joint, ld_out, map, gap, err_flag);
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+extern "C" {
+
+int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
+                      double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap, int32_t *err_flag,
+                      void *stream) {
+  return rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag, stream,
+                       false);
+}
+
+// A validated, fully bound pgm_rows_plan_run (a prepared launch): repeated batches over the same
+// buffers pay one argument-free call each instead of re-marshalling thirteen arguments.
+struct RowsBound {
+  void *handle;
+  int32_t mode;
+  const uint8_t *codes;
+  int64_t ld_codes, row0, n_rows;
+  double *marg, *joint;
+  int64_t ld_out;
+  int32_t *map;
+  double *gap;
+  int32_t *err;
+  void *stream;
+};
+
+int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
+                       int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap,
+                       int32_t *err_flag, void *stream, void **bound) {
+  if (!bound) return fail(PGM_EINVAL, "rows_plan_bind: null output pointer");
+  *bound = nullptr;
+  const int st = rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag,
+                               stream, true);
+  if (st != PGM_OK) return st;
+  RowsBound *b = new (std::nothrow) RowsBound{handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map,
+                                              gap, err_flag, stream};
+  if (!b) return fail(PGM_ENOMEM, "rows_plan_bind: out of host memory");
+  *bound = b;
+  return PGM_OK;
+}
+
+int pgm_rows_bound_run(void *bound) {
+  const RowsBound *b = (const RowsBound *)bound;
+  if (!b) return fail(PGM_EINVAL, "rows_bound_run: null handle");
+  return rows_plan_run(b->handle, b->mode, b->codes, b->ld_codes, b->row0, b->n_rows, b->marg, b->joint, b->ld_out,
+                       b->map, b->gap, b->err, b->stream, false);
+}
+
+int pgm_rows_bound_destroy(void *bound) {
+  delete (RowsBound *)bound;
   return PGM_OK;
 }
 

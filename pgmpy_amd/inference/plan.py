@@ -126,19 +126,19 @@ class PatternPlan:
         return comps
 
     def kernel_name(self):
-        """The device kernel pgm_rows_plan_run launches for this plan's marginal/MAP outputs
-        (the all-affine kernel when every component has one query variable, no hidden variable,
-        <= 4 factors and <= 8 evidence terms; pgmhip.hip pgm_rows_plan_create)."""
+        """The device kernel pgm_rows_plan_run launches for this plan's marginal/MAP outputs: the
+        plan-specialised hipRTC kernel `pgm_rows_jit` when every component has one query variable and
+        no hidden variable (pgmhip.hip rows_jit_source; if hipRTC is unavailable the AOT
+        k_rows_affine / k_rows run instead), else the table-driven k_rows."""
         if self.kind != "fused":
             return None
-        ev = set(self.evidence_vars)
         for q, h, f in self.components():
-            n_terms = sum(1 for i in f for v in self.factors[i][0] if v in ev)
-            if len(q) != 1 or h or len(f) > 4 or n_terms > 8:
+            if len(q) != 1 or h:
                 return "k_rows"
-        return "k_rows_affine"
+        return "pgm_rows_jit"
 
-    def _make_rows_plan(self, split):
+    def _rows_plan_struct(self, split):
+        """(pgm_rows_plan, packed CPT values, component count): host-only."""
         comps = self.components() if split else [(list(self.variables), list(self.hidden),
                                                   list(range(len(self.factors))))]
         if len(comps) > N.ROWS_MAX_COMP:
@@ -191,11 +191,26 @@ class PatternPlan:
         if values.size >= 2 ** 31:
             raise ValueError("plan values too large")
         pl.n_values = int(values.size)
+        return pl, values, len(comps)
+
+    def specialised_source(self):
+        """Source of the plan-specialised (hipRTC) row kernel for this plan (pgm_rows_plan_source);
+        host-only, no device needed."""
+        pl, _, _ = self._rows_plan_struct(split=True)
+        L = N.load_library()
+        need = ctypes.c_size_t()
+        N.check(L.pgm_rows_plan_source(ctypes.byref(pl), None, 0, ctypes.byref(need)), "rows_plan_source")
+        buf = ctypes.create_string_buffer(need.value)
+        N.check(L.pgm_rows_plan_source(ctypes.byref(pl), buf, need.value, None), "rows_plan_source")
+        return buf.value.decode()
+
+    def _make_rows_plan(self, split):
+        pl, values, n_comp = self._rows_plan_struct(split)
         L = N.lib()
         h = ctypes.c_void_p()
         N.check(L.pgm_rows_plan_create(ctypes.byref(pl), values.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)),
                 "rows_plan_create")
-        return h, pl, len(comps)
+        return h, pl, n_comp
 
     def _host_values(self, fi):
         """CPT values (C-order) of factor fi, packed into the plan (a copy, no arithmetic)."""
@@ -291,6 +306,14 @@ class PatternPlan:
                                     int(ld_out), N.ptr(out.get("map")), N.ptr(out.get("gap")), N.ptr(err),
                                     N.stream_handle()), "rows_plan_run")
         return out
+
+    def bind(self, codes, ld, row0, n_rows, out, err=None, stream=None):
+        """A prepared launch of run() on fixed buffers (pgm_rows_plan_bind): `.run()` re-runs the same
+        pass with one argument-free C call.  Fused plans with marginal / MAP outputs only."""
+        if self.kind != "fused" or "joint" in out:
+            raise ValueError("bind(): fused plans without a joint output only")
+        self._build_fused()
+        return BoundRows(self, codes, ld, row0, n_rows, out, err, stream)
 
     def _dev_factors(self):
         if not hasattr(self, "_dev_cache"):
@@ -442,3 +465,38 @@ class PatternPlan:
                 "factors": [list(v) for v, _ in self.factors], "hidden": self.hidden,
                 "evidence_columns": len(self.ev_used), "query_space": self.P, "hidden_space": self.H,
                 "values": int(sum(int(np.prod(c.cardinality)) for _, c in self.factors))}
+
+
+class BoundRows:
+    """Prepared fused row-plan launch (pgm_rows_plan_bind / pgm_rows_bound_run).  Keeps the plan and
+    every buffer alive for as long as the bound handle exists."""
+
+    def __init__(self, plan, codes, ld, row0, n_rows, out, err, stream):
+        import ctypes
+
+        L = N.lib()
+        self._keep = (plan, codes, out, err)
+        mode = plan._mode(out)
+        ld_out = int(out["marg"].stride(0)) if "marg" in out else int(n_rows)
+        h = ctypes.c_void_p()
+        N.check(L.pgm_rows_plan_bind(plan._handle, mode, N.ptr(codes), int(ld), int(row0), int(n_rows),
+                                     N.ptr(out.get("marg")), None, ld_out, N.ptr(out.get("map")),
+                                     N.ptr(out.get("gap")), N.ptr(err), N.stream_handle(stream), ctypes.byref(h)),
+                "rows_plan_bind")
+        self._h = h
+        self._run = L.pgm_rows_bound_run
+        self.out = out
+
+    def run(self):
+        st = self._run(self._h)
+        if st != 0:
+            N.check(st, "rows_bound_run")
+        return self.out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.load_library().pgm_rows_bound_destroy(h)
+            except Exception:
+                pass

@@ -140,3 +140,35 @@ def test_encode_frame_categorical_numeric_and_nan():
                            state_names={"b": [0, 1], "a": ["0", "1"]}))
     codes = encode_frame(bn, pd.DataFrame({"a": [1, 0, 1], "b": ["1", "0", 1]}))
     assert codes.tolist() == [[1, 0, 1], [1, 0, 1]]
+
+
+def test_specialised_row_kernel_source_compiles_for_gfx950():
+    """pgm_rows_plan_source (host-only) emits the C3 template's specialised kernel: every evidence
+    column loaded once, one store per marginal entry, and it compiles for gfx950 with hipcc."""
+    import random
+    import shutil
+    import subprocess
+    import tempfile
+
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    obs = sorted(v for v in m.nodes() if v not in missing)
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    assert plan.kernel_name() == "pgm_rows_jit"
+    src = plan.specialised_source()
+    assert src.count("M[") == plan.n_acc == 17
+    assert src.count("cr[") == 7  # the template's 7 evidence columns
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "k.hip")
+        with open(path, "w") as f:
+            f.write(src)
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-x", "hip", "-include", "hip/hip_runtime.h",
+                            "--cuda-device-only", "-c", path, "-o", os.path.join(d, "k.o")],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr

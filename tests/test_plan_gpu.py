@@ -104,3 +104,104 @@ def test_c3_template_factorises_into_components(gpu):
     assert plan.kind == "fused"
     d = plan.describe()
     assert d["components"] == 3 and d["evidence_columns"] == 7 and d["values"] == 723
+
+
+def test_bound_rows_launch_matches_run(gpu):
+    """pgm_rows_plan_bind / pgm_rows_bound_run (the prepared launch bench.py times) writes exactly
+    what pgm_rows_plan_run writes, re-runs on new codes in place, and validates once at bind."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    rows = 1000
+    codes, nodes = forward_sample_codes(m, rows, seed=5)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+    plan.run(d, rows, 0, rows, ref)
+    out = plan.alloc_outputs(rows, marginals=True, map_=True)
+    bound = plan.bind(d, rows, 0, rows, out)
+    bound.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    d.copy_(upload_codes(np.ascontiguousarray(ev[:, ::-1])))  # new evidence, same buffer
+    bound.run()
+    plan.run(d, rows, 0, rows, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    with pytest.raises(ValueError):
+        plan.bind(d, rows, 0, rows, {"marg": torch.empty((plan.n_acc, rows // 2), dtype=torch.float64,
+                                                          device=d.device)})
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_specialised_kernel_bit_identical(gpu, seed):
+    """The plan-specialised (hipRTC) row kernel agrees with the AOT kernels (k_rows_affine and the
+    table-driven k_rows) to the last place: marginals, MAP index (where the top-two gap is not a
+    tie) and MAP gap, NaN rows of impossible evidence, and the out-of-range evidence flag."""
+    import torch
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.inference.batch import encode_frame, upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+
+    bn, onet = random_bn(seed)
+    rng = np.random.default_rng(500 + seed)
+    names = sorted(bn.nodes())
+    checked = 0
+    for trial in range(60):
+        if checked >= 4:
+            break
+        picks = list(rng.choice(names, size=int(rng.integers(6, 13)), replace=False))
+        nq = int(rng.integers(1, 3))
+        q, e = picks[:nq], picks[nq:]
+        n = 300
+        rows = {v: [onet.states[v][int(rng.integers(0, onet.card[v]))] for _ in range(n)] for v in e}
+        df = pd.DataFrame(rows, columns=e)
+        col_of = {c: i for i, c in enumerate(e)}
+        codes = upload_codes(encode_frame(bn, df))
+        plan = PatternPlan(bn, q, e, col_of)
+        if plan.kind != "fused" or plan.kernel_name() != "pgm_rows_jit":
+            continue
+        outs = {}
+        for name, extra in (("jit", 0), ("aot", N.ROWS_NO_JIT), ("generic", N.ROWS_GENERIC)):
+            plan.extra_mode = extra
+            o = plan.alloc_outputs(n, marginals=True, map_=True, gap=True)
+            err = torch.zeros(1, dtype=torch.int32, device=codes.device)
+            plan.run(codes, n, 0, n, o, err=err)
+            outs[name] = (o, int(err.item()))
+        plan.extra_mode = 0
+        for name in ("aot", "generic"):
+            a, b = outs["jit"][0], outs[name][0]
+            assert torch.equal(a["marg"].isnan(), b["marg"].isnan())
+            # same arithmetic order as k_rows_affine (bit-identical there); the table-driven k_rows
+            # may round differently in the last place
+            torch.testing.assert_close(a["marg"], b["marg"], rtol=1e-14, atol=0, equal_nan=True)
+            torch.testing.assert_close(a["gap"], b["gap"], rtol=1e-12, atol=1e-15)
+            clear = a["gap"] > 1e-9
+            assert torch.equal(a["map"][clear], b["map"][clear]), name
+            assert outs["jit"][1] == outs[name][1] == 0
+        # an out-of-range code raises the flag and reads state 0 in both kernels
+        used = [col_of[v] for v in plan.ev_used]
+        if used:
+            bad = codes.clone()
+            bad[used[0], :7] = 250
+            for extra in (0, N.ROWS_NO_JIT):
+                plan.extra_mode = extra
+                o = plan.alloc_outputs(n, marginals=True)
+                err = torch.zeros(1, dtype=torch.int32, device=codes.device)
+                plan.run(bad, n, 0, n, o, err=err)
+                assert int(err.item()) == 1
+            plan.extra_mode = 0
+        checked += 1
+    assert checked >= 1
