@@ -1114,6 +1114,7 @@ struct RowsHandle {
   int jit_state = 0;  // 0 not compiled, 1 ready, -1 unavailable (the AOT kernels run instead)
   hipModule_t jit_mod = nullptr;
   hipFunction_t jit_fn = nullptr;
+  hipFunction_t jit_fn2 = nullptr;  // two rows per thread
 };
 
 template <bool VL, bool AL, int MAXFC, int MAXT>
@@ -1649,26 +1650,34 @@ static void appendf(std::string &o, const char *fmt, ...) {
   o += buf;
 }
 
-static std::string rows_jit_source(const pgm_rows_plan *pl) {
+// R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
+static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
   const bool lds = NV * 8 <= 48 * 1024;
-  std::string o;
-  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_rows_jit(const double *__restrict__ V, "
-       "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, double *__restrict__ M, "
-       "long long ldo, int *__restrict__ MP, double *__restrict__ G, int *__restrict__ E, int mode) {\n";
-  o += "  const int t = threadIdx.x;\n  const long long r = (long long)blockIdx.x * 256 + t;\n";
-  o += "  const long long rc = r < n ? r : n - 1;\n";
+  appendf(o, "extern \"C\" __global__ void __launch_bounds__(256) pgm_rows_jit%s(const double *__restrict__ V, "
+             "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
+             "double *__restrict__ M, long long ldo, int *__restrict__ MP, double *__restrict__ G, "
+             "int *__restrict__ E, int mode) {\n", R == 2 ? "2" : "");
+  o += "  const int t = threadIdx.x;\n";
+  appendf(o, "  const long long r = ((long long)blockIdx.x * 256 + t) * %d;\n", R);
+  appendf(o, "  const long long rc = r < n ? r : n - %d;\n", R);
   const int K = (NV + 255) / 256;
   if (lds) {
     appendf(o, "  __shared__ double S[%d];\n", K * 256);
     for (int i = 0; i < K; ++i) appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, 256 * i, NV, 256 * i, NV - 1);
   }
-  // distinct evidence columns, each loaded once
-  std::vector<int> cols;
+  std::vector<int> cols;  // distinct evidence columns, each loaded once per row
   for (int j = 0; j < pl->n_ev; ++j)
     if (std::find(cols.begin(), cols.end(), pl->ev_col[j]) == cols.end()) cols.push_back(pl->ev_col[j]);
   if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + rc;\n";
-  for (size_t i = 0; i < cols.size(); ++i) appendf(o, "  const unsigned e%zu = cr[%dLL * ldc];\n", i, cols[i]);
+  for (size_t i = 0; i < cols.size(); ++i) {
+    if (R == 1) {
+      appendf(o, "  const unsigned e%zu_0 = cr[%dLL * ldc];\n", i, cols[i]);
+    } else {
+      appendf(o, "  const unsigned w%zu = *(const unsigned short *)(cr + %dLL * ldc);\n", i, cols[i]);
+      appendf(o, "  const unsigned e%zu_0 = w%zu & 255u, e%zu_1 = w%zu >> 8;\n", i, i, i, i);
+    }
+  }
   if (lds) {
     for (int i = 0; i < K; ++i) appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", 256 * i, NV, 256 * i, NV - 1, i);
     o += "  __syncthreads();\n#define VAL(i) S[i]\n";
@@ -1677,66 +1686,105 @@ static std::string rows_jit_source(const pgm_rows_plan *pl) {
   }
   o += "  unsigned bad = 0u;\n";
   const int NC = pl->n_comp;
-  for (int c = 0; c < NC; ++c) {
-    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
-    const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
-    const int P = nq == 1 ? pl->loop_card[lb] : 1;
-    for (int f = fb; f < fe; ++f) {
-      appendf(o, "  int o%d_%d = %d;\n", c, f - fb, pl->fac_base[f]);
-      for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) {
-        const int ci = (int)(std::find(cols.begin(), cols.end(), pl->ev_col[j]) - cols.begin());
-        appendf(o, "  { const unsigned x = e%d; bad |= (unsigned)(x >= %uu); o%d_%d += (x >= %uu ? 0 : (int)x) * %d; }\n", ci,
-                (unsigned)pl->ev_card[j], c, f - fb, (unsigned)pl->ev_card[j], pl->ev_stride[j]);
-      }
-    }
-    for (int q = 0; q < P; ++q) {
-      appendf(o, "  const double p%d_%d = ", c, q);
-      if (fe == fb) o += "1.0";
+  for (int u = 0; u < R; ++u) {
+    for (int c = 0; c < NC; ++c) {
+      const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
+      const int fb = pl->comp_fac_begin[c], fe = pl->comp_fac_end[c];
+      const int P = nq == 1 ? pl->loop_card[lb] : 1;
       for (int f = fb; f < fe; ++f) {
-        const int qs = nq == 1 ? pl->fac_stride[f][lb] : 0;
-        appendf(o, "%sVAL(o%d_%d + %d)", f > fb ? " * " : "", c, f - fb, q * qs);
+        appendf(o, "  int o%d_%d_%d = %d;\n", c, f - fb, u, pl->fac_base[f]);
+        for (int j = pl->fac_ev_begin[f]; j < pl->fac_ev_end[f]; ++j) {
+          const int ci = (int)(std::find(cols.begin(), cols.end(), pl->ev_col[j]) - cols.begin());
+          const unsigned cd = (unsigned)pl->ev_card[j];
+          appendf(o, "  { const unsigned x = e%d_%d; bad |= (unsigned)(x >= %uu); o%d_%d_%d += (x >= %uu ? 0 : (int)x) * %d; }\n",
+                  ci, u, cd, c, f - fb, u, cd, pl->ev_stride[j]);
+        }
       }
+      for (int q = 0; q < P; ++q) {
+        appendf(o, "  const double p%d_%d_%d = ", c, q, u);
+        if (fe == fb) o += "1.0";
+        for (int f = fb; f < fe; ++f) {
+          const int qs = nq == 1 ? pl->fac_stride[f][lb] : 0;
+          appendf(o, "%sVAL(o%d_%d_%d + %d)", f > fb ? " * " : "", c, f - fb, u, q * qs);
+        }
+        o += ";\n";
+      }
+      appendf(o, "  const double m%d_%d = p%d_0_%d", c, u, c, u);
+      for (int q = 1; q < P; ++q) appendf(o, " + p%d_%d_%d", c, q, u);
       o += ";\n";
     }
-    appendf(o, "  const double m%d = p%d_0", c, c);
-    for (int q = 1; q < P; ++q) appendf(o, " + p%d_%d", c, q);
-    o += ";\n";
+    appendf(o, "  const double z_%d = ", u);
+    if (NC == 1) appendf(o, "m0_%d", u);
+    else {
+      o += "1.0";
+      for (int c = 0; c < NC; ++c) appendf(o, " * m%d_%d", c, u);
+    }
+    appendf(o, ";\n  const bool dead_%d = !(z_%d > 0.0);\n", u, u);
   }
-  o += "  const double z = ";
-  if (NC == 1) o += "m0";
-  else {
-    o += "1.0";
-    for (int c = 0; c < NC; ++c) appendf(o, " * m%d", c);
-  }
-  o += ";\n  const bool dead = !(z > 0.0);\n";
   o += "  if (bad && r < n && E) atomicOr(E, 1);\n  if (r >= n) return;\n";
   o += "  if (mode & 1) {\n";
   for (int c = 0; c < NC; ++c) {
     const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
     if (nq != 1) continue;
-    appendf(o, "    { const double iv = dead ? __builtin_nan(\"\") : 1.0 / m%d;\n", c);
-    for (int q = 0; q < pl->loop_card[lb]; ++q)
-      appendf(o, "      M[%dLL * ldo + r] = p%d_%d * iv;\n", pl->loop_marg_off[lb] + q, c, q);
+    o += "    {";
+    for (int u = 0; u < R; ++u)
+      appendf(o, " const double iv_%d = dead_%d ? __builtin_nan(\"\") : 1.0 / m%d_%d;", u, u, c, u);
+    o += "\n";
+    for (int q = 0; q < pl->loop_card[lb]; ++q) {
+      if (R == 1)
+        appendf(o, "      M[%dLL * ldo + r] = p%d_%d_0 * iv_0;\n", pl->loop_marg_off[lb] + q, c, q);
+      else
+        appendf(o, "      *(double2 *)(M + %dLL * ldo + r) = make_double2(p%d_%d_0 * iv_0, p%d_%d_1 * iv_1);\n",
+                pl->loop_marg_off[lb] + q, c, q, c, q);
+    }
     o += "    }\n";
   }
-  o += "  }\n  if (mode & 12) {\n    int m = 0;\n    double mg = 1.0;\n";
-  for (int c = 0; c < NC; ++c) {
-    const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
-    const int P = nq == 1 ? pl->loop_card[lb] : 1;
-    const int ms = nq == 1 ? pl->loop_map_stride[lb] : 0;
-    appendf(o, "    { double b = -1.0, s = -1.0; int bs = 0;\n");
-    for (int q = 0; q < P; ++q)
-      appendf(o, "      if (p%d_%d > b) { s = b; b = p%d_%d; bs = %d; } else if (p%d_%d > s) { s = p%d_%d; }\n", c, q, c, q,
-              q, c, q, c, q);
-    appendf(o, "      m += bs * %d;\n", ms);
-    if (P > 1)
-      o += "      const double g = b > 0.0 ? (b - (s < 0.0 ? 0.0 : s)) / b : 0.0;\n";
-    else
-      o += "      const double g = 1.0;\n";
-    o += NC == 1 ? "      mg = g; }\n" : "      mg = fmin(mg, g); }\n";
+  o += "  }\n  if (mode & 12) {\n";
+  for (int u = 0; u < R; ++u) {
+    appendf(o, "    int m_%d = 0;\n    double mg_%d = 1.0;\n", u, u);
+    for (int c = 0; c < NC; ++c) {
+      const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
+      const int P = nq == 1 ? pl->loop_card[lb] : 1;
+      const int ms = nq == 1 ? pl->loop_map_stride[lb] : 0;
+      o += "    { double b = -1.0, s = -1.0; int bs = 0;\n";
+      for (int q = 0; q < P; ++q)
+        appendf(o, "      if (p%d_%d_%d > b) { s = b; b = p%d_%d_%d; bs = %d; } else if (p%d_%d_%d > s) { s = p%d_%d_%d; }\n",
+                c, q, u, c, q, u, q, c, q, u, c, q, u);
+      appendf(o, "      m_%d += bs * %d;\n", u, ms);
+      if (P > 1)
+        o += "      const double g = b > 0.0 ? (b - (s < 0.0 ? 0.0 : s)) / b : 0.0;\n";
+      else
+        o += "      const double g = 1.0;\n";
+      appendf(o, NC == 1 ? "      mg_%d = g; }\n" : "      mg_%d = fmin(mg_%d, g); }\n", u, u);
+    }
   }
-  o += "    if (MP) MP[r] = dead ? 0 : m;\n    if ((mode & 8) && G) G[r] = dead ? 0.0 : mg;\n  }\n}\n";
+  if (R == 1) {
+    o += "    if (MP) MP[r] = dead_0 ? 0 : m_0;\n    if ((mode & 8) && G) G[r] = dead_0 ? 0.0 : mg_0;\n  }\n}\n";
+  } else {
+    o += "    if (MP) *(int2 *)(MP + r) = make_int2(dead_0 ? 0 : m_0, dead_1 ? 0 : m_1);\n";
+    o += "    if ((mode & 8) && G) *(double2 *)(G + r) = make_double2(dead_0 ? 0.0 : mg_0, dead_1 ? 0.0 : mg_1);\n  }\n}\n";
+  }
+}
+
+static std::string rows_jit_source(const pgm_rows_plan *pl) {
+  std::string o;
+  emit_rows_kernel(o, pl, 1);
+  o += "\n";
+  emit_rows_kernel(o, pl, 2);
   return o;
+}
+
+// the two-rows-per-thread kernel's alignment contract (else the one-row kernel runs)
+static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
+                         const double *marg, int64_t ld_out, const int32_t *map, const double *gap) {
+  static const bool off = getenv("PGM_NO_JIT2") != nullptr;  // testing / tuning
+  // measured (MI355X): one row per thread is faster while the launch is latency-bound (100k rows:
+  // 4.6 vs 5.2 us), two rows with 16-B stores once it is HBM-bound (4M rows: 110 vs 126 us)
+  if (off || n_rows < 400000 || n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
+  if ((mode & PGM_ROWS_MARGINALS) && (((uintptr_t)marg & 15) || ld_out % 2)) return false;
+  if (map && ((uintptr_t)map & 7)) return false;
+  if ((mode & PGM_ROWS_MAPGAP) && gap && ((uintptr_t)gap & 15)) return false;
+  return true;
 }
 
 static std::mutex g_rtc_mu;  // hipRTC program creation is serialised (one compile at a time)
@@ -1774,7 +1822,8 @@ static bool rows_jit_ready(RowsHandle *h) {
     h->jit_mod = nullptr;
     return false;
   }
-  if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess) {
+  if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess ||
+      hipModuleGetFunction(&h->jit_fn2, h->jit_mod, "pgm_rows_jit2") != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -2566,7 +2615,8 @@ static int rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64
   const int32_t *t = h->d_desc;
   if (!(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP)) &&
       rows_jit_ready(h)) {
-    const uint64_t jblocks = ((uint64_t)n_rows + 255) / 256;
+    const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap);
+    const uint64_t jblocks = ((uint64_t)n_rows + (two ? 511 : 255)) / (two ? 512 : 256);
     if (jblocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
     if (dry) return PGM_OK;
     const uint8_t *cp = codes;
@@ -2575,7 +2625,7 @@ static int rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64
     int32_t *mp = map, *ef = err_flag;
     int32_t md = mode;
     void *args[] = {(void *)&v, (void *)&cp, &ldc, &r0, &nr, (void *)&mg, &ldo, (void *)&mp, (void *)&gp, (void *)&ef, &md};
-    HIP_TRY(hipModuleLaunchKernel(h->jit_fn, (unsigned)jblocks, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+    HIP_TRY(hipModuleLaunchKernel(two ? h->jit_fn2 : h->jit_fn, (unsigned)jblocks, 1, 1, 256, 1, 1, 0, s, args, nullptr));
     return PGM_OK;
   }
   if (h->all_affine && !(mode & PGM_ROWS_JOINT) && !(mode & PGM_ROWS_GENERIC)) {
@@ -2623,7 +2673,25 @@ int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t 
 
 // A validated, fully bound pgm_rows_plan_run (a prepared launch): repeated batches over the same
 // buffers pay one argument-free call each instead of re-marshalling thirteen arguments.
+struct RowsJitArgs {  // pgm_rows_jit's parameters, packed as the kernel's argument segment
+  const double *V;
+  const uint8_t *C;
+  int64_t ldc, row0, n;
+  double *M;
+  int64_t ldo;
+  int32_t *MP;
+  double *G;
+  int32_t *E;
+  int32_t mode;
+  int32_t pad;
+};
+
 struct RowsBound {
+  // specialised kernel bound: the packed argument segment and launch shape, launched directly
+  hipFunction_t fn = nullptr;
+  RowsJitArgs args;
+  size_t args_size = sizeof(RowsJitArgs);
+  unsigned blocks = 0;
   void *handle;
   int32_t mode;
   const uint8_t *codes;
@@ -2644,16 +2712,43 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
   const int st = rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag,
                                stream, true);
   if (st != PGM_OK) return st;
-  RowsBound *b = new (std::nothrow) RowsBound{handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map,
-                                              gap, err_flag, stream};
+  RowsBound *b = new (std::nothrow) RowsBound;
   if (!b) return fail(PGM_ENOMEM, "rows_plan_bind: out of host memory");
+  b->handle = handle;
+  b->mode = mode;
+  b->codes = codes;
+  b->ld_codes = ld_codes;
+  b->row0 = row0;
+  b->n_rows = n_rows;
+  b->marg = marg;
+  b->joint = joint;
+  b->ld_out = ld_out;
+  b->map = map;
+  b->gap = gap;
+  b->err = err_flag;
+  b->stream = stream;
+  RowsHandle *h = (RowsHandle *)handle;
+  // the same choice rows_plan_run makes (the dry run above compiled the kernel if it applies)
+  if (n_rows > 0 && h->jit_state > 0 &&
+      !(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP))) {
+    const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap);
+    b->fn = two ? h->jit_fn2 : h->jit_fn;
+    b->args = RowsJitArgs{h->d_values, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, err_flag, mode, 0};
+    b->blocks = (unsigned)(((uint64_t)n_rows + (two ? 511 : 255)) / (two ? 512 : 256));
+  }
   *bound = b;
   return PGM_OK;
 }
 
 int pgm_rows_bound_run(void *bound) {
-  const RowsBound *b = (const RowsBound *)bound;
+  RowsBound *b = (RowsBound *)bound;
   if (!b) return fail(PGM_EINVAL, "rows_bound_run: null handle");
+  if (b->fn) {
+    void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &b->args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &b->args_size,
+                     HIP_LAUNCH_PARAM_END};
+    HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(b->stream), nullptr, extra));
+    return PGM_OK;
+  }
   return rows_plan_run(b->handle, b->mode, b->codes, b->ld_codes, b->row0, b->n_rows, b->marg, b->joint, b->ld_out,
                        b->map, b->gap, b->err, b->stream, false);
 }

@@ -165,7 +165,7 @@ def test_specialised_kernel_bit_identical(gpu, seed):
         picks = list(rng.choice(names, size=int(rng.integers(6, 13)), replace=False))
         nq = int(rng.integers(1, 3))
         q, e = picks[:nq], picks[nq:]
-        n = 300
+        n = 300 if seed % 2 == 0 else 301
         rows = {v: [onet.states[v][int(rng.integers(0, onet.card[v]))] for _ in range(n)] for v in e}
         df = pd.DataFrame(rows, columns=e)
         col_of = {c: i for i, c in enumerate(e)}
@@ -205,3 +205,37 @@ def test_specialised_kernel_bit_identical(gpu, seed):
             plan.extra_mode = 0
         checked += 1
     assert checked >= 1
+
+
+@pytest.mark.parametrize("rows", [400_000, 400_001])
+def test_specialised_kernel_large_batches(gpu, rows):
+    """Large batches: even row counts take the two-rows-per-thread specialised kernel (16-B stores,
+    2-byte code loads), odd ones the one-row kernel; both bit-identical to k_rows_affine."""
+    import random
+
+    import torch
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    codes, nodes = forward_sample_codes(m, 2000, seed=11)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(np.tile(codes[[pos[v] for v in obs]], (1, rows // 2000 + 1))[:, :rows])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    res = []
+    for extra in (0, N.ROWS_NO_JIT):
+        plan.extra_mode = extra
+        o = plan.alloc_outputs(rows, marginals=True, map_=True, gap=True)
+        plan.run(d, rows, 0, rows, o)
+        res.append(o)
+    plan.extra_mode = 0
+    torch.cuda.synchronize()
+    for k in ("marg", "map", "gap"):
+        assert torch.equal(res[0][k], res[1][k]), k

@@ -83,10 +83,14 @@ def main():
             for _ in range(a.reps):
                 bound.run()
             cpu_us = (_t.perf_counter() - c0) * 1e6 / a.reps  # host cost per launch (GPU may lag behind)
+            c0 = _t.perf_counter()
+            for _ in range(a.reps):
+                N.lib().pgm_version()
+            ctypes_us = (_t.perf_counter() - c0) * 1e6 / a.reps  # bare ctypes call, for comparison
             torch.cuda.synchronize()
             bpr = plan.algorithmic_bytes_per_row(marginals=outs.get("marginals", False), map_=outs.get("map_", False))
             print(json.dumps({"rows": rows, "variant": name, "kernel_us": us, "rows_per_s": rows / us * 1e6,
-                              "GBps": bpr * rows / us / 1e3, "bytes_per_row": bpr, "unbound_us": us_unbound, "host_us_per_launch": cpu_us}),
+                              "GBps": bpr * rows / us / 1e3, "bytes_per_row": bpr, "unbound_us": us_unbound, "host_us_per_launch": cpu_us, "ctypes_call_us": ctypes_us}),
                   flush=True)
         plan.extra_mode = 0
         if a.variants is None or "compact_codes" in a.variants:
