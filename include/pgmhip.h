@@ -128,6 +128,20 @@ typedef struct {
 
 int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream);
 
+/* The same product and, in the same pass, M = reduce(C) over the keep dims with marg_s == 0
+ * (marg_s[i]: stride of keep dim i in M; the last keep dim, the evidence rows, must have stride 1
+ * in C and M).  Batched-BP collect (a clique belief and its message to the parent,
+ * ExactInference.py:784-802) and distribute (beta_c *= sigma'/mu in place, C may alias operand 0,
+ * with the marginal onto a child separator) read each clique once.  reduce: PGM_RED_SUM or
+ * PGM_RED_MAX (max-calibration).  Only shapes with pgm_product_n_marginal_ok() == 1 run fused
+ * (<= 4 operands, rows innermost with an even count >= 64, <= 512 reduced states per kept state,
+ * enough kept states to fill the chip); others return PGM_EINVAL without launching and the caller
+ * runs pgm_product_n + pgm_contract. */
+int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *ops, const double *C,
+                              const int64_t *marg_s, const double *M);
+int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops, double *C,
+                           const int64_t *marg_s, int32_t reduce, double *M, void *stream);
+
 /* ---------------------------------------------------------------- dense pairwise step (FP64 MFMA)
  * C[b, m, n] = sum_k A[b, m, k] * B[b, k, n] where each index is a GROUP of variables laid out in
  * any order inside its tensor: the element offsets come from a DEVICE int64 table,

@@ -148,6 +148,10 @@ _SIGS = {
     "pgm_contract_workspace": ([ctypes.POINTER(ContractDesc), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_product_n": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, _P], ctypes.c_int),
+    "pgm_product_n_marginal_ok": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P,
+                                   ctypes.POINTER(ctypes.c_int64), _P], ctypes.c_int),
+    "pgm_product_n_marginal": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P,
+                                ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, _P, _P], ctypes.c_int),
     "pgm_gemm": ([ctypes.POINTER(GemmDesc), _P, _P, _P, _P], ctypes.c_int),
     "pgm_batch_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_batch_add_contract": ([_P, ctypes.POINTER(ContractDesc), _P, _P, _P], ctypes.c_int),

@@ -801,6 +801,184 @@ __global__ __launch_bounds__(256) void k_productn_rows2(const ProdNK p, double *
   }
 }
 
+// ----------------------------------------------------------------------------- n-ary product + marginal
+// C = prod_i X_i (as pgm_product_n) and, in the same pass, M = SUM/MAX of C over the keep dims M
+// does not have: a batched-BP clique belief written together with its separator message (collect)
+// or updated in place together with the marginal onto its children's separator (distribute), so
+// the belief is not read again.  Rows (the last keep dim) two per lane with 16-B accesses as in
+// k_productn_rows2.  A block owns one kept outer index (separator state); the reduction (the
+// clique's other states) is walked from an LDS offset table with the next entry's operands in
+// flight while the current product is stored and accumulated.
+#define RMAX_MARG 512
+#define MOPS 4
+struct ProdMK {
+  int32_t n_ops, nk, nr, n_red;  // nk: kept outer dims + the row dim (last); nr: reduced dims
+  int32_t kind[MOPS];
+  int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
+  uint32_t n_outer, NP;          // kept outer index space; row pairs
+  FDiv kdiv[KMAX];
+  int64_t ksc[KMAX], ksm[KMAX], ks[MOPS][KMAX];
+  FDiv rdiv[KMAX];
+  int64_t rsc[KMAX], rs[MOPS][KMAX];
+  const double *ops[MOPS];
+};
+
+template <int NOPS>
+__device__ __forceinline__ double prodm_combine(const ProdMK &p, const double (&v)[NOPS]) {
+  double prod = 1.0;
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i) {
+    if (i < p.n_ops) {
+      if (p.kind[i] == PGM_PRODN_MUL) {
+        prod *= v[i];
+      } else if (p.kind[i] == PGM_PRODN_RATIO && i + 1 < NOPS) {
+        const double r = v[i] / v[i + 1];
+        prod *= (r != r) ? 0.0 : r;
+      }
+    }
+  }
+  return prod;
+}
+
+template <int NOPS, int RED>
+__global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *C, double *__restrict__ M) {
+  __shared__ int64_t tc[RMAX_MARG];
+  __shared__ int64_t to[NOPS][RMAX_MARG];
+  const uint32_t NR = p.n_red;
+  for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+    uint32_t idx = j;
+    int64_t oc = 0, oo[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) oo[i] = 0;
+    for (int k = p.nr - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.rdiv[k]);
+      const uint32_t dg = idx - q * p.rdiv[k].d;
+      oc += (int64_t)dg * p.rsc[k];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) oo[i] += (int64_t)dg * p.rs[i][k];
+      idx = q;
+    }
+    tc[j] = oc;
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) to[i][j] = oo[i];
+  }
+  __syncthreads();
+  const int kx = p.nk - 1;
+  const uint32_t xstep = gridDim.x * blockDim.x;
+  for (uint32_t o = blockIdx.y; o < p.n_outer; o += gridDim.y) {
+    int64_t oc = 0, om = 0, off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    uint32_t idx = o;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oc += (int64_t)dg * p.ksc[k];
+      om += (int64_t)dg * p.ksm[k];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      idx = q;
+    }
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < p.NP; x += xstep) {
+      auto load = [&](uint32_t j, double2 (&v)[NOPS]) {
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          const double *b = p.ops[i] + off[i] + to[i][j];
+          if (p.vec[i]) {
+            v[i] = ((const double2 *)b)[x];
+          } else {
+            const double s = b[0];
+            v[i] = make_double2(s, s);
+          }
+        }
+      };
+      double2 acc = make_double2(red_init<RED>(), red_init<RED>());
+      double2 cur[NOPS], nxt[NOPS];
+      load(0, cur);
+      for (uint32_t j = 0; j < NR; ++j) {
+        if (j + 1 < NR) load(j + 1, nxt);  // next entry's operands in flight during this one's store
+        double lo[NOPS], hi[NOPS];
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          lo[i] = cur[i].x;
+          hi[i] = cur[i].y;
+        }
+        const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
+        ((double2 *)(C + oc + tc[j]))[x] = pr;
+        acc.x = red_op<RED>(acc.x, pr.x);
+        acc.y = red_op<RED>(acc.y, pr.y);
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) cur[i] = nxt[i];
+      }
+      ((double2 *)(M + om))[x] = acc;
+    }
+  }
+}
+
+// 1 = the fused kernel applies (k filled), 0 = it does not (use product_n + contract), < 0 error
+static int plan_product_marg(const pgm_productn_desc *d, const double *const *ops, const double *C,
+                             const int64_t *marg_s, const double *M, ProdMK &k, dim3 &grid) {
+  if (!d || !ops || !C || !marg_s || !M) return fail(PGM_EINVAL, "product_n_marginal: null argument");
+  if (d->n_ops < 1 || d->n_ops > PMAX || d->n_keep < 1 || d->n_keep > PGM_MAX_DIMS)
+    return fail(PGM_EINVAL, "product_n_marginal: n_ops %d / n_keep %d out of range", d->n_ops, d->n_keep);
+  if (g_no_rows2 || d->n_ops > MOPS || d->n_keep < 2) return 0;
+  memset(&k, 0, sizeof k);
+  const int last = d->n_keep - 1;
+  const int64_t NX = d->keep_card[last];
+  if (NX < 64 || NX % 2 || d->keep_sc[last] != 1 || marg_s[last] != 1) return 0;
+  if (((uintptr_t)C & 15) || ((uintptr_t)M & 15)) return 0;
+  k.n_ops = d->n_ops;
+  for (int t = 0; t < MOPS; ++t) {
+    const bool real = t < d->n_ops;
+    k.ops[t] = real ? ops[t] : ops[0];
+    k.kind[t] = real ? d->op_kind[t] : PGM_PRODN_MUL;
+    if (real && (!ops[t] || d->op_kind[t] < 0 || d->op_kind[t] > 2))
+      return fail(PGM_EINVAL, "product_n_marginal: operand %d", t);
+    const int64_t sx = real ? d->keep_s[t][last] : 0;
+    if (sx != 0 && sx != 1) return 0;
+    if (sx == 1 && ((uintptr_t)ops[t] & 15)) return 0;
+    k.vec[t] = sx == 1;
+  }
+  uint64_t n_outer = 1, n_red = 1;
+  for (int i = 0; i < last; ++i) {
+    const int64_t c = d->keep_card[i];
+    if (c <= 0) return fail(PGM_EINVAL, "product_n_marginal: keep_card[%d] <= 0", i);
+    if (c == 1) continue;
+    const bool kept = marg_s[i] != 0;
+    if (d->keep_sc[i] % 2 || (kept && marg_s[i] % 2)) return 0;
+    for (int t = 0; t < d->n_ops; ++t)
+      if (k.vec[t] && d->keep_s[t][i] % 2) return 0;
+    if (kept) {
+      if (k.nk >= KMAX - 1) return 0;
+      k.kdiv[k.nk] = make_fdiv((uint32_t)c);
+      k.ksc[k.nk] = d->keep_sc[i];
+      k.ksm[k.nk] = marg_s[i];
+      for (int t = 0; t < d->n_ops; ++t) k.ks[t][k.nk] = d->keep_s[t][i];
+      ++k.nk;
+      n_outer *= (uint64_t)c;
+    } else {
+      if (k.nr >= KMAX) return 0;
+      k.rdiv[k.nr] = make_fdiv((uint32_t)c);
+      k.rsc[k.nr] = d->keep_sc[i];
+      for (int t = 0; t < d->n_ops; ++t) k.rs[t][k.nr] = d->keep_s[t][i];
+      ++k.nr;
+      n_red *= (uint64_t)c;
+    }
+  }
+  if (n_red > RMAX_MARG || n_outer >= (1ull << 31)) return 0;
+  k.kdiv[k.nk] = make_fdiv((uint32_t)NX);  // the row dim, last
+  ++k.nk;
+  k.n_red = (int32_t)n_red;
+  k.n_outer = (uint32_t)n_outer;
+  k.NP = (uint32_t)(NX / 2);
+  const uint64_t xb = (k.NP + 255) / 256;
+  const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
+  const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, 2048 / gy));
+  if (gx * gy < 512) return 0;  // too few blocks to fill the chip: the two-kernel path is faster
+  grid = dim3((unsigned)gx, (unsigned)gy, 1);
+  return 1;
+}
+
 // ----------------------------------------------------------------------------- gather
 struct GatherK {
   int32_t nk, n_ev, batch_dim, _pad;
@@ -2055,6 +2233,37 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
     case 2: hipLaunchKernelGGL((k_productn<2>), grid, dim3(256), 0, s, k, C); break;
     case 4: hipLaunchKernelGGL((k_productn<4>), grid, dim3(256), 0, s, k, C); break;
     default: hipLaunchKernelGGL((k_productn<8>), grid, dim3(256), 0, s, k, C); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *ops, const double *C,
+                              const int64_t *marg_s, const double *M) {
+  ProdMK k;
+  dim3 g;
+  return plan_product_marg(d, ops, C, marg_s, M, k, g) == 1 ? 1 : 0;
+}
+
+int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops, double *C, const int64_t *marg_s,
+                           int32_t reduce, double *M, void *stream) {
+  if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
+    return fail(PGM_EINVAL, "product_n_marginal: reduce must be PGM_RED_SUM or PGM_RED_MAX");
+  ProdMK k;
+  dim3 g;
+  const int r = plan_product_marg(d, ops, C, marg_s, M, k, g);
+  if (r < 0) return r;
+  if (r == 0)
+    return fail(PGM_EINVAL, "product_n_marginal: shape not supported by the fused kernel "
+                            "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
+  hipStream_t s = S(stream);
+  const bool two = k.n_ops <= 2;
+  if (reduce == PGM_RED_SUM) {
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
+  } else {
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
   }
   HIP_TRY(hipGetLastError());
   return PGM_OK;

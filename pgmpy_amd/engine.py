@@ -293,6 +293,34 @@ def product_n(operands, out_labels, out=None, kinds=None):
     return out
 
 
+def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None):
+    """(descriptor, operand pointers, C, marginal strides, M, fused?) for C = product_n(...) and
+    M[marg_labels] = reduce of C over the other labels (pgm_product_n_marginal); marg_labels must
+    be a subset of out_labels.  fused is False when the fused kernel does not apply."""
+    d, ptrs, out = prepare_product_n(operands, out_labels, out, kinds)
+    out_labels, marg_labels = list(out_labels), list(marg_labels)
+    if any(l not in out_labels for l in marg_labels):
+        raise ValueError("marginal labels must be output labels")
+    M = empty([int(out.shape[out_labels.index(l)]) for l in marg_labels])
+    ms = (ctypes.c_int64 * len(out_labels))(*[int(M.stride(marg_labels.index(l))) if l in marg_labels else 0
+                                               for l in out_labels])
+    ok = bool(N.lib().pgm_product_n_marginal_ok(ctypes.byref(d), ptrs, N.ptr(out), ms, N.ptr(M)))
+    return d, ptrs, out, ms, M, ok
+
+
+def product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum"):
+    """C = prod of operands over out_labels and M = reduce(C) onto marg_labels, in one pass when
+    the fused kernel applies (else product_n then contract).  Returns (C, M)."""
+    d, ptrs, out, ms, M, ok = prepare_product_n_marginal(operands, out_labels, marg_labels, out, kinds)
+    L = N.lib()
+    if ok:
+        N.check(L.pgm_product_n_marginal(ctypes.byref(d), ptrs, N.ptr(out), ms, _REDUCE[reduce], N.ptr(M),
+                                         N.stream_handle()), "product_n_marginal")
+        return out, M
+    N.check(L.pgm_product_n(ctypes.byref(d), ptrs, N.ptr(out), N.stream_handle()), "product_n")
+    return out, contract(out, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy", out=M)
+
+
 def copy(A, la=None, out_labels=None):
     la = list(range(A.dim())) if la is None else la
     out_labels = la if out_labels is None else out_labels

@@ -110,6 +110,18 @@ class BPSchedule:
         def scope_size(sc):
             return int(np.prod([size[v] for v in sc])) if sc else 1
 
+        kids = {}
+        for p, c in bjt.order:
+            kids.setdefault(p, []).append(c)
+
+        def largest_kid_scope(c):
+            """The largest separator scope (in c's variable order) of c's children: the marginal of
+            c's final belief the distribute sweep needs first."""
+            lc = bjt.pot[c][1]
+            scs = {tuple(v for v in lc if v in k) for k in kids[c]}
+            return max(scs, key=lambda x: (scope_size(x), len(x)))
+
+        premarg = {}  # clique -> (scope, marginal of its final belief) made in the finalising pass
         # collect: post-order (children before parents)
         post = [c for _, c in reversed(bjt.order)] + [bjt.root]
         for c in post:
@@ -122,16 +134,23 @@ class BPSchedule:
             ops = [(t, ls)] + _aggregate(prog, small, ls, scope_size)
             if len(ops) == 1:
                 ops.append((E.to_device(np.ones(n_rows)), [R]))  # broadcast psi over the rows
-            beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
+            # the belief and its message to the parent (at the root: its largest child-separator
+            # marginal) in one pass over the clique
             if c in parent:
                 sep = [v for v in ls if v in parent[c]]
-                msgs[c] = (prog.contract(beliefs[c][0], ls + [R], None, None, sep + [R], reduce=red,
-                                         combine="copy"), sep + [R])
+                bt, m = prog.product_n_marginal(ops, ls + [R], sep + [R], reduce=red)
+                beliefs[c] = (bt, ls)
+                msgs[c] = (m, sep + [R])
+            elif c in kids:
+                sc = largest_kid_scope(c)
+                bt, m = prog.product_n_marginal(ops, ls + [R], list(sc) + [R], reduce=red)
+                beliefs[c] = (bt, ls)
+                premarg[c] = (sc, m)
+            else:
+                beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
         # distribute: root -> leaves; one sigma per distinct separator scope of a parent, each
-        # marginalised from the smallest already-computed containing scope (or the belief)
-        kids = {}
-        for p, c in bjt.order:
-            kids.setdefault(p, []).append(c)
+        # marginalised from the smallest already-computed containing scope (or the belief); a
+        # child's update beta_c *= sigma / mu also yields its own largest child-separator marginal
         for p in [bjt.root] + [c for _, c in bjt.order]:
             if p not in kids:
                 continue
@@ -140,17 +159,30 @@ class BPSchedule:
             for c in kids[p]:
                 scopes.setdefault(tuple(msgs[c][1][:-1]), []).append(c)
             have = {tuple(lp): tp}
+            if p in premarg:
+                sc0, m0 = premarg[p]
+                have[tuple(sc0)] = m0
             for sc in sorted(scopes, key=lambda x: -scope_size(x)):
-                src = min((h for h in have if set(sc) <= set(h)), key=scope_size)
-                sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
-                                      combine="copy")
-                have[sc] = sigma
+                if sc in have:
+                    sigma = have[sc]
+                else:
+                    src = min((h for h in have if set(sc) <= set(h)), key=scope_size)
+                    sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
+                                          combine="copy")
+                    have[sc] = sigma
                 for c in scopes[sc]:
                     tc, lc = beliefs[c]
                     mu, sl = msgs[c]
-                    # beta_c *= sigma / mu (0/0 -> 0) in one pass
-                    prog.product_n([(tc, lc + [R]), (sigma, sl), (mu, sl)], lc + [R], out=tc,
-                                   kinds=[N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN])
+                    # beta_c *= sigma / mu (0/0 -> 0) in one pass (+ its largest child-scope marginal)
+                    upd = [(tc, lc + [R]), (sigma, sl), (mu, sl)]
+                    kinds = [N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN]
+                    if c in kids:
+                        sc_c = largest_kid_scope(c)
+                        _, m = prog.product_n_marginal(upd, lc + [R], list(sc_c) + [R], out=tc, kinds=kinds,
+                                                       reduce=red)
+                        premarg[c] = (sc_c, m)
+                    else:
+                        prog.product_n(upd, lc + [R], out=tc, kinds=kinds)
                     seps[(p, c)] = (sigma, sl[:-1])
         marg = {}
         if marginals:

@@ -98,6 +98,25 @@ class Program:
                           f"-> {list(out_labels)}{tuple(out.shape)}")
         return out
 
+    def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum"):
+        """Recorded C = product_n(...) with M = reduce(C) onto marg_labels in the same pass
+        (pgm_product_n_marginal) when the fused kernel applies, else product_n + contract.
+        Returns (C, M)."""
+        ops = list(operands)
+        if len(ops) <= 4:
+            d, ptrs, out2, ms, M, ok = E.prepare_product_n_marginal(ops, out_labels, marg_labels, out, kinds)
+            if ok:
+                L = N.lib()
+                self._keep.extend([d, ptrs, out2, ms, M] + [t for t, _ in ops])
+                args = (ctypes.byref(d), ptrs, N.ptr(out2), ms, E._REDUCE[reduce], N.ptr(M))
+                self._steps.append(lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal"))
+                self.notes.append(f"product_n_marginal {[(list(ls), tuple(t.shape)) for t, ls in ops]} "
+                                  f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}")
+                return out2, M
+        C = self.product_n(ops, out_labels, out, kinds)
+        M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")
+        return C, M
+
     def indicator(self, codes_col, card, n_rows, err=None):
         out = E.empty([card, n_rows])
         L = N.lib()

@@ -436,3 +436,72 @@ def test_rows2_product_and_marginal_paths(gpu, rows):
     view.copy_(E.to_device(full))
     got = E.to_host(E.contract(view, list("abcdr"), None, None, ["b", "d", "r"], reduce="sum", combine="copy"))
     np.testing.assert_allclose(got, full.sum(axis=(0, 2)), rtol=1e-13)
+
+
+@pytest.mark.parametrize("rows,red", [(64, "sum"), (200, "sum"), (200, "max"), (201, "sum"), (30, "sum")])
+def test_product_n_marginal_fused(gpu, rows, red):
+    """pgm_product_n_marginal: the clique product and its separator marginal in one pass (fused
+    when rows are innermost with an even count >= 64; product_n + contract otherwise), including
+    the in-place ratio update beta *= sigma / mu (0/0 -> 0) of the distribute sweep."""
+    import torch
+
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    rng = np.random.default_rng(rows)
+    cl = list("abcdef")
+    card = dict(zip(cl, (8, 2, 3, 8, 5, 9)))  # 576 kept states: enough blocks for the fused kernel
+    sh = [card[v] for v in cl]
+    psi = rng.random(sh)
+    msg = rng.random([card["a"], card["c"], card["f"], rows])
+    R = E.ROW
+    fused = E.prepare_product_n_marginal([(E.to_device(psi), cl), (E.to_device(msg), ["a", "c", "f", R])],
+                                         cl + [R], ["a", "d", "f", R])[-1]
+    assert fused == (rows % 2 == 0 and rows >= 64)
+    C, M = E.product_n_marginal([(E.to_device(psi), cl), (E.to_device(msg), ["a", "c", "f", R])], cl + [R],
+                                ["a", "d", "f", R], reduce=red)
+    full = psi[..., None] * msg[:, None, :, None, None, :, :]
+    np.testing.assert_array_equal(E.to_host(C), full)
+    exp = full.sum(axis=(1, 2, 4)) if red == "sum" else full.max(axis=(1, 2, 4))
+    np.testing.assert_allclose(E.to_host(M), exp, rtol=1e-13)
+    # in place: beta *= sigma / mu with zeros, marginal onto (a, d, f)
+    beta = E.to_device(full)
+    sig = rng.random([card["a"], card["d"], card["f"], rows])
+    mu = rng.random([card["a"], card["d"], card["f"], rows])
+    sig[0, 0, 0, :5] = 0.0
+    mu[0, 0, 0, :5] = 0.0
+    C2, M2 = E.product_n_marginal([(beta, cl + [R]), (E.to_device(sig), ["a", "d", "f", R]),
+                                   (E.to_device(mu), ["a", "d", "f", R])], cl + [R], ["a", "d", "f", R], out=beta,
+                                  kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN], reduce=red)
+    assert C2.data_ptr() == beta.data_ptr()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = sig / mu
+    q[np.isnan(q)] = 0
+    upd = full * q[:, None, None, :, None, :, :]
+    np.testing.assert_allclose(E.to_host(beta), upd, rtol=1e-15)
+    exp2 = upd.sum(axis=(1, 2, 4)) if red == "sum" else upd.max(axis=(1, 2, 4))
+    np.testing.assert_allclose(E.to_host(M2), exp2, rtol=1e-13)
+    torch.cuda.synchronize()
+
+
+def test_bp_fused_marginals_many_rows(gpu):
+    """Batched BP with >= 64 evidence rows takes the fused belief + separator-marginal kernels;
+    calibrated beliefs must equal the unfused schedule's (single-row calibrations)."""
+    import pandas as pd
+
+    from pgmpy_amd.inference.bp_batch import BatchedJunctionTree
+    from pgmpy_amd.inference.EliminationOrder import junction_tree_from_model
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import codes_to_frame, forward_sample_codes
+
+    m = get_example_model("pathfinder")
+    bjt = BatchedJunctionTree(junction_tree_from_model(m))
+    leaves = sorted(v for v in m.nodes() if m.out_degree(v) == 0)
+    codes, nodes = forward_sample_codes(m, 128, seed=3)
+    df = codes_to_frame(m, codes, nodes, columns=leaves[:6])
+    cal = bjt.calibrate_frame(df)
+    assert any("product_n_marginal" in n for n in bjt.schedule(128, list(df.columns)).prog.notes)
+    for r in (0, 77, 127):
+        one = bjt.calibrate_frame(df.iloc[[r, r]].reset_index(drop=True))  # 2 rows: unfused kernels
+        for c in bjt.cliques:
+            np.testing.assert_allclose(cal.clique_belief(c, r), one.clique_belief(c, 0), rtol=1e-11, atol=1e-300)
