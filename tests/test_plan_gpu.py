@@ -239,3 +239,34 @@ def test_specialised_kernel_large_batches(gpu, rows):
     torch.cuda.synchronize()
     for k in ("marg", "map", "gap"):
         assert torch.equal(res[0][k], res[1][k]), k
+
+
+@pytest.mark.parametrize("row0,n", [(0, 1), (37, 1), (5, 255), (1000, 257), (2, 400_000), (3, 400_000)])
+def test_specialised_kernel_row_windows(gpu, row0, n):
+    """Rows [row0, row0 + n) of a wider code matrix (ld > n): single rows, ragged counts, odd and even
+    offsets (the two-rows kernel needs an even row0) give what a contiguous copy of the window gives."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    codes, nodes = forward_sample_codes(m, 3000, seed=21)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ld = row0 + n + 3
+    ev = np.ascontiguousarray(np.tile(codes[[pos[v] for v in obs]], (1, ld // 3000 + 1))[:, :ld])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    full = upload_codes(ev)
+    win = upload_codes(np.ascontiguousarray(ev[:, row0:row0 + n]))
+    a = plan.alloc_outputs(n, marginals=True, map_=True)
+    b = plan.alloc_outputs(n, marginals=True, map_=True)
+    plan.run(full, ld, row0, n, a)
+    plan.run(win, n, 0, n, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a["marg"], b["marg"]) and torch.equal(a["map"], b["map"])
