@@ -229,6 +229,9 @@ int pgm_batch_create(void **handle);
 int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const double *A, const double *B, double *C);
 int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
                          int32_t *err_flag);
+/* an n-ary product job (pgm_product_n's descriptor and checks; flat mode): batched BP runs every
+ * small clique / separator product of one dependency level of the calibration as one launch */
+int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const double *const *ops, double *C);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
 int pgm_batch_destroy(void *handle);

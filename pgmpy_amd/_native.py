@@ -156,6 +156,7 @@ _SIGS = {
     "pgm_batch_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_batch_add_contract": ([_P, ctypes.POINTER(ContractDesc), _P, _P, _P], ctypes.c_int),
     "pgm_batch_add_gather": ([_P, ctypes.POINTER(GatherDesc), _P, _P, _P, _P], ctypes.c_int),
+    "pgm_batch_add_product_n": ([_P, ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P], ctypes.c_int),
     "pgm_batch_finalize": ([_P], ctypes.c_int),
     "pgm_batch_run": ([_P, _P], ctypes.c_int),
     "pgm_batch_destroy": ([_P], ctypes.c_int),

@@ -669,6 +669,31 @@ __device__ __forceinline__ double prodn_combine(const ProdNK &p, const double (&
   return prod;
 }
 
+// flat mode: every output decoded on its own (grid-stride over tid / nthreads); also the body of a
+// batched product_n job (k_batch)
+template <int NOPS>
+__device__ __forceinline__ void prodn_flat(const ProdNK &p, double *__restrict__ C, uint64_t tid, uint64_t nthreads) {
+  for (uint64_t out = tid; out < p.n_out; out += nthreads) {
+    uint32_t idx = (uint32_t)out;
+    int64_t off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    int64_t oc = 0;
+    for (int k = p.nk - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = q;
+    }
+    double v[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) v[i] = p.ops[i][off[i]];
+    C[oc] = prodn_combine<NOPS>(p, v);
+  }
+}
+
 template <int NOPS>
 __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__restrict__ C) {
   if (p.row_mode) {
@@ -717,26 +742,7 @@ __global__ __launch_bounds__(256) void k_productn(const ProdNK p, double *__rest
     }
     return;
   }
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t out = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; out < p.n_out; out += stride) {
-    uint32_t idx = (uint32_t)out;
-    int64_t off[NOPS];
-#pragma unroll
-    for (int i = 0; i < NOPS; ++i) off[i] = 0;
-    int64_t oc = 0;
-    for (int k = p.nk - 1; k >= 0; --k) {
-      const uint32_t q = fdiv(idx, p.kdiv[k]);
-      const uint32_t dg = idx - q * p.kdiv[k].d;
-#pragma unroll
-      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
-      oc += (int64_t)dg * p.ksc[k];
-      idx = q;
-    }
-    double v[NOPS];
-#pragma unroll
-    for (int i = 0; i < NOPS; ++i) v[i] = p.ops[i][off[i]];
-    C[oc] = prodn_combine<NOPS>(p, v);
-  }
+  prodn_flat<NOPS>(p, C, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
 }
 
 // Row mode, two rows per lane (16-B loads/stores; the 8-B form runs at 0.54-0.70x the 16-B rate on
@@ -840,7 +846,9 @@ __device__ __forceinline__ double prodm_combine(const ProdMK &p, const double (&
   return prod;
 }
 
-template <int NOPS, int RED>
+// U == 1: the next entry's operands in flight while the current one is stored; U > 1: U entries'
+// operands loaded together (U x NOPS 16-B loads in flight per lane), then U products stored
+template <int NOPS, int RED, int U>
 __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *C, double *__restrict__ M) {
   __shared__ int64_t tc[RMAX_MARG];
   __shared__ int64_t to[NOPS][RMAX_MARG];
@@ -893,6 +901,30 @@ __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *
         }
       };
       double2 acc = make_double2(red_init<RED>(), red_init<RED>());
+      if constexpr (U > 1) {
+        for (uint32_t j0 = 0; j0 < NR; j0 += U) {
+          double2 v[U][NOPS];
+#pragma unroll
+          for (int u = 0; u < U; ++u) load(j0 + u < NR ? j0 + u : NR - 1, v[u]);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (j0 + u < NR) {
+              double lo[NOPS], hi[NOPS];
+#pragma unroll
+              for (int i = 0; i < NOPS; ++i) {
+                lo[i] = v[u][i].x;
+                hi[i] = v[u][i].y;
+              }
+              const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
+              ((double2 *)(C + oc + tc[j0 + u]))[x] = pr;
+              acc.x = red_op<RED>(acc.x, pr.x);
+              acc.y = red_op<RED>(acc.y, pr.y);
+            }
+          }
+        }
+        ((double2 *)(M + om))[x] = acc;
+        continue;
+      }
       double2 cur[NOPS], nxt[NOPS];
       load(0, cur);
       for (uint32_t j = 0; j < NR; ++j) {
@@ -973,7 +1005,9 @@ static int plan_product_marg(const pgm_productn_desc *d, const double *const *op
   k.NP = (uint32_t)(NX / 2);
   const uint64_t xb = (k.NP + 255) / 256;
   const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
-  const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, 2048 / gy));
+  // target block count (tuning knob PGM_MARG_BLOCKS)
+  static const uint64_t target = getenv("PGM_MARG_BLOCKS") ? strtoull(getenv("PGM_MARG_BLOCKS"), nullptr, 10) : 2048;
+  const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, target / gy));
   if (gx * gy < 512) return 0;  // too few blocks to fill the chip: the two-kernel path is faster
   grid = dim3((unsigned)gx, (unsigned)gy, 1);
   return 1;
@@ -1028,7 +1062,7 @@ __global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *_
 // level of a compiled contraction path (all steps whose inputs are ready) is one launch instead
 // of one launch per step.
 struct BatchJob {
-  int32_t kind, cmb, red, _pad;  // kind 0: contraction, 1: gather
+  int32_t kind, cmb, red, _pad;  // kind 0: contraction, 1: gather, 2: n-ary product
   uint32_t block0, nblocks;
   const double *A, *B;
   double *C;
@@ -1036,6 +1070,7 @@ struct BatchJob {
   int32_t *err;
   ContractK c;
   GatherK g;
+  ProdNK pn;
 };
 
 template <int CMB>
@@ -1055,6 +1090,12 @@ __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs
   const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
   if (J.kind == 1) {
     gather_body(J.g, J.A, J.codes, J.C, J.err, tid, n);
+    return;
+  }
+  if (J.kind == 2) {
+    if (J.pn.n_ops <= 2) prodn_flat<2>(J.pn, J.C, tid, n);
+    else if (J.pn.n_ops <= 4) prodn_flat<4>(J.pn, J.C, tid, n);
+    else prodn_flat<PMAX>(J.pn, J.C, tid, n);
     return;
   }
   switch (J.cmb) {
@@ -2140,8 +2181,12 @@ int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, d
   return PGM_OK;
 }
 
-int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream) {
-  if (!d || !ops || !C) return fail(PGM_EINVAL, "product_n: null argument");
+}  // extern "C"
+
+// descriptor -> kernel parameters (coalesced dims, aliased unused operand slots); shared by
+// pgm_product_n and the batched product_n job
+static int plan_prodn(const pgm_productn_desc *d, const double *const *ops, ProdNK &k) {
+  if (!d || !ops) return fail(PGM_EINVAL, "product_n: null argument");
   if (d->n_ops < 1 || d->n_ops > PMAX || d->n_keep < 0 || d->n_keep > PGM_MAX_DIMS)
     return fail(PGM_EINVAL, "product_n: n_ops %d (1..%d) / n_keep %d", d->n_ops, PMAX, d->n_keep);
   // coalesce: one Dims per group of up to 3 operand strides is not enough -> do it by hand
@@ -2169,7 +2214,6 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
   }
   if (n_out >= (1ull << 31)) return fail(PGM_EINVAL, "product_n: output too large");
   if (n > KMAX) return fail(PGM_EINVAL, "product_n: %d dims after coalescing (limit %d)", n, KMAX);
-  ProdNK k;
   memset(&k, 0, sizeof k);
   k.n_ops = d->n_ops;
   k.nk = n;
@@ -2196,13 +2240,27 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
   }
   const uint64_t NX = n > 0 ? (uint64_t)card[n - 1] : 1;
   k.row_mode = (n > 0 && NX >= 64) ? 1 : 0;
+  return PGM_OK;
+}
+
+extern "C" {
+
+int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream) {
+  if (!d || !ops || !C) return fail(PGM_EINVAL, "product_n: null argument");
+  ProdNK k;
+  const int prc = plan_prodn(d, ops, k);
+  if (prc != PGM_OK) return prc;
+  const int n = k.nk;
+  const uint64_t n_out = k.n_out;
+  const uint64_t NX = n > 0 ? (uint64_t)k.kdiv[n - 1].d : 1;
+  const int64_t *sc = k.ksc;
   // two rows per lane when every access is 16-B aligned (batched BP: rows innermost, even count)
   bool rows2 = k.row_mode && (NX % 2 == 0) && sc[n - 1] == 1 && ((uintptr_t)C & 15) == 0 && !g_no_rows2;
   for (int i = 0; rows2 && i < n - 1; ++i) rows2 = (sc[i] % 2) == 0;
   for (int t = 0; rows2 && t < d->n_ops; ++t) {
-    const int64_t sx = so[t][n - 1];
+    const int64_t sx = k.ks[t][n - 1];
     rows2 = sx == 0 || (sx == 1 && ((uintptr_t)ops[t] & 15) == 0);
-    for (int i = 0; rows2 && sx == 1 && i < n - 1; ++i) rows2 = (so[t][i] % 2) == 0;
+    for (int i = 0; rows2 && sx == 1 && i < n - 1; ++i) rows2 = (k.ks[t][i] % 2) == 0;
   }
   dim3 grid;
   if (rows2) {
@@ -2258,13 +2316,24 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
                             "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
   hipStream_t s = S(stream);
   const bool two = k.n_ops <= 2;
-  if (reduce == PGM_RED_SUM) {
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
-  } else {
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
+  // entries per load batch (tuning knob PGM_MARG_U: 1 = one-ahead prefetch, 2, 4)
+  static const int U = getenv("PGM_MARG_U") ? atoi(getenv("PGM_MARG_U")) : 1;
+#define PGM_MARG_LAUNCH(UU)                                                                             \
+  if (reduce == PGM_RED_SUM) {                                                                          \
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM, UU>), g, dim3(256), 0, s, k, C, M);    \
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM, UU>), g, dim3(256), 0, s, k, C, M);     \
+  } else {                                                                                              \
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX, UU>), g, dim3(256), 0, s, k, C, M);    \
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX, UU>), g, dim3(256), 0, s, k, C, M);     \
   }
+  if (U >= 4) {
+    PGM_MARG_LAUNCH(4)
+  } else if (U == 2) {
+    PGM_MARG_LAUNCH(2)
+  } else {
+    PGM_MARG_LAUNCH(1)
+  }
+#undef PGM_MARG_LAUNCH
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }
@@ -2418,6 +2487,19 @@ int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A
   J.codes = codes;
   J.err = err_flag;
   return batch_append(h, J, J.g.n_out);
+}
+
+int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const double *const *ops, double *C) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !C) return fail(PGM_EINVAL, "batch_add_product_n: null argument");
+  BatchJob J;
+  memset(&J, 0, sizeof J);
+  int rc = plan_prodn(d, ops, J.pn);
+  if (rc != PGM_OK) return rc;
+  if (J.pn.n_out == 0) return PGM_OK;
+  J.kind = 2;
+  J.C = C;
+  return batch_append(h, J, J.pn.n_out);
 }
 
 int pgm_batch_finalize(void *handle) {

@@ -17,6 +17,8 @@ columns) is a pgmpy_amd.program.Program: all buffers preallocated, replayed as
 one HIP graph.  Algorithmic bytes per calibration: 8 (4 sum|C| + 4 sum|S|)
 (SURVEY.md §8(d)).
 """
+import os
+
 import numpy as np
 
 from .. import _native as N
@@ -84,7 +86,7 @@ def _aggregate(prog, small, clique_labels, scope_size):
 class BPSchedule:
     """A compiled batched calibration for fixed (n_rows, evidence columns, operation)."""
 
-    def __init__(self, bjt, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True):
+    def __init__(self, bjt, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True, levels=True):
         import torch
 
         self.bjt = bjt
@@ -92,7 +94,11 @@ class BPSchedule:
         self.ev_vars = list(ev_vars)
         red = "sum" if operation == "marginalize" else "max"
         R = E.ROW
-        prog = Program()
+        # levelled: independent cliques' small products / separator marginals share one launch per
+        # dependency level (collect: tree height; distribute: depth)
+        if os.environ.get("PGM_BP_LEVELS") == "0":  # A/B knob: one launch per step
+            levels = False
+        prog = Program(levels=levels)
         dev = E.device()
         self.codes = torch.empty((max(1, len(self.ev_vars)), n_rows), dtype=torch.uint8, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)

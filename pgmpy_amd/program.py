@@ -7,6 +7,7 @@ them into a HIP graph (pgm_graph_capture_*) so a whole compiled schedule — a
 batched BP calibration, a fixed-shape contraction plan — is one launch.
 """
 import ctypes
+import os
 
 from . import _native as N
 from . import engine as E
@@ -14,6 +15,26 @@ from . import engine as E
 
 BATCH_MAX_WORK = 1 << 22  # index-space size (outputs x reduction) up to which a step joins a batch
 BATCH_SPLIT_WORK = 1 << 16  # a step the planner would split (few outputs, long reduction) joins only this small
+# outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
+# their own row-mode launch (16-B two-rows-per-lane).  Tuning knob: PGM_PRODN_BATCH_MAX.
+PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
+
+
+def _key(t):
+    """Hazard identity of a device tensor: its storage (views of one buffer conflict)."""
+    return t.untyped_storage().data_ptr()
+
+
+class _Rec:
+    """One recorded launch of a levelled Program: plain launch, optional batch job, buffers it
+    reads / writes (storage keys)."""
+
+    __slots__ = ("fn", "note", "job", "reads", "writes", "level")
+
+    def __init__(self, fn, note, job, reads, writes):
+        self.fn, self.note, self.job = fn, note, job
+        self.reads, self.writes = reads, writes
+        self.level = 0
 
 
 class _Batch:
@@ -24,7 +45,16 @@ class _Batch:
 
 
 class Program:
-    def __init__(self):
+    """levels=True: launches are recorded with the buffers they read and write and, before the first
+    run / capture, grouped into dependency levels (a step's level is one past every earlier step it
+    must follow: read-after-write, write-after-read, write-after-write).  Each level is its big steps'
+    own launches plus ONE pgm_batch launch of all its small jobs (contractions, gathers, n-ary
+    products): a batched BP sweep becomes ~2 launches per tree level instead of ~4 per clique."""
+
+    def __init__(self, levels=False):
+        self._levels = levels
+        self._recs = []
+        self._lowered = False
         self._steps = []
         self._keep = []
         self._graph = None
@@ -66,11 +96,85 @@ class Program:
         self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
         self.notes.append(f"batch of {len(b.jobs)}")
 
+    # ------------------------------------------------------------------ levelled recording
+    def _emit(self, fn, note, reads, writes, job=None):
+        """Append one launch (plain `fn(stream)`), or record it for levelling."""
+        if self._levels:
+            if self._lowered:
+                raise RuntimeError("levelled Program: no recording after the first run / capture")
+            rk = [k for k in (_key(t) for t in reads if t is not None) if k]
+            wk = [k for k in (_key(t) for t in writes if t is not None) if k]
+            self._recs.append(_Rec(fn, note, job, rk, wk))
+        else:
+            self._steps.append(fn)
+            self.notes.append(note)
+
+    def _lower(self):
+        """Levelled Program -> steps: per level, its unbatched launches then one batch launch."""
+        if not self._levels or self._lowered:
+            return
+        self._lowered = True
+        last_w, last_r = {}, {}
+        n_lv = 0
+        for r in self._recs:
+            lv = 0
+            for k in r.reads:
+                lv = max(lv, last_w.get(k, -1) + 1)
+            for k in r.writes:
+                lv = max(lv, last_w.get(k, -1) + 1, last_r.get(k, -1) + 1)
+            r.level = lv
+            n_lv = max(n_lv, lv + 1)
+            for k in r.reads:
+                last_r[k] = max(last_r.get(k, -1), lv)
+            for k in r.writes:
+                last_w[k] = max(last_w.get(k, -1), lv)
+        by_level = [[] for _ in range(n_lv)]
+        for r in self._recs:
+            by_level[r.level].append(r)
+        for recs in by_level:
+            small = [r for r in recs if r.job is not None]
+            for r in recs:
+                if r.job is None or len(small) == 1:
+                    self._steps.append(r.fn)
+                    self.notes.append(r.note)
+            if len(small) < 2:
+                continue
+            L = N.lib()
+            h = ctypes.c_void_p()
+            N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
+            self._handles.append(h)
+            for r in small:
+                kind, args = r.job
+                if kind == "contract":
+                    N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
+                elif kind == "gather":
+                    N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
+                else:
+                    N.check(L.pgm_batch_add_product_n(h, *args), "batch_add_product_n")
+            N.check(L.pgm_batch_finalize(h), "batch_finalize")
+            self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+            self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
+
+    @property
+    def n_levels(self):
+        self._lower()
+        return 1 + max((r.level for r in self._recs), default=-1)
+
     # ------------------------------------------------------------------ recording
     def contract(self, A, la, B, lb, out_labels, reduce=None, combine="mul", out=None):
         d, out, ws, wsb = E.prepare_contract(A, la, B, lb, out_labels, reduce, combine, out)
         self._keep.extend([d, A, B, out, ws])
         L = N.lib()
+        if self._levels:
+            w = _work(d)
+            args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
+            job = None
+            if w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
+                job = ("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)))
+            self._emit(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"),
+                       f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}",
+                       [A, B], [out, ws], job)
+            return out
         w = _work(d) if self._batch is not None else 0
         if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
             self._batch.jobs.append(("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)),
@@ -93,9 +197,10 @@ class Program:
         d, ptrs, out = E.prepare_product_n(ops, out_labels, out, kinds)
         self._keep.extend([d, ptrs, out] + [t for t, _ in ops])
         args = (ctypes.byref(d), ptrs, N.ptr(out))
-        self._steps.append(lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n"))
-        self.notes.append(f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
-                          f"-> {list(out_labels)}{tuple(out.shape)}")
+        job = ("product_n", args) if out.numel() <= PRODN_BATCH_MAX else None
+        self._emit(lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n"),
+                   f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
+                   f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job)
         return out
 
     def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum"):
@@ -109,9 +214,10 @@ class Program:
                 L = N.lib()
                 self._keep.extend([d, ptrs, out2, ms, M] + [t for t, _ in ops])
                 args = (ctypes.byref(d), ptrs, N.ptr(out2), ms, E._REDUCE[reduce], N.ptr(M))
-                self._steps.append(lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal"))
-                self.notes.append(f"product_n_marginal {[(list(ls), tuple(t.shape)) for t, ls in ops]} "
-                                  f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}")
+                self._emit(lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal"),
+                           f"product_n_marginal {[(list(ls), tuple(t.shape)) for t, ls in ops]} "
+                           f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}",
+                           [t for t, _ in ops], [out2, M])
                 return out2, M
         C = self.product_n(ops, out_labels, out, kinds)
         M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")
@@ -123,8 +229,9 @@ class Program:
         args = (N.ptr(codes_col), int(n_rows), int(card), N.ptr(out), int(out.stride(0)), int(out.stride(1)),
                 N.ptr(err))
         self._keep.extend([codes_col, out, err])
-        self._steps.append(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"))
-        self.notes.append(f"indicator card {card}")
+        # err is an atomic OR flag: not a hazard
+        self._emit(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"), f"indicator card {card}",
+                   [codes_col], [out])
         return out
 
     def gather(self, A, la, evidence, out_labels, codes, ld, row0, n_rows, err=None):
@@ -132,6 +239,10 @@ class Program:
         L = N.lib()
         args = (ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err))
         self._keep.extend([d, A, codes, out, err])
+        if self._levels:
+            self._emit(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"), f"gather {list(la)} -> {list(out_labels)}",
+                       [A, codes], [out], ("gather", args) if out.numel() <= BATCH_MAX_WORK else None)
+            return out
         if self._batch is not None and out.numel() <= BATCH_MAX_WORK:
             self._batch.jobs.append(("gather", args, args))
             return out
@@ -145,21 +256,21 @@ class Program:
         L = N.lib()
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C))
         self._keep.extend([d, table, A, B, C])
-        self._steps.append(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"))
-        self.notes.append(f"gemm b{d.batch} m{d.m} n{d.n} k{d.k}")
+        self._emit(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"), f"gemm b{d.batch} m{d.m} n{d.n} k{d.k}",
+                   [A, B], [C])
         return C
 
     def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):
         L = N.lib()
         args = (N.ptr(X), int(n_rows), int(row_len), int(s_row), int(s_elem), None, N.ptr(out32))
         self._keep.extend([X, out32])
-        self._steps.append(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"))
-        self.notes.append("argmax")
+        self._emit(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"), "argmax", [X], [out32])
 
     def time_steps(self, reps=3):
         """[(us, note)] per recorded step, each replayed alone (profiling aid; not graph-replayed)."""
         import ctypes as C
 
+        self._lower()
         L = N.lib()
         s = N.stream_handle()
         a, b = C.c_void_p(), C.c_void_p()
@@ -181,6 +292,7 @@ class Program:
 
     # ------------------------------------------------------------------ execution
     def run(self, stream=None):
+        self._lower()
         s = N.stream_handle(stream)
         if self._graph is not None:
             N.check(N.lib().pgm_graph_launch(self._graph, s), "graph_launch")
@@ -194,6 +306,7 @@ class Program:
 
         if self._graph is not None:
             return
+        self._lower()
         L = N.lib()
         self._stream = torch.cuda.Stream()
         torch.cuda.current_stream().synchronize()
@@ -208,6 +321,7 @@ class Program:
         self._graph = g
 
     def __len__(self):
+        self._lower()
         return len(self._steps)
 
     def __del__(self):

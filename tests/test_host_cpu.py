@@ -172,3 +172,30 @@ def test_specialised_row_kernel_source_compiles_for_gfx950():
                             "--cuda-device-only", "-c", path, "-o", os.path.join(d, "k.o")],
                            capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
+
+
+def test_program_dependency_levels():
+    """Levelled Program (pgmpy_amd/program.py): RAW, WAR and WAW hazards order steps into levels;
+    independent steps share a level; views of one buffer conflict.  No launches (host only)."""
+    import torch
+
+    from pgmpy_amd.program import Program
+
+    a, b, c, d = (torch.zeros(8) for _ in range(4))
+    prog = Program(levels=True)
+    ran = []
+
+    def step(name):
+        return lambda s: ran.append(name)
+
+    prog._emit(step("w_a"), "w_a", [d], [a])            # L0
+    prog._emit(step("w_b"), "w_b", [d], [b])            # L0 (independent)
+    prog._emit(step("r_ab_w_c"), "r_ab_w_c", [a, b], [c])  # L1 (RAW on a, b)
+    prog._emit(step("w_d"), "w_d", [], [d])             # L1 (WAR on d, read at L0)
+    prog._emit(step("inplace_c"), "inplace_c", [c, a[2:]], [c])  # L2 (RAW/WAW on c)
+    prog._emit(step("w_a_view"), "w_a_view", [], [a[:4]])  # L3 (WAR: a read at L2 through a view)
+    assert prog.n_levels == 4
+    assert [r.level for r in prog._recs] == [0, 0, 1, 1, 2, 3]
+    for f in prog._steps:
+        f(None)
+    assert ran == ["w_a", "w_b", "r_ab_w_c", "w_d", "inplace_c", "w_a_view"]

@@ -71,6 +71,19 @@ def main():
       2 * nbytes)
     t("marginal to sep (copy/sum)", ct(full, cl + [Rl], sep + [Rl]), nbytes)
 
+    def pm(ops, marg, kinds=None, o=None):  # fused product + marginal
+        import ctypes
+
+        d, ptrs, o2, ms, M, ok = E.prepare_product_n_marginal(ops, cl + [Rl], marg + [Rl], o, kinds)
+        assert ok
+        return lambda: N.check(L.pgm_product_n_marginal(ctypes.byref(d), ptrs, N.ptr(o2), ms, E._REDUCE["sum"], N.ptr(M),
+                                                        N.stream_handle()))
+
+    t("fused psi x msg + marg to msg scope (collect)", pm([(psi, cl), (msg, msg_l + [Rl]), (ones, [Rl])], msg_l),
+      nbytes)
+    t("fused update in place + marg to sep", pm([(full, cl + [Rl]), (sig, sep + [Rl]), (mu, sep + [Rl])], sep,
+                                              [N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN], full), 2 * nbytes)
+
 
 if __name__ == "__main__":
     main()
