@@ -644,6 +644,7 @@ struct ProdNK {
   int32_t n_ops, nk;
   int32_t kind[PMAX];
   uint32_t n_out, row_mode;
+  uint32_t pairs, _pad;  // batched jobs: two innermost elements per lane with 16-B accesses
   FDiv kdiv[KMAX];
   int64_t ksc[KMAX];
   int64_t ks[PMAX][KMAX];
@@ -691,6 +692,45 @@ __device__ __forceinline__ void prodn_flat(const ProdNK &p, double *__restrict__
 #pragma unroll
     for (int i = 0; i < NOPS; ++i) v[i] = p.ops[i][off[i]];
     C[oc] = prodn_combine<NOPS>(p, v);
+  }
+}
+
+// flat mode over element PAIRS along the innermost dim (host-checked: even innermost card, output
+// innermost stride 1, every operand's innermost stride 0 or 1, all other strides of 16-B accessed
+// arrays even, bases 16-B aligned): 16-B loads/stores for batched jobs
+template <int NOPS>
+__device__ __forceinline__ void prodn_flat2(const ProdNK &p, double *__restrict__ C, uint64_t tid, uint64_t nthreads) {
+  const int kx = p.nk - 1;
+  bool vec[NOPS];
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i) vec[i] = p.ks[i][kx] != 0;
+  const uint32_t n_pairs = p.n_out >> 1;
+  for (uint64_t q = tid; q < n_pairs; q += nthreads) {
+    uint32_t idx = (uint32_t)q << 1;
+    int64_t off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    int64_t oc = 0;
+    for (int k = kx; k >= 0; --k) {
+      const uint32_t qq = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - qq * p.kdiv[k].d;
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = qq;
+    }
+    double lo[NOPS], hi[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) {
+      if (vec[i]) {
+        const double2 w = *(const double2 *)(p.ops[i] + off[i]);
+        lo[i] = w.x;
+        hi[i] = w.y;
+      } else {
+        lo[i] = hi[i] = p.ops[i][off[i]];
+      }
+    }
+    *(double2 *)(C + oc) = make_double2(prodn_combine<NOPS>(p, lo), prodn_combine<NOPS>(p, hi));
   }
 }
 
@@ -821,6 +861,7 @@ struct ProdMK {
   int32_t n_ops, nk, nr, n_red;  // nk: kept outer dims + the row dim (last); nr: reduced dims
   int32_t kind[MOPS];
   int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
+  int32_t jvar[MOPS];            // operand varies over the reduced entries (else loaded once per outer)
   uint32_t n_outer, NP;          // kept outer index space; row pairs
   FDiv kdiv[KMAX];
   int64_t ksc[KMAX], ksm[KMAX], ks[MOPS][KMAX];
@@ -947,6 +988,111 @@ __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *
   }
 }
 
+// j-outer form: for each reduced entry j the block sweeps its x range (XI row pairs per lane,
+// x = x0 + i*256), so every store instruction of the block lands in one contiguous run of the
+// belief and XI x NOPS 16-B operand loads are in flight per lane; the marginal stays in XI
+// register accumulators until the last j.  Block = (kept outer index, 256*XI row pairs).
+template <int NOPS, int RED, int XI>
+__global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double *C, double *__restrict__ M) {
+  __shared__ int64_t tc[RMAX_MARG];
+  __shared__ int64_t to[NOPS][RMAX_MARG];
+  const uint32_t NR = p.n_red;
+  for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
+    uint32_t idx = j;
+    int64_t oc = 0, oo[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) oo[i] = 0;
+    for (int k = p.nr - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.rdiv[k]);
+      const uint32_t dg = idx - q * p.rdiv[k].d;
+      oc += (int64_t)dg * p.rsc[k];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) oo[i] += (int64_t)dg * p.rs[i][k];
+      idx = q;
+    }
+    tc[j] = oc;
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) to[i][j] = oo[i];
+  }
+  __syncthreads();
+  const int kx = p.nk - 1;
+  for (uint32_t o = blockIdx.y; o < p.n_outer; o += gridDim.y) {
+    int64_t oc = 0, om = 0, off[NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) off[i] = 0;
+    uint32_t idx = o;
+    for (int k = kx - 1; k >= 0; --k) {
+      const uint32_t q = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - q * p.kdiv[k].d;
+      oc += (int64_t)dg * p.ksc[k];
+      om += (int64_t)dg * p.ksm[k];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
+      idx = q;
+    }
+    const uint32_t x0 = blockIdx.x * (256u * XI) + threadIdx.x;
+    uint32_t xs[XI];
+#pragma unroll
+    for (int u = 0; u < XI; ++u) {
+      const uint32_t x = x0 + 256u * u;
+      xs[u] = x < p.NP ? x : p.NP - 1;
+    }
+    double2 acc[XI];
+#pragma unroll
+    for (int u = 0; u < XI; ++u) acc[u] = make_double2(red_init<RED>(), red_init<RED>());
+    // operands that do not vary over the reduced entries: loaded once per outer index
+    double2 h[XI][NOPS];
+#pragma unroll
+    for (int i = 0; i < NOPS; ++i) {
+      if (p.jvar[i]) continue;
+      const double *b = p.ops[i] + off[i];
+      if (p.vec[i]) {
+#pragma unroll
+        for (int u = 0; u < XI; ++u) h[u][i] = ((const double2 *)b)[xs[u]];
+      } else {
+        const double sv = b[0];
+#pragma unroll
+        for (int u = 0; u < XI; ++u) h[u][i] = make_double2(sv, sv);
+      }
+    }
+    for (uint32_t j = 0; j < NR; ++j) {
+      double2 v[XI][NOPS];
+#pragma unroll
+      for (int i = 0; i < NOPS; ++i) {
+        const double *b = p.ops[i] + off[i] + to[i][j];
+        if (!p.jvar[i]) {
+#pragma unroll
+          for (int u = 0; u < XI; ++u) v[u][i] = h[u][i];
+        } else if (p.vec[i]) {
+#pragma unroll
+          for (int u = 0; u < XI; ++u) v[u][i] = ((const double2 *)b)[xs[u]];
+        } else {
+          const double sv = b[0];
+#pragma unroll
+          for (int u = 0; u < XI; ++u) v[u][i] = make_double2(sv, sv);
+        }
+      }
+      double2 *cj = (double2 *)(C + oc + tc[j]);
+#pragma unroll
+      for (int u = 0; u < XI; ++u) {
+        double lo[NOPS], hi[NOPS];
+#pragma unroll
+        for (int i = 0; i < NOPS; ++i) {
+          lo[i] = v[u][i].x;
+          hi[i] = v[u][i].y;
+        }
+        const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
+        if (x0 + 256u * u < p.NP) cj[x0 + 256u * u] = pr;
+        acc[u].x = red_op<RED>(acc[u].x, pr.x);
+        acc[u].y = red_op<RED>(acc[u].y, pr.y);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < XI; ++u)
+      if (x0 + 256u * u < p.NP) ((double2 *)(M + om))[x0 + 256u * u] = acc[u];
+  }
+}
+
 // 1 = the fused kernel applies (k filled), 0 = it does not (use product_n + contract), < 0 error
 static int plan_product_marg(const pgm_productn_desc *d, const double *const *ops, const double *C,
                              const int64_t *marg_s, const double *M, ProdMK &k, dim3 &grid) {
@@ -998,6 +1144,10 @@ static int plan_product_marg(const pgm_productn_desc *d, const double *const *op
     }
   }
   if (n_red > RMAX_MARG || n_outer >= (1ull << 31)) return 0;
+  for (int t = 0; t < MOPS; ++t) {
+    k.jvar[t] = 0;
+    for (int r = 0; t < d->n_ops && r < k.nr; ++r) k.jvar[t] |= k.rs[t][r] != 0;
+  }
   k.kdiv[k.nk] = make_fdiv((uint32_t)NX);  // the row dim, last
   ++k.nk;
   k.n_red = (int32_t)n_red;
@@ -1093,6 +1243,12 @@ __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs
     return;
   }
   if (J.kind == 2) {
+    if (J.pn.pairs) {
+      if (J.pn.n_ops <= 2) prodn_flat2<2>(J.pn, J.C, tid, n);
+      else if (J.pn.n_ops <= 4) prodn_flat2<4>(J.pn, J.C, tid, n);
+      else prodn_flat2<PMAX>(J.pn, J.C, tid, n);
+      return;
+    }
     if (J.pn.n_ops <= 2) prodn_flat<2>(J.pn, J.C, tid, n);
     else if (J.pn.n_ops <= 4) prodn_flat<4>(J.pn, J.C, tid, n);
     else prodn_flat<PMAX>(J.pn, J.C, tid, n);
@@ -1869,21 +2025,32 @@ static void appendf(std::string &o, const char *fmt, ...) {
   o += buf;
 }
 
+// workgroup size of the specialised row kernel (tuning knob PGM_ROWS_JIT_WG: 64, 128 or 256 rows)
+static int jit_wg() {
+  static const int wg = [] {
+    const char *e = getenv("PGM_ROWS_JIT_WG");
+    const int v = e ? atoi(e) : 256;
+    return (v == 64 || v == 128) ? v : 256;
+  }();
+  return wg;
+}
+
 // R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
 static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
   const bool lds = NV * 8 <= 48 * 1024;
-  appendf(o, "extern \"C\" __global__ void __launch_bounds__(256) pgm_rows_jit%s(const double *__restrict__ V, "
+  const int WG = jit_wg();
+  appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_jit%s(const double *__restrict__ V, "
              "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
              "double *__restrict__ M, long long ldo, int *__restrict__ MP, double *__restrict__ G, "
-             "int *__restrict__ E, int mode) {\n", R == 2 ? "2" : "");
+             "int *__restrict__ E, int mode) {\n", WG, R == 2 ? "2" : "");
   o += "  const int t = threadIdx.x;\n";
-  appendf(o, "  const long long r = ((long long)blockIdx.x * 256 + t) * %d;\n", R);
+  appendf(o, "  const long long r = ((long long)blockIdx.x * %d + t) * %d;\n", WG, R);
   appendf(o, "  const long long rc = r < n ? r : n - %d;\n", R);
-  const int K = (NV + 255) / 256;
+  const int K = (NV + WG - 1) / WG;
   if (lds) {
-    appendf(o, "  __shared__ double S[%d];\n", K * 256);
-    for (int i = 0; i < K; ++i) appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, 256 * i, NV, 256 * i, NV - 1);
+    appendf(o, "  __shared__ double S[%d];\n", K * WG);
+    for (int i = 0; i < K; ++i) appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
   }
   std::vector<int> cols;  // distinct evidence columns, each loaded once per row
   for (int j = 0; j < pl->n_ev; ++j)
@@ -1898,7 +2065,7 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
     }
   }
   if (lds) {
-    for (int i = 0; i < K; ++i) appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", 256 * i, NV, 256 * i, NV - 1, i);
+    for (int i = 0; i < K; ++i) appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
     o += "  __syncthreads();\n#define VAL(i) S[i]\n";
   } else {
     o += "#define VAL(i) V[i]\n";
@@ -2318,6 +2485,33 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
   const bool two = k.n_ops <= 2;
   // entries per load batch (tuning knob PGM_MARG_U: 1 = one-ahead prefetch, 2, 4)
   static const int U = getenv("PGM_MARG_U") ? atoi(getenv("PGM_MARG_U")) : 1;
+  // j-outer form (tuning knob PGM_MARG_JX = row pairs per lane: 1, 2 or 4; 0 = the j-inner kernel)
+  // default (-1): j-outer with 2 row pairs per lane from 1,024 row pairs up, else 1 (MI355X, pathfinder's
+  // largest clique: collect 413 -> 272 us at 4,000 rows, 94 -> 80 us at 1,000)
+  static const int JX = getenv("PGM_MARG_JX") ? atoi(getenv("PGM_MARG_JX")) : -1;
+  if (JX != 0) {
+    const int XI = JX < 0 ? (k.NP >= 1024 ? 2 : 1) : JX >= 4 ? 4 : JX == 2 ? 2 : 1;
+    const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
+    const dim3 gj((unsigned)gxj, g.y, 1);
+#define PGM_MARGJ_LAUNCH(XX)                                                                                 \
+  if (reduce == PGM_RED_SUM) {                                                                               \
+    if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);      \
+    else hipLaunchKernelGGL((k_productn_marg_jx<MOPS, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);       \
+  } else {                                                                                                   \
+    if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);      \
+    else hipLaunchKernelGGL((k_productn_marg_jx<MOPS, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);       \
+  }
+    if (XI == 4) {
+      PGM_MARGJ_LAUNCH(4)
+    } else if (XI == 2) {
+      PGM_MARGJ_LAUNCH(2)
+    } else {
+      PGM_MARGJ_LAUNCH(1)
+    }
+#undef PGM_MARGJ_LAUNCH
+    HIP_TRY(hipGetLastError());
+    return PGM_OK;
+  }
 #define PGM_MARG_LAUNCH(UU)                                                                             \
   if (reduce == PGM_RED_SUM) {                                                                          \
     if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM, UU>), g, dim3(256), 0, s, k, C, M);    \
@@ -2499,7 +2693,18 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
   if (J.pn.n_out == 0) return PGM_OK;
   J.kind = 2;
   J.C = C;
-  return batch_append(h, J, J.pn.n_out);
+  // pairs: 16-B accesses when every access along the innermost dim is aligned and unit/zero stride
+  ProdNK &k = J.pn;
+  const int kx = k.nk - 1;
+  bool pairs = kx >= 0 && k.kdiv[kx].d % 2 == 0 && k.ksc[kx] == 1 && ((uintptr_t)C & 15) == 0 && !g_no_rows2;
+  for (int i = 0; pairs && i < kx; ++i) pairs = k.ksc[i] % 2 == 0;
+  for (int t = 0; pairs && t < k.n_ops; ++t) {
+    const int64_t sx = k.ks[t][kx];
+    pairs = sx == 0 || (sx == 1 && ((uintptr_t)k.ops[t] & 15) == 0);
+    for (int i = 0; pairs && sx == 1 && i < kx; ++i) pairs = k.ks[t][i] % 2 == 0;
+  }
+  k.pairs = pairs ? 1u : 0u;
+  return batch_append(h, J, pairs ? k.n_out / 2 : k.n_out);
 }
 
 int pgm_batch_finalize(void *handle) {
@@ -2907,7 +3112,8 @@ static int rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64
   if (!(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP)) &&
       rows_jit_ready(h)) {
     const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap);
-    const uint64_t jblocks = ((uint64_t)n_rows + (two ? 511 : 255)) / (two ? 512 : 256);
+    const uint64_t rpb = (uint64_t)jit_wg() * (two ? 2 : 1);  // rows per block
+    const uint64_t jblocks = ((uint64_t)n_rows + rpb - 1) / rpb;
     if (jblocks > 0x7fffffffull) return fail(PGM_EINVAL, "rows_plan_run: too many rows");
     if (dry) return PGM_OK;
     const uint8_t *cp = codes;
@@ -2916,7 +3122,8 @@ static int rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64
     int32_t *mp = map, *ef = err_flag;
     int32_t md = mode;
     void *args[] = {(void *)&v, (void *)&cp, &ldc, &r0, &nr, (void *)&mg, &ldo, (void *)&mp, (void *)&gp, (void *)&ef, &md};
-    HIP_TRY(hipModuleLaunchKernel(two ? h->jit_fn2 : h->jit_fn, (unsigned)jblocks, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+    HIP_TRY(hipModuleLaunchKernel(two ? h->jit_fn2 : h->jit_fn, (unsigned)jblocks, 1, 1, (unsigned)jit_wg(), 1, 1, 0, s,
+                                  args, nullptr));
     return PGM_OK;
   }
   if (h->all_affine && !(mode & PGM_ROWS_JOINT) && !(mode & PGM_ROWS_GENERIC)) {
@@ -3025,7 +3232,8 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
     const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap);
     b->fn = two ? h->jit_fn2 : h->jit_fn;
     b->args = RowsJitArgs{h->d_values, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, err_flag, mode, 0};
-    b->blocks = (unsigned)(((uint64_t)n_rows + (two ? 511 : 255)) / (two ? 512 : 256));
+    const uint64_t rpb = (uint64_t)jit_wg() * (two ? 2 : 1);
+    b->blocks = (unsigned)(((uint64_t)n_rows + rpb - 1) / rpb);
   }
   *bound = b;
   return PGM_OK;
@@ -3037,7 +3245,7 @@ int pgm_rows_bound_run(void *bound) {
   if (b->fn) {
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &b->args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &b->args_size,
                      HIP_LAUNCH_PARAM_END};
-    HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(b->stream), nullptr, extra));
+    HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, (unsigned)jit_wg(), 1, 1, 0, S(b->stream), nullptr, extra));
     return PGM_OK;
   }
   return rows_plan_run(b->handle, b->mode, b->codes, b->ld_codes, b->row0, b->n_rows, b->marg, b->joint, b->ld_out,

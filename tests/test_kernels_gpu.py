@@ -534,9 +534,13 @@ def test_batch_product_n_jobs(gpu):
     prog.product_n([(x, ["a", "r"]), (nn, ["a", "r"]), (dd, ["a", "r"])], ["a", "r"], out=x,
                    kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN])
     o3 = prog.product_n([(o1, ["y", "x", "r"]), (c, ["x"])], ["x", "y", "r"])  # depends on o1: next level
+    # odd innermost extent: the 8-B flat form (the others run two elements per lane, 16-B)
+    e_ = rng.random((3, 7))
+    o4 = prog.product_n([(E.to_device(e_), ["x", "q"]), (c, ["x"])], ["x", "q"])
     assert prog.n_levels == 2
-    assert len(prog) == 2 and prog.notes[0].startswith("level batch of 2")
+    assert len(prog) == 2 and prog.notes[0].startswith("level batch of 3")
     prog.run()
+    np.testing.assert_array_equal(E.to_host(o4), e_ * E.to_host(c)[:, None])
     np.testing.assert_array_equal(E.to_host(o1), ref1)
     np.testing.assert_array_equal(E.to_host(x), ref2)
     np.testing.assert_array_equal(E.to_host(o3), np.transpose(ref1, (1, 0, 2)) * E.to_host(c)[:, None, None])
