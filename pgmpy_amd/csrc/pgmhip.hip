@@ -862,6 +862,7 @@ struct ProdMK {
   int32_t kind[MOPS];
   int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
   int32_t jvar[MOPS];            // operand varies over the reduced entries (else loaded once per outer)
+  uint32_t xcd, _pad;            // j-outer kernel: consecutive logical blocks on one XCD (grid % 8 == 0)
   uint32_t n_outer, NP;          // kept outer index space; row pairs
   FDiv kdiv[KMAX];
   int64_t ksc[KMAX], ksm[KMAX], ks[MOPS][KMAX];
@@ -1016,7 +1017,16 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
   }
   __syncthreads();
   const int kx = p.nk - 1;
-  for (uint32_t o = blockIdx.y; o < p.n_outer; o += gridDim.y) {
+  // dispatch sends block b to XCD b % 8: give each XCD a contiguous range of logical blocks, so
+  // blocks sharing broadcast operand rows (neighbouring kept indices) share that XCD's L2
+  uint32_t bx = blockIdx.x, by = blockIdx.y;
+  if (p.xcd) {
+    const uint32_t nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t L = (b & 7u) * (nb >> 3) + (b >> 3);
+    bx = L % gridDim.x;
+    by = L / gridDim.x;
+  }
+  for (uint32_t o = by; o < p.n_outer; o += gridDim.y) {
     int64_t oc = 0, om = 0, off[NOPS];
 #pragma unroll
     for (int i = 0; i < NOPS; ++i) off[i] = 0;
@@ -1030,7 +1040,7 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
       for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
       idx = q;
     }
-    const uint32_t x0 = blockIdx.x * (256u * XI) + threadIdx.x;
+    const uint32_t x0 = bx * (256u * XI) + threadIdx.x;
     uint32_t xs[XI];
 #pragma unroll
     for (int u = 0; u < XI; ++u) {
@@ -2493,6 +2503,8 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     const int XI = JX < 0 ? (k.NP >= 1024 ? 2 : 1) : JX >= 4 ? 4 : JX == 2 ? 2 : 1;
     const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
     const dim3 gj((unsigned)gxj, g.y, 1);
+    static const bool xcd = getenv("PGM_MARG_XCD") && atoi(getenv("PGM_MARG_XCD")) > 0;  // tuning knob
+    k.xcd = (xcd && g.y == k.n_outer && (gxj * g.y) % 8 == 0) ? 1u : 0u;
 #define PGM_MARGJ_LAUNCH(XX)                                                                                 \
   if (reduce == PGM_RED_SUM) {                                                                               \
     if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);      \
