@@ -158,6 +158,10 @@ typedef struct {
   int64_t batch, m, n, k;
   const int64_t *offsets; /* device, 3*batch + 2*m + 2*k + 2*n entries */
   int64_t stride[9];      /* per table part: >= 0 -> offset = index * stride (table not read), -1 -> table */
+  int32_t lane_order;     /* hint for table groups: bit 0 = consecutive m are adjacent in A, bit 1 = consecutive
+                             k are adjacent in B (tile loads then run along that axis); strided groups are
+                             detected from the strides */
+  int32_t _pad;
 } pgm_gemm_desc;
 
 int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream);

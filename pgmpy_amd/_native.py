@@ -80,7 +80,8 @@ class ProductNDesc(ctypes.Structure):
 
 class GemmDesc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int64), ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("k", ctypes.c_int64),
-                ("offsets", ctypes.c_void_p), ("stride", ctypes.c_int64 * 9)]
+                ("offsets", ctypes.c_void_p), ("stride", ctypes.c_int64 * 9), ("lane_order", ctypes.c_int32),
+                ("_pad", ctypes.c_int32)]
 
 
 class GatherDesc(ctypes.Structure):

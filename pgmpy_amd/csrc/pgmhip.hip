@@ -1347,6 +1347,7 @@ struct GemmK {
   const int64_t *a_b, *b_b, *c_b, *a_m, *c_m, *a_k, *b_k, *b_n, *c_n;
   int64_t s_ab, s_bb, s_cb, s_am, s_cm, s_ak, s_bk, s_bn, s_cn;  // >= 0: strided group, -1: table
   uint32_t tiles_n;
+  uint32_t a_mfast, b_kfast;  // tile-load lane order: A along m (else k), B along k (else n) — the unit-stride axis
 };
 // offset of index i of a group: the table (TAB) or a single stride (the group collapses)
 template <bool TAB>
@@ -1370,36 +1371,53 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   const int64_t b = blockIdx.y;
   const double *Ab = A + goff<TA>(p.s_ab, p.a_b, b);
   const double *Bb = B + goff<TB>(p.s_bb, p.b_b, b);
-  // this thread's fixed tile rows (A: 4 m rows, k = tid & 15) and columns (B: 4 k rows, n = tid & 63)
-  int64_t arow[4];
-  bool aok[4];
+  // this thread's 4 tile elements per operand and k tile, lanes along the operand's unit-stride axis:
+  // A k-fast (m = tid/16 + 16i, k = tid%16) or m-fast (m = tid%64, k = tid/64 + 4i);
+  // B n-fast (k = tid/64 + 4i, n = tid%64) or k-fast (k = tid%16, n = tid/16 + 16i)
+  const bool amf = p.a_mfast, bkf = p.b_kfast;
+  int am[4], ak[4], bk[4], bn[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t gm = m0 + ((tid + 256 * i) >> 4);
+    am[i] = amf ? (tid & 63) : (tid >> 4) + 16 * i;
+    ak[i] = amf ? (tid >> 6) + 4 * i : (tid & 15);
+    bk[i] = bkf ? (tid & 15) : (tid >> 6) + 4 * i;
+    bn[i] = bkf ? (tid >> 4) + 16 * i : (tid & 63);
+  }
+  int64_t arow[4], bcol[4];
+  bool aok[4], bok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t gm = m0 + am[i];
     aok[i] = gm < p.M;
     arow[i] = aok[i] ? goff<TA>(p.s_am, p.a_m, gm) : 0;
+    const int64_t gn = n0 + bn[i];
+    bok[i] = gn < p.N;
+    bcol[i] = bok[i] ? goff<TB>(p.s_bn, p.b_n, gn) : 0;
   }
-  const int64_t gn = n0 + (tid & 63);
-  const bool bok = gn < p.N;
-  const int64_t bcol = bok ? goff<TB>(p.s_bn, p.b_n, gn) : 0;
   double ra[4], rb[4];
-  // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
-  auto load = [&](int64_t k0) {
-    const int64_t gka = k0 + (tid & 15);
-    const bool ka = gka < p.K;
-    const int64_t oka = goff<TA>(p.s_ak, p.a_k, ka ? gka : p.K - 1);
-    double va[4], vb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) va[i] = Ab[arow[i] + oka];
+  // k offsets (table reads for table groups) are fetched one k tile ahead of the loads that use
+  // them, so a table lookup never sits in series with its data load
+  int64_t oa[4], ob[4];
+  auto offs = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t gkb = k0 + ((tid + 256 * i) >> 6);
-      vb[i] = Bb[goff<TB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1) + bcol];
+      const int64_t gka = k0 + ak[i], gkb = k0 + bk[i];
+      oa[i] = goff<TA>(p.s_ak, p.a_k, gka < p.K ? gka : p.K - 1);
+      ob[i] = goff<TB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1);
+    }
+  };
+  // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
+  auto load = [&](int64_t k0) {
+    double va[4], vb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      va[i] = Ab[arow[i] + oa[i]];
+      vb[i] = Bb[ob[i] + bcol[i]];
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ra[i] = (aok[i] && ka) ? va[i] : 0.0;
-      rb[i] = (bok && k0 + ((tid + 256 * i) >> 6) < p.K) ? vb[i] : 0.0;
+      ra[i] = (aok[i] && k0 + ak[i] < p.K) ? va[i] : 0.0;
+      rb[i] = (bok[i] && k0 + bk[i] < p.K) ? vb[i] : 0.0;
     }
   };
   d4 acc[2][2];
@@ -1407,14 +1425,19 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  offs(0);
   load(0);
+  offs(BK);
   for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) As[tid & 15][(tid + 256 * i) >> 4] = ra[i];
+    for (int i = 0; i < 4; ++i) As[ak[i]][am[i]] = ra[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Bs[(tid + 256 * i) >> 6][tid & 63] = rb[i];
+    for (int i = 0; i < 4; ++i) Bs[bk[i]][bn[i]] = rb[i];
     __syncthreads();
-    if (k0 + BK < p.K) load(k0 + BK);  // in flight during this tile's MFMAs
+    if (k0 + BK < p.K) {  // in flight during this tile's MFMAs
+      load(k0 + BK);
+      offs(k0 + 2 * BK);
+    }
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int kq = 4 * s + (lane >> 4);
@@ -2818,6 +2841,13 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
   if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
+  // tile-load lane order along each operand's unit-stride axis (knob PGM_GEMM_FIXED_ORDER: k-fast A,
+  // n-fast B always, the original mapping)
+  static const bool fixed_order = getenv("PGM_GEMM_FIXED_ORDER") != nullptr;
+  const bool am_unit = d->stride[3] == 1 || (d->stride[3] < 0 && (d->lane_order & 1));
+  const bool bk_unit = d->stride[6] == 1 || (d->stride[6] < 0 && (d->lane_order & 2));
+  k.a_mfast = (!fixed_order && am_unit && d->stride[5] != 1) ? 1u : 0u;
+  k.b_kfast = (!fixed_order && bk_unit && d->stride[7] != 1) ? 1u : 0u;
   const bool ta = d->stride[0] < 0 || d->stride[3] < 0 || d->stride[5] < 0;
   const bool tb = d->stride[1] < 0 || d->stride[6] < 0 || d->stride[7] < 0;
   const bool tc = d->stride[2] < 0 || d->stride[4] < 0 || d->stride[8] < 0;

@@ -221,7 +221,26 @@ def prepare_gemm(A, la, B, lb, keep, shape):
     for i, l in enumerate(lb):
         if card.setdefault(l, int(B.shape[i])) != int(B.shape[i]):
             raise ValueError(f"cardinality mismatch for {l!r}")
-    batch, Ms, Ns, Ks = shape
+    batch, Ms, Ns, Ks = list(shape[0]), list(shape[1]), list(shape[2]), list(shape[3])
+    # tile loads run along each operand's innermost (unit-stride) variable when it is the last of
+    # its group: A along m (lane_order bit 0) or k, B along k (bit 1) or n.  The k enumeration order
+    # is shared by A and B, so when only B is k-innermost its innermost variable goes last.
+    def unit_label(T, ls):  # the variable stored with stride 1 (None if none)
+        u = [l for i, l in enumerate(ls) if T.stride(i) == 1 and T.shape[i] > 1]
+        return u[0] if u else None
+
+    def last(g, l):
+        return [x for x in g if x != l] + [l]
+
+    ia, ib = unit_label(A, la), unit_label(B, lb)
+    if ia is not None and ia in Ks:
+        Ks = last(Ks, ia)
+    elif ib is not None and ib in Ks:
+        Ks = last(Ks, ib)
+    if ia is not None and ia in Ms and keep[-1] not in Ms:  # (C's innermost variable keeps its order)
+        Ms = last(Ms, ia)
+    lane_order = (1 if (ia is not None and Ms and Ms[-1] == ia) else 0) | \
+        (2 if (ib is not None and Ks and Ks[-1] == ib) else 0)
     C = empty([card[l] for l in keep])
     parts = [_group_offsets(A, la, batch, card), _group_offsets(B, lb, batch, card), _group_offsets(C, keep, batch, card),
              _group_offsets(A, la, Ms, card), _group_offsets(C, keep, Ms, card),
@@ -233,6 +252,7 @@ def prepare_gemm(A, la, B, lb, keep, shape):
     d.offsets = table.data_ptr()
     for i, (_, st) in enumerate(parts):
         d.stride[i] = st
+    d.lane_order = lane_order
     return d, table, C
 
 

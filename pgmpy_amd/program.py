@@ -256,8 +256,17 @@ class Program:
         L = N.lib()
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(C))
         self._keep.extend([d, table, A, B, C])
-        self._emit(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"), f"gemm b{d.batch} m{d.m} n{d.n} k{d.k}",
-                   [A, B], [C])
+        groups = dict(zip(("b", "m", "n", "k"), shape))
+
+        def unit_group(T, ls):  # which group holds the operand's stride-1 variable (layout note)
+            for i, l in enumerate(ls):
+                if T.stride(i) == 1 and T.shape[i] > 1:
+                    return next((g for g, gl in groups.items() if l in gl), "?") + f"({T.shape[i]})"
+            return "-"
+
+        self._emit(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"),
+                   f"gemm b{d.batch} m{d.m} n{d.n} k{d.k} unit A:{unit_group(A, la)} B:{unit_group(B, lb)} "
+                   f"lane_order {d.lane_order} strides(ab,bb,cb,am,cm,ak,bk,bn,cn)={list(d.stride)}", [A, B], [C])
         return C
 
     def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):

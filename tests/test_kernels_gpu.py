@@ -302,6 +302,20 @@ def test_pair_gemm_matches_einsum(gpu, shape):
                                rtol=1e-12, atol=1e-12)
 
 
+def test_pair_gemm_unit_stride_lane_orders(gpu):
+    """pgm_gemm tile loads follow each operand's unit-stride axis: A stored m-innermost (m-fast
+    lanes), B stored k-innermost (k-fast lanes), ragged tile edges, a batch group."""
+    from pgmpy_amd import engine as E
+
+    rng = np.random.default_rng(12)
+    A = rng.random((3, 37, 100))  # [b, k, m]
+    B = rng.random((3, 70, 37))   # [b, n, k]
+    C = E.pair_gemm(E.to_device(A), ["b", "k", "m"], E.to_device(B), ["b", "n", "k"], ["b", "m", "n"], force=True)
+    assert C is not None
+    ref = np.einsum("bkm,bnk->bmn", A, B)
+    np.testing.assert_allclose(E.to_host(C), ref, rtol=1e-12, atol=1e-12)
+
+
 def test_pair_gemm_declines_non_gemm_steps(gpu):
     from pgmpy_amd import engine as E
 
