@@ -1356,83 +1356,100 @@ __device__ __forceinline__ int64_t goff(int64_t s, const int64_t *tab, int64_t i
   else return i * s;
 }
 
-// TA / TB / TC: operand A, B, C addressed through its offset tables (some group does not collapse)
-template <bool TA, bool TB, bool TC>
+// TA / TB / TC: operand A, B, C addressed through its offset tables (some group does not collapse).
+// BM x BN block tile, 4 waves in a WY x WX grid, each wave FM x FN 16x16 f64 MFMA tiles; BK = 16.
+// Tiles: 64x64 (2x2 waves of 32x32), 16x128 for M <= 16 (1x4 waves of 16x32: no MFMA rows wasted on
+// a 16-row step), 128x64 for 64 < M <= 128 (2x2 waves of 64x32: B read once per batch, not twice).
+template <int BM, int BN, bool TA, bool TB, bool TC>
 __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *__restrict__ A,
                                                   const double *__restrict__ B, double *__restrict__ C) {
-  constexpr int BM = 64, BN = 64, BK = 16;
+  constexpr int BK = 16;
+  constexpr int WY = BM >= 32 ? 2 : 1, WX = 4 / WY;
+  constexpr int FM = BM / 16 / WY, FN = BN / 16 / WX;
+  constexpr int NA = BM * BK / 256, NB = BN * BK / 256;  // tile elements per thread per k tile
+  static_assert(FM >= 1 && FN >= 1 && NA >= 1 && NB >= 1, "tile shape");
   __shared__ double As[BK][BM + 2];
   __shared__ double Bs[BK][BN + 2];
   typedef double d4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wy = wave >> 1, wx = wave & 1;
+  const int wy = wave / WX, wx = wave % WX;
   const uint32_t t = blockIdx.x;  // n fastest within an m row of tiles (A rows stay hot in L2)
   const int64_t n0 = (int64_t)(t % p.tiles_n) * BN, m0 = (int64_t)(t / p.tiles_n) * BM;
   const int64_t b = blockIdx.y;
   const double *Ab = A + goff<TA>(p.s_ab, p.a_b, b);
   const double *Bb = B + goff<TB>(p.s_bb, p.b_b, b);
-  // this thread's 4 tile elements per operand and k tile, lanes along the operand's unit-stride axis:
-  // A k-fast (m = tid/16 + 16i, k = tid%16) or m-fast (m = tid%64, k = tid/64 + 4i);
-  // B n-fast (k = tid/64 + 4i, n = tid%64) or k-fast (k = tid%16, n = tid/16 + 16i)
+  // this thread's tile elements per operand and k tile (e = tid + 256 i), lanes along the operand's
+  // unit-stride axis: A k-fast (k = e % 16, m = e / 16) or m-fast (m = e % BM, k = e / BM);
+  // B n-fast (n = e % BN, k = e / BN) or k-fast (k = e % 16, n = e / 16)
   const bool amf = p.a_mfast, bkf = p.b_kfast;
-  int am[4], ak[4], bk[4], bn[4];
+  int am[NA], ak[NA], bk[NB], bn[NB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    am[i] = amf ? (tid & 63) : (tid >> 4) + 16 * i;
-    ak[i] = amf ? (tid >> 6) + 4 * i : (tid & 15);
-    bk[i] = bkf ? (tid & 15) : (tid >> 6) + 4 * i;
-    bn[i] = bkf ? (tid >> 4) + 16 * i : (tid & 63);
+  for (int i = 0; i < NA; ++i) {
+    const int e = tid + 256 * i;
+    am[i] = amf ? (e % BM) : (e >> 4);
+    ak[i] = amf ? (e / BM) : (e & 15);
   }
-  int64_t arow[4], bcol[4];
-  bool aok[4], bok[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NB; ++i) {
+    const int e = tid + 256 * i;
+    bk[i] = bkf ? (e & 15) : (e / BN);
+    bn[i] = bkf ? (e >> 4) : (e % BN);
+  }
+  int64_t arow[NA], bcol[NB];
+  bool aok[NA], bok[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
     const int64_t gm = m0 + am[i];
     aok[i] = gm < p.M;
     arow[i] = aok[i] ? goff<TA>(p.s_am, p.a_m, gm) : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
     const int64_t gn = n0 + bn[i];
     bok[i] = gn < p.N;
     bcol[i] = bok[i] ? goff<TB>(p.s_bn, p.b_n, gn) : 0;
   }
-  double ra[4], rb[4];
+  double ra[NA], rb[NB];
   // k offsets (table reads for table groups) are fetched one k tile ahead of the loads that use
   // them, so a table lookup never sits in series with its data load
-  int64_t oa[4], ob[4];
+  int64_t oa[NA], ob[NB];
   auto offs = [&](int64_t k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t gka = k0 + ak[i], gkb = k0 + bk[i];
+    for (int i = 0; i < NA; ++i) {
+      const int64_t gka = k0 + ak[i];
       oa[i] = goff<TA>(p.s_ak, p.a_k, gka < p.K ? gka : p.K - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int64_t gkb = k0 + bk[i];
       ob[i] = goff<TB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1);
     }
   };
   // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
   auto load = [&](int64_t k0) {
-    double va[4], vb[4];
+    double va[NA], vb[NB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      va[i] = Ab[arow[i] + oa[i]];
-      vb[i] = Bb[ob[i] + bcol[i]];
-    }
+    for (int i = 0; i < NA; ++i) va[i] = Ab[arow[i] + oa[i]];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i] = (aok[i] && k0 + ak[i] < p.K) ? va[i] : 0.0;
-      rb[i] = (bok[i] && k0 + bk[i] < p.K) ? vb[i] : 0.0;
-    }
+    for (int i = 0; i < NB; ++i) vb[i] = Bb[ob[i] + bcol[i]];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = (aok[i] && k0 + ak[i] < p.K) ? va[i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = (bok[i] && k0 + bk[i] < p.K) ? vb[i] : 0.0;
   };
-  d4 acc[2][2];
+  d4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < FN; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   offs(0);
   load(0);
   offs(BK);
   for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) As[ak[i]][am[i]] = ra[i];
+    for (int i = 0; i < NA; ++i) As[ak[i]][am[i]] = ra[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Bs[bk[i]][bn[i]] = rb[i];
+    for (int i = 0; i < NB; ++i) Bs[bk[i]][bn[i]] = rb[i];
     __syncthreads();
     if (k0 + BK < p.K) {  // in flight during this tile's MFMAs
       load(k0 + BK);
@@ -1441,28 +1458,46 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int kq = 4 * s + (lane >> 4);
-      const double a0 = As[kq][32 * wy + (lane & 15)], a1 = As[kq][32 * wy + 16 + (lane & 15)];
-      const double b0 = Bs[kq][32 * wx + (lane & 15)], b1 = Bs[kq][32 * wx + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      double av[FM], bv[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[i] = As[kq][(wy * FM + i) * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[j] = Bs[kq][(wx * FN + j) * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
   double *Cb = C + goff<TC>(p.s_cb, p.c_b, b);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t cn = n0 + 32 * wx + 16 * j + (lane & 15);
+  for (int j = 0; j < FN; ++j) {
+    const int64_t cn = n0 + (wx * FN + j) * 16 + (lane & 15);
     if (cn >= p.N) continue;
     const int64_t ocn = goff<TC>(p.s_cn, p.c_n, cn);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t cm = m0 + 32 * wy + 16 * i + (lane >> 4) + 4 * r;
+        const int64_t cm = m0 + (wy * FM + i) * 16 + (lane >> 4) + 4 * r;
         if (cm < p.M) Cb[goff<TC>(p.s_cm, p.c_m, cm) + ocn] = acc[i][j][r];
       }
+  }
+}
+
+template <int BM, int BN>
+static void launch_gemm(int tabs, dim3 g, hipStream_t s, const GemmK &k, const double *A, const double *B, double *C) {
+  const dim3 b(256);
+  switch (tabs) {
+    case 0: hipLaunchKernelGGL((k_gemm_f64<BM, BN, false, false, false>), g, b, 0, s, k, A, B, C); break;
+    case 1: hipLaunchKernelGGL((k_gemm_f64<BM, BN, false, false, true>), g, b, 0, s, k, A, B, C); break;
+    case 2: hipLaunchKernelGGL((k_gemm_f64<BM, BN, false, true, false>), g, b, 0, s, k, A, B, C); break;
+    case 3: hipLaunchKernelGGL((k_gemm_f64<BM, BN, false, true, true>), g, b, 0, s, k, A, B, C); break;
+    case 4: hipLaunchKernelGGL((k_gemm_f64<BM, BN, true, false, false>), g, b, 0, s, k, A, B, C); break;
+    case 5: hipLaunchKernelGGL((k_gemm_f64<BM, BN, true, false, true>), g, b, 0, s, k, A, B, C); break;
+    case 6: hipLaunchKernelGGL((k_gemm_f64<BM, BN, true, true, false>), g, b, 0, s, k, A, B, C); break;
+    default: hipLaunchKernelGGL((k_gemm_f64<BM, BN, true, true, true>), g, b, 0, s, k, A, B, C); break;
   }
 }
 
@@ -2837,7 +2872,14 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   k.s_bk = d->stride[6];
   k.s_bn = d->stride[7];
   k.s_cn = d->stride[8];
-  const uint64_t tn = ((uint64_t)d->n + 63) / 64, tm = ((uint64_t)d->m + 63) / 64;
+  // block tile by M (knob PGM_GEMM_TILE=64: always 64x64)
+  static const bool tile64 = getenv("PGM_GEMM_TILE") && atoi(getenv("PGM_GEMM_TILE")) == 64;
+  // 128-row tile only while it still gives >= 4 blocks per CU (it halves the blocks of a 65..128-row
+  // step; it pays when B is large and would be read twice: C2's 500 x (100 x 576 x 125) step 495 -> 396 us)
+  const bool tall_ok = d->m > 64 && d->m <= 128 && (uint64_t)d->batch * (((uint64_t)d->n + 63) / 64) >= 1024;
+  const int cfg = tile64 ? 0 : d->m <= 16 ? 1 : tall_ok ? 2 : 0;
+  const uint64_t BM = cfg == 1 ? 16 : cfg == 2 ? 128 : 64, BN = cfg == 1 ? 128 : 64;
+  const uint64_t tn = ((uint64_t)d->n + BN - 1) / BN, tm = ((uint64_t)d->m + BM - 1) / BM;
   if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
   if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
@@ -2851,18 +2893,12 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   const bool ta = d->stride[0] < 0 || d->stride[3] < 0 || d->stride[5] < 0;
   const bool tb = d->stride[1] < 0 || d->stride[6] < 0 || d->stride[7] < 0;
   const bool tc = d->stride[2] < 0 || d->stride[4] < 0 || d->stride[8] < 0;
-  const dim3 g((unsigned)(tn * tm), (unsigned)d->batch), b(256);
+  const int tabs = (ta ? 4 : 0) | (tb ? 2 : 0) | (tc ? 1 : 0);
+  const dim3 g((unsigned)(tn * tm), (unsigned)d->batch);
   hipStream_t s = S(stream);
-  switch ((ta ? 4 : 0) | (tb ? 2 : 0) | (tc ? 1 : 0)) {
-    case 0: hipLaunchKernelGGL((k_gemm_f64<false, false, false>), g, b, 0, s, k, A, B, C); break;
-    case 1: hipLaunchKernelGGL((k_gemm_f64<false, false, true>), g, b, 0, s, k, A, B, C); break;
-    case 2: hipLaunchKernelGGL((k_gemm_f64<false, true, false>), g, b, 0, s, k, A, B, C); break;
-    case 3: hipLaunchKernelGGL((k_gemm_f64<false, true, true>), g, b, 0, s, k, A, B, C); break;
-    case 4: hipLaunchKernelGGL((k_gemm_f64<true, false, false>), g, b, 0, s, k, A, B, C); break;
-    case 5: hipLaunchKernelGGL((k_gemm_f64<true, false, true>), g, b, 0, s, k, A, B, C); break;
-    case 6: hipLaunchKernelGGL((k_gemm_f64<true, true, false>), g, b, 0, s, k, A, B, C); break;
-    default: hipLaunchKernelGGL((k_gemm_f64<true, true, true>), g, b, 0, s, k, A, B, C); break;
-  }
+  if (cfg == 1) launch_gemm<16, 128>(tabs, g, s, k, A, B, C);
+  else if (cfg == 2) launch_gemm<128, 64>(tabs, g, s, k, A, B, C);
+  else launch_gemm<64, 64>(tabs, g, s, k, A, B, C);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

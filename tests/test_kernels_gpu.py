@@ -273,6 +273,9 @@ def test_product_n_and_graph_replay(gpu):
     ({"b": 3, "c": 2}, {"m1": 9, "m2": 7}, {"n1": 5, "n2": 13}, {"k1": 4, "k2": 6}),
     ({}, {"m": 16}, {"n": 16}, {"k": 8}),
     ({}, {"m": 65}, {"n": 129}, {"k": 700}),
+    # the 16 x 128 tile (M <= 16) and the 128 x 64 tile (64 < M <= 128), ragged edges, table groups
+    ({"b": 4}, {"m": 16}, {"n": 300}, {"k": 37}),
+    ({"b": 2}, {"m1": 10, "m2": 10}, {"n": 200}, {"k1": 5, "k2": 25}),
 ])
 def test_pair_gemm_matches_einsum(gpu, shape):
     """FP64 MFMA dense steps (pgm_gemm) vs numpy, with permuted / non-contiguous operands."""
