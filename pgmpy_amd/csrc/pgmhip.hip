@@ -183,6 +183,63 @@ __device__ __forceinline__ void contract_flat(const ContractK &p, const double *
   }
 }
 
+// Flat mode over output PAIRS along the innermost kept dim, one lane per pair, 16-B accesses (batched
+// BP separator marginals: rows innermost).  Host-checked (pgm_batch_add_contract): even innermost kept
+// extent, output innermost stride 1, each operand's innermost kept stride 0 or 1, every other stride
+// of a 16-B-read operand even, bases 16-B aligned.  Same summation order as contract_flat with G = 1.
+template <int CMB, int RED>
+__device__ __forceinline__ void contract_flat2(const ContractK &p, const double *__restrict__ A,
+                                               const double *__restrict__ B, double *__restrict__ C, uint64_t tid,
+                                               uint64_t nthreads) {
+  const int kx = p.nk - 1;
+  const bool va = p.ksa[kx] != 0, vb = p.ksb[kx] != 0;
+  const uint32_t n_pairs = p.n_out >> 1;
+  for (uint64_t q = tid; q < n_pairs; q += nthreads) {
+    int64_t oa = 0, ob = 0, oc = 0;
+    uint32_t idx = (uint32_t)q << 1;
+    for (int k = kx; k >= 0; --k) {
+      const uint32_t qq = fdiv(idx, p.kdiv[k]);
+      const uint32_t dg = idx - qq * p.kdiv[k].d;
+      oa += (int64_t)dg * p.ksa[k];
+      if constexpr (CMB != PGM_COMBINE_COPY) ob += (int64_t)dg * p.ksb[k];
+      oc += (int64_t)dg * p.ksc[k];
+      idx = qq;
+    }
+    double lo = red_init<RED>(), hi = red_init<RED>();
+    for (uint32_t ro = 0; ro < p.n_ro; ++ro) {
+      int64_t ra, rb;
+      decode_ro(p, ro, ra, rb);
+      const double *a = A + oa + ra;
+      const double *b = B + ob + rb;
+      for (uint32_t ri = 0; ri < p.ri_card; ++ri) {
+        double xl, xh;
+        if (va) {
+          const double2 w = *(const double2 *)(a + (int64_t)ri * p.ri_sa);
+          xl = w.x;
+          xh = w.y;
+        } else {
+          xl = xh = a[(int64_t)ri * p.ri_sa];
+        }
+        if constexpr (CMB != PGM_COMBINE_COPY) {
+          double yl, yh;
+          if (vb) {
+            const double2 w = *(const double2 *)(b + (int64_t)ri * p.ri_sb);
+            yl = w.x;
+            yh = w.y;
+          } else {
+            yl = yh = b[(int64_t)ri * p.ri_sb];
+          }
+          xl = combine<CMB>(xl, yl);
+          xh = combine<CMB>(xh, yh);
+        }
+        lo = red_op<RED>(lo, xl);
+        hi = red_op<RED>(hi, xh);
+      }
+    }
+    *(double2 *)(C + oc) = make_double2(lo, hi);
+  }
+}
+
 template <int CMB, int RED>
 __global__ __launch_bounds__(256) void k_contract(const ContractK p, const double *__restrict__ A,
                                                   const double *__restrict__ B, double *__restrict__ C,
@@ -1235,6 +1292,14 @@ struct BatchJob {
 
 template <int CMB>
 __device__ __forceinline__ void batch_contract_c(const BatchJob &J, uint64_t tid, uint64_t n) {
+  if (J.c.row_mode == 2) {  // output pairs, 16-B accesses
+    switch (J.red) {
+      case PGM_RED_NONE: contract_flat2<CMB, PGM_RED_NONE>(J.c, J.A, J.B, J.C, tid, n); break;
+      case PGM_RED_SUM: contract_flat2<CMB, PGM_RED_SUM>(J.c, J.A, J.B, J.C, tid, n); break;
+      default: contract_flat2<CMB, PGM_RED_MAX>(J.c, J.A, J.B, J.C, tid, n); break;
+    }
+    return;
+  }
   switch (J.red) {
     case PGM_RED_NONE: contract_flat<CMB, PGM_RED_NONE>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
     case PGM_RED_SUM: contract_flat<CMB, PGM_RED_SUM>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
@@ -2732,6 +2797,20 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   if (d->reduce != PGM_RED_NONE && (uint64_t)k.n_ro * k.ri_card > 1)
     while (g < 6 && ((uint64_t)k.n_out << g) < 4096 && (1u << (g + 1)) <= k.ri_card) ++g;
   k.g_log2 = g;
+  // output pairs with 16-B accesses when one lane per output is the choice anyway and every access
+  // along the innermost kept dim is aligned and unit-stride (or broadcast)
+  const int kx = k.nk - 1;
+  const bool use_b = d->combine != PGM_COMBINE_COPY;
+  bool pairs = g == 0 && kx >= 0 && !g_no_rows2 && k.kdiv[kx].d % 2 == 0 && k.ksc[kx] == 1 && ((uintptr_t)C & 15) == 0;
+  const bool va = pairs && k.ksa[kx] != 0, vb = pairs && use_b && k.ksb[kx] != 0;
+  pairs = pairs && (k.ksa[kx] == 0 || k.ksa[kx] == 1) && (!use_b || k.ksb[kx] == 0 || k.ksb[kx] == 1);
+  for (int i = 0; pairs && i < kx; ++i) pairs = k.ksc[i] % 2 == 0 && (!va || k.ksa[i] % 2 == 0) && (!vb || k.ksb[i] % 2 == 0);
+  for (int i = 0; pairs && i + 1 < k.nr; ++i) pairs = (!va || k.rsa[i] % 2 == 0) && (!vb || k.rsb[i] % 2 == 0);
+  if (pairs) pairs = (!va || (k.ri_sa % 2 == 0 && ((uintptr_t)A & 15) == 0)) && (!vb || (k.ri_sb % 2 == 0 && ((uintptr_t)B & 15) == 0));
+  if (pairs) {
+    k.row_mode = 2;
+    return batch_append(h, J, (uint64_t)k.n_out / 2);
+  }
   return batch_append(h, J, (uint64_t)k.n_out << g);
 }
 

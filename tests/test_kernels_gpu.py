@@ -365,6 +365,9 @@ def test_program_batch_matches_eager(gpu):
         (rng.random((2, 3, 4)), ["u", "v", "w"], None, None, ["w", "u", "v"], None, "copy"),
         (rng.random((300, 40)), ["m", "k"], rng.random((40, 50)), ["k", "n"], ["m", "n"], "sum", "mul"),
         (rng.random((6,)), ["s"], rng.random((5,)), ["t"], ["t", "s"], None, "add"),
+        # rows innermost and even: the 16-B output-pair form (separator marginal, max-product message)
+        (rng.random((4, 6, 1024)), ["s2", "t2", "r"], None, None, ["t2", "r"], "sum", "copy"),
+        (rng.random((3, 4, 2048)), ["a3", "b3", "r3"], rng.random((4, 2048)), ["b3", "r3"], ["a3", "r3"], "max", "mul"),
     ]
     dev = [(E.to_device(A), la, None if B is None else E.to_device(B), lb, out, red, cmb)
            for A, la, B, lb, out, red, cmb in jobs]
