@@ -919,7 +919,6 @@ struct ProdMK {
   int32_t kind[MOPS];
   int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
   int32_t jvar[MOPS];            // operand varies over the reduced entries (else loaded once per outer)
-  uint32_t xcd, _pad;            // j-outer kernel: consecutive logical blocks on one XCD (grid % 8 == 0)
   uint32_t n_outer, NP;          // kept outer index space; row pairs
   FDiv kdiv[KMAX];
   int64_t ksc[KMAX], ksm[KMAX], ks[MOPS][KMAX];
@@ -945,9 +944,7 @@ __device__ __forceinline__ double prodm_combine(const ProdMK &p, const double (&
   return prod;
 }
 
-// U == 1: the next entry's operands in flight while the current one is stored; U > 1: U entries'
-// operands loaded together (U x NOPS 16-B loads in flight per lane), then U products stored
-template <int NOPS, int RED, int U>
+template <int NOPS, int RED>
 __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *C, double *__restrict__ M) {
   __shared__ int64_t tc[RMAX_MARG];
   __shared__ int64_t to[NOPS][RMAX_MARG];
@@ -1000,30 +997,6 @@ __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *
         }
       };
       double2 acc = make_double2(red_init<RED>(), red_init<RED>());
-      if constexpr (U > 1) {
-        for (uint32_t j0 = 0; j0 < NR; j0 += U) {
-          double2 v[U][NOPS];
-#pragma unroll
-          for (int u = 0; u < U; ++u) load(j0 + u < NR ? j0 + u : NR - 1, v[u]);
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            if (j0 + u < NR) {
-              double lo[NOPS], hi[NOPS];
-#pragma unroll
-              for (int i = 0; i < NOPS; ++i) {
-                lo[i] = v[u][i].x;
-                hi[i] = v[u][i].y;
-              }
-              const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
-              ((double2 *)(C + oc + tc[j0 + u]))[x] = pr;
-              acc.x = red_op<RED>(acc.x, pr.x);
-              acc.y = red_op<RED>(acc.y, pr.y);
-            }
-          }
-        }
-        ((double2 *)(M + om))[x] = acc;
-        continue;
-      }
       double2 cur[NOPS], nxt[NOPS];
       load(0, cur);
       for (uint32_t j = 0; j < NR; ++j) {
@@ -1074,16 +1047,7 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
   }
   __syncthreads();
   const int kx = p.nk - 1;
-  // dispatch sends block b to XCD b % 8: give each XCD a contiguous range of logical blocks, so
-  // blocks sharing broadcast operand rows (neighbouring kept indices) share that XCD's L2
-  uint32_t bx = blockIdx.x, by = blockIdx.y;
-  if (p.xcd) {
-    const uint32_t nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t L = (b & 7u) * (nb >> 3) + (b >> 3);
-    bx = L % gridDim.x;
-    by = L / gridDim.x;
-  }
-  for (uint32_t o = by; o < p.n_outer; o += gridDim.y) {
+  for (uint32_t o = blockIdx.y; o < p.n_outer; o += gridDim.y) {
     int64_t oc = 0, om = 0, off[NOPS];
 #pragma unroll
     for (int i = 0; i < NOPS; ++i) off[i] = 0;
@@ -1097,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
       for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
       idx = q;
     }
-    const uint32_t x0 = bx * (256u * XI) + threadIdx.x;
+    const uint32_t x0 = blockIdx.x * (256u * XI) + threadIdx.x;
     uint32_t xs[XI];
 #pragma unroll
     for (int u = 0; u < XI; ++u) {
@@ -2616,8 +2580,6 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
                             "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
   hipStream_t s = S(stream);
   const bool two = k.n_ops <= 2;
-  // entries per load batch (tuning knob PGM_MARG_U: 1 = one-ahead prefetch, 2, 4)
-  static const int U = getenv("PGM_MARG_U") ? atoi(getenv("PGM_MARG_U")) : 1;
   // j-outer form (tuning knob PGM_MARG_JX = row pairs per lane: 1, 2 or 4; 0 = the j-inner kernel)
   // default (-1): j-outer with 2 row pairs per lane from 1,024 row pairs up, else 1 (MI355X, pathfinder's
   // largest clique: collect 413 -> 272 us at 4,000 rows, 94 -> 80 us at 1,000)
@@ -2626,8 +2588,6 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     const int XI = JX < 0 ? (k.NP >= 1024 ? 2 : 1) : JX >= 4 ? 4 : JX == 2 ? 2 : 1;
     const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
     const dim3 gj((unsigned)gxj, g.y, 1);
-    static const bool xcd = getenv("PGM_MARG_XCD") && atoi(getenv("PGM_MARG_XCD")) > 0;  // tuning knob
-    k.xcd = (xcd && g.y == k.n_outer && (gxj * g.y) % 8 == 0) ? 1u : 0u;
 #define PGM_MARGJ_LAUNCH(XX)                                                                                 \
   if (reduce == PGM_RED_SUM) {                                                                               \
     if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);      \
@@ -2647,22 +2607,13 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     HIP_TRY(hipGetLastError());
     return PGM_OK;
   }
-#define PGM_MARG_LAUNCH(UU)                                                                             \
-  if (reduce == PGM_RED_SUM) {                                                                          \
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM, UU>), g, dim3(256), 0, s, k, C, M);    \
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM, UU>), g, dim3(256), 0, s, k, C, M);     \
-  } else {                                                                                              \
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX, UU>), g, dim3(256), 0, s, k, C, M);    \
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX, UU>), g, dim3(256), 0, s, k, C, M);     \
-  }
-  if (U >= 4) {
-    PGM_MARG_LAUNCH(4)
-  } else if (U == 2) {
-    PGM_MARG_LAUNCH(2)
+  if (reduce == PGM_RED_SUM) {
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
   } else {
-    PGM_MARG_LAUNCH(1)
+    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
+    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
   }
-#undef PGM_MARG_LAUNCH
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }
