@@ -28,7 +28,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 8
+#define PGM_ABI_VERSION 9  // 9: pgm_gemm_desc.lane_order, pgm_batch_add_product_n
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
