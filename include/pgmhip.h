@@ -236,6 +236,9 @@ int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A
 /* an n-ary product job (pgm_product_n's descriptor and checks; flat mode): batched BP runs every
  * small clique / separator product of one dependency level of the calibration as one launch */
 int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const double *const *ops, double *C);
+/* a findings-indicator job (pgm_indicator's arguments): all of a BP sweep's findings in one launch */
+int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
+                            int64_t s_state, int64_t s_row, int32_t *err_flag);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
 int pgm_batch_destroy(void *handle);

@@ -158,6 +158,8 @@ _SIGS = {
     "pgm_batch_add_contract": ([_P, ctypes.POINTER(ContractDesc), _P, _P, _P], ctypes.c_int),
     "pgm_batch_add_gather": ([_P, ctypes.POINTER(GatherDesc), _P, _P, _P, _P], ctypes.c_int),
     "pgm_batch_add_product_n": ([_P, ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P], ctypes.c_int),
+    "pgm_batch_add_indicator": ([_P, _P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P],
+                                ctypes.c_int),
     "pgm_batch_finalize": ([_P], ctypes.c_int),
     "pgm_batch_run": ([_P, _P], ctypes.c_int),
     "pgm_batch_destroy": ([_P], ctypes.c_int),

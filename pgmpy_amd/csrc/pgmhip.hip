@@ -28,7 +28,7 @@
 
 #include "pgmhip.h"
 
-#define PGM_ABI_VERSION 9  // 9: pgm_gemm_desc.lane_order, pgm_batch_add_product_n
+#define PGM_ABI_VERSION 9  // 9: pgm_gemm_desc.lane_order, pgm_batch_add_product_n / _indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -1237,13 +1237,33 @@ __global__ __launch_bounds__(256) void k_gather(const GatherK p, const double *_
   gather_body(p, A, codes, C, err, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
 }
 
+// findings as 0/1 indicators (BP): out[k, r] = (codes[r] == k), 1 for a missing code (PGM_EV_MISSING)
+__device__ __forceinline__ void indicator_body(const uint8_t *__restrict__ codes, int64_t n_rows, int64_t card,
+                                               double *__restrict__ out, int64_t s_state, int64_t s_row,
+                                               int32_t *__restrict__ err, int64_t tid, int64_t stride) {
+  const int64_t n = n_rows * card;
+  for (int64_t i = tid; i < n; i += stride) {
+    const int64_t r = i % n_rows, k = i / n_rows;
+    const uint32_t c = codes[r];
+    double v;
+    if (c == PGM_EV_MISSING)
+      v = 1.0;
+    else {
+      if (c >= (uint64_t)card && err) atomicOr(err, 1);
+      v = (c == (uint64_t)k) ? 1.0 : 0.0;
+    }
+    out[k * s_state + r * s_row] = v;
+  }
+}
+
 // ----------------------------------------------------------------------------- batched small jobs
 // Many independent small contractions / evidence gathers in ONE launch: workgroup -> job through a
 // block map, each job runs the flat-mode contraction (or the gather) over its own blocks.  One
 // level of a compiled contraction path (all steps whose inputs are ready) is one launch instead
 // of one launch per step.
 struct BatchJob {
-  int32_t kind, cmb, red, _pad;  // kind 0: contraction, 1: gather, 2: n-ary product
+  int32_t kind, cmb, red, _pad;  // kind 0: contraction, 1: gather, 2: n-ary product, 3: findings indicator
+  int64_t ind_rows, ind_card, ind_s_state, ind_s_row;
   uint32_t block0, nblocks;
   const double *A, *B;
   double *C;
@@ -1281,6 +1301,10 @@ __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs
     gather_body(J.g, J.A, J.codes, J.C, J.err, tid, n);
     return;
   }
+  if (J.kind == 3) {
+    indicator_body(J.codes, J.ind_rows, J.ind_card, J.C, J.ind_s_state, J.ind_s_row, J.err, (int64_t)tid, (int64_t)n);
+    return;
+  }
   if (J.kind == 2) {
     if (J.pn.pairs) {
       if (J.pn.n_ops <= 2) prodn_flat2<2>(J.pn, J.C, tid, n);
@@ -1305,20 +1329,8 @@ __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs
 __global__ __launch_bounds__(256) void k_indicator(const uint8_t *__restrict__ codes, int64_t n_rows, int64_t card,
                                                    double *__restrict__ out, int64_t s_state, int64_t s_row,
                                                    int32_t *__restrict__ err) {
-  const int64_t n = n_rows * card;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int64_t r = i % n_rows, k = i / n_rows;
-    const uint32_t c = codes[r];
-    double v;
-    if (c == PGM_EV_MISSING)
-      v = 1.0;
-    else {
-      if (c >= (uint64_t)card && err) atomicOr(err, 1);
-      v = (c == (uint64_t)k) ? 1.0 : 0.0;
-    }
-    out[k * s_state + r * s_row] = v;
-  }
+  indicator_body(codes, n_rows, card, out, s_state, s_row, err, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                 (int64_t)gridDim.x * blockDim.x);
 }
 
 // ----------------------------------------------------------------------------- argmax
@@ -2805,6 +2817,24 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
   }
   k.pairs = pairs ? 1u : 0u;
   return batch_append(h, J, pairs ? k.n_out / 2 : k.n_out);
+}
+
+int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
+                            int64_t s_state, int64_t s_row, int32_t *err_flag) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !codes || !out) return fail(PGM_EINVAL, "batch_add_indicator: null argument");
+  if (n_rows <= 0 || card <= 0) return PGM_OK;
+  BatchJob J;
+  memset(&J, 0, sizeof J);
+  J.kind = 3;
+  J.codes = codes;
+  J.C = out;
+  J.err = err_flag;
+  J.ind_rows = n_rows;
+  J.ind_card = card;
+  J.ind_s_state = s_state;
+  J.ind_s_row = s_row;
+  return batch_append(h, J, (uint64_t)(n_rows * card));
 }
 
 int pgm_batch_finalize(void *handle) {

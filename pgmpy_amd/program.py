@@ -149,6 +149,8 @@ class Program:
                     N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
                 elif kind == "gather":
                     N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
+                elif kind == "indicator":
+                    N.check(L.pgm_batch_add_indicator(h, *args), "batch_add_indicator")
                 else:
                     N.check(L.pgm_batch_add_product_n(h, *args), "batch_add_product_n")
             N.check(L.pgm_batch_finalize(h), "batch_finalize")
@@ -229,9 +231,9 @@ class Program:
         args = (N.ptr(codes_col), int(n_rows), int(card), N.ptr(out), int(out.stride(0)), int(out.stride(1)),
                 N.ptr(err))
         self._keep.extend([codes_col, out, err])
-        # err is an atomic OR flag: not a hazard
+        # err is an atomic OR flag: not a hazard; a levelled program batches all findings into one launch
         self._emit(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"), f"indicator card {card}",
-                   [codes_col], [out])
+                   [codes_col], [out], ("indicator", args))
         return out
 
     def gather(self, A, la, evidence, out_labels, codes, ld, row0, n_rows, err=None):
