@@ -598,3 +598,28 @@ def test_bp_levelled_schedule_matches_sequential(gpu, operation):
     if operation == "marginalize":
         for v in bjt.variables[:20]:
             np.testing.assert_allclose(c2.marginal(v), c1.marginal(v), rtol=1e-11, atol=1e-300)
+
+
+def test_bp_levelled_findings_batch_flags_bad_codes(gpu):
+    """Findings indicators of a levelled sweep run as ONE batched launch (pgm_batch_add_indicator);
+    an out-of-range evidence code still sets the error flag (-> IndexError, test_Factor.py:555-565)."""
+    import torch
+
+    from pgmpy_amd.inference.bp_batch import BatchedJunctionTree
+    from pgmpy_amd.inference.EliminationOrder import junction_tree_from_model
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("alarm")
+    bjt = BatchedJunctionTree(junction_tree_from_model(m))
+    leaves = sorted(v for v in m.nodes() if m.out_degree(v) == 0)[:5]
+    rows = 128
+    sch = bjt.schedule(rows, leaves)
+    assert not any(n.startswith("indicator") for n in sch.prog.notes)  # all inside level batches
+    codes = torch.zeros((len(leaves), rows), dtype=torch.uint8, device="cuda")
+    sch.run(codes)
+    torch.cuda.synchronize()
+    assert int(sch.err.item()) == 0
+    codes[2, 7] = 77  # not a state of that variable
+    sch.run(codes)
+    torch.cuda.synchronize()
+    assert int(sch.err.item()) != 0
