@@ -2144,6 +2144,12 @@ static int jit_wg() {
   return wg;
 }
 
+// nontemporal marginal stores in the one-row kernel (tuning knob PGM_ROWS_JIT_NT=1)
+static bool jit_nt() {
+  static const bool nt = getenv("PGM_ROWS_JIT_NT") && atoi(getenv("PGM_ROWS_JIT_NT")) > 0;
+  return nt;
+}
+
 // R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
 static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
@@ -2226,7 +2232,10 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
       appendf(o, " const double iv_%d = dead_%d ? __builtin_nan(\"\") : 1.0 / m%d_%d;", u, u, c, u);
     o += "\n";
     for (int q = 0; q < pl->loop_card[lb]; ++q) {
-      if (R == 1)
+      if (R == 1 && jit_nt())
+        appendf(o, "      __builtin_nontemporal_store(p%d_%d_0 * iv_0, &M[%dLL * ldo + r]);\n", c, q,
+                pl->loop_marg_off[lb] + q);
+      else if (R == 1)
         appendf(o, "      M[%dLL * ldo + r] = p%d_%d_0 * iv_0;\n", pl->loop_marg_off[lb] + q, c, q);
       else
         appendf(o, "      *(double2 *)(M + %dLL * ldo + r) = make_double2(p%d_%d_0 * iv_0, p%d_%d_1 * iv_1);\n",
