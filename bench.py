@@ -354,7 +354,8 @@ def bench_c2(args):
         r = ve.query(q, evidence, show_progress=False)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    (plan, _), = ve._compiled.values()
+    runner, = ve._compiled.values()
+    plan = runner.plan
     ps = plan.path_stats(1)
     return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
             "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,

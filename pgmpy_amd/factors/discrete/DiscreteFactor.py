@@ -54,13 +54,23 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         super(DiscreteFactor, self).store_state_names(variables, cardinality, state_names)
 
     # ------------------------------------------------------------------ storage
+    # Two copies may exist: `_dev` (fp64 device tensor) and `_host` (ndarray).  A host array that
+    # has been handed to the caller (`values` getter, or an array passed to the setter) may be
+    # edited in place at any later time, as the reference's plain ndarray attribute allows; such a
+    # factor is "exposed" and its device copy / value token are checked against a CRC of the host
+    # bytes, so an edit made long after the read is still seen by the next device op and by every
+    # compiled plan that read the factor (pgmpy_amd.inference.plan.PatternPlan.is_current).
+    _exposed = False
+    _dev_crc = None
+
     @property
     def values(self):
         if self._host is None:
             self._host = E.to_host(self._dev)
-        # the host array is handed out (callers may edit it in place): it becomes authoritative
-        self._dev = None
-        self._version += 1
+            self._dev_crc = _crc(self._host)
+        elif not self._exposed and self._dev is not None:
+            self._dev_crc = _crc(self._host)
+        self._exposed = True
         return self._host
 
     @values.setter
@@ -69,30 +79,48 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         if _is_device(v):
             self._dev = v
             self._host = None
+            self._exposed = False
         else:
-            self._host = np.asarray(v, dtype=np.float64)
+            self._host = np.asarray(v, dtype=np.float64)  # may alias the caller's array: exposed
             self._dev = None
+            self._exposed = True
 
     def _values_readonly(self):
-        """Host values for internal readers (plan compilers): a read-only view, the device copy
+        """Host values for internal readers (plan compilers): a read-only view; the device copy
         stays valid and the version is unchanged."""
         if self._host is None:
             self._host = E.to_host(self._dev)
+            if self._exposed:
+                self._dev_crc = _crc(self._host)
         v = self._host.view()
         v.flags.writeable = False
         return v
 
+    def _value_token(self):
+        """Changes whenever the values may have changed (compiled plans compare it)."""
+        if self._exposed and self._host is not None:
+            return (self._version, _crc(self._host))
+        return (self._version, None)
+
     def _d(self):
-        """Device tensor of the values (uploaded on first use)."""
+        """Device tensor of the values (uploaded on first use, re-uploaded after a host edit)."""
+        if self._dev is not None and self._exposed and self._host is not None:
+            crc = _crc(self._host)
+            if crc != self._dev_crc:
+                self._dev = None
+                self._version += 1
         if self._dev is None:
             h = self._host.reshape(tuple(int(c) for c in self.cardinality))
             self._dev = E.to_device(h)
+            if self._exposed:
+                self._dev_crc = _crc(self._host)
         return self._dev
 
     def _set_d(self, t):
         self._version += 1
         self._dev = t
         self._host = None
+        self._exposed = False
 
     def _meta_copy(self):
         """New factor object with copied metadata and NO values (the caller sets them)."""
@@ -101,6 +129,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         f.cardinality = np.array(self.cardinality)
         f._host = None
         f._dev = None
+        f._exposed = False
         f.state_names = self.state_names.copy()
         f.no_to_name = self.no_to_name.copy()
         f.name_to_no = self.name_to_no.copy()
@@ -337,9 +366,12 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         return f
 
     def is_valid_cpd(self):
-        return np.allclose(
-            self.to_factor().marginalize(self.scope()[:1], inplace=False).values.flatten(),
-            np.ones(int(np.prod(self.cardinality[:0:-1]))), atol=0.01)
+        """Do the values sum to 1 over the first variable (DiscreteFactor.py:955-965)?  The
+        reference calls self.to_factor(), which only TabularCPD defines; a DiscreteFactor is
+        already a factor, so its own marginal is used."""
+        col_sums = self.marginalize(self.scope()[:1], inplace=False)._values_readonly()
+        return bool(np.allclose(np.asarray(col_sums).flatten(), np.ones(int(np.prod(self.cardinality[:0:-1]))),
+                                atol=0.01))
 
     # ------------------------------------------------------------------ printing
     def __str__(self):
@@ -423,6 +455,12 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         card = np.array(self.cardinality)[order] if order else np.array(self.cardinality)
         return hash(str(sorted(variable_hashes)) + str(hash(np.ascontiguousarray(vals).tobytes()))
                     + str(hash(np.ascontiguousarray(card).tobytes())) + str(hash(frozenset(self.state_names))))
+
+
+def _crc(a):
+    import zlib
+
+    return zlib.crc32(memoryview(np.ascontiguousarray(a)).cast("B"))
 
 
 def _is_device(x):

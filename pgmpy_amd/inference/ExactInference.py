@@ -16,6 +16,7 @@ Batched evidence (many rows per call) lives in pgmpy_amd.inference.batch /
 bp_batch.
 """
 import itertools
+import threading
 from collections import defaultdict
 
 import networkx as nx
@@ -172,47 +173,42 @@ class VariableElimination(Inference):
                                                 elimination_order=elimination_order, joint=joint,
                                                 show_progress=show_progress)
 
-    def _model_token(self):
-        return (self.model.number_of_edges(), tuple((id(c), c._version) for c in self.model.cpds))
-
     def _query_compiled(self, variables, evidence, joint):
         """query() for a Bayesian network with the greedy order, through a compiled evidence-pattern
         plan (pgmpy_amd.inference.plan.PatternPlan) cached per (query variables, evidence
         variables): pruning (inference/base.py:154-212), the evidence slice, the greedy contraction
         (ExactInference.py:349-406) and the normalisation run as one fused kernel or one replayed
-        graph on a single evidence row.  The model's CPD identities and value versions are part of
-        the cache key, so editing the model recompiles."""
-        from .batch import upload_codes
-        from .plan import PatternPlan
+        graph on a single evidence row.  A cached plan is reused only while the model structure and
+        the values of the CPDs it read are unchanged (PatternPlan.is_current), so editing the model
+        recompiles.  Thread-safe: the cache is locked and each runner serialises its own buffers."""
+        from .plan import PatternPlan, QueryRunner
 
         ev_vars = sorted(evidence, key=str)
-        cache = self.__dict__.setdefault("_compiled", {})
-        key = (tuple(variables), tuple(ev_vars), bool(joint), self._model_token())
-        hit = cache.get(key)
-        if hit is None:
-            plan = PatternPlan(self.model, variables, ev_vars, {v: i for i, v in enumerate(ev_vars)})
-            out = plan.alloc_outputs(1, marginals=not joint, joint=joint)
-            hit = (plan, out)
-            if len(cache) >= 64:
-                cache.pop(next(iter(cache)))
-            cache[key] = hit
-        plan, out = hit
-        codes = np.empty((max(1, len(ev_vars)), 1), dtype=np.uint8)
-        for j, v in enumerate(ev_vars):
-            codes[j, 0] = self.model.get_cpds(v).get_state_no(v, evidence[v])
-        plan.run(upload_codes(codes), 1, 0, 1, out)
-        states = self.model.states
+        key = (tuple(variables), tuple(ev_vars), bool(joint))
+        lock = self.__dict__.get("_compiled_lock")
+        if lock is None:
+            lock = self.__dict__.setdefault("_compiled_lock", threading.Lock())
+        with lock:
+            cache = self.__dict__.setdefault("_compiled", {})
+            runner = cache.pop(key, None)
+            if runner is None or not runner.plan.is_current():
+                plan = PatternPlan(self.model, variables, ev_vars, {v: i for i, v in enumerate(ev_vars)})
+                runner = QueryRunner(plan, joint)
+                while len(cache) >= 64:
+                    cache.pop(next(iter(cache)))
+            cache[key] = runner  # most recently used last
+        plan = runner.plan
+        model = self.model
+        codes = [model.get_cpds(v).get_state_no(v, evidence[v]) for v in ev_vars]
+        vals = runner.run(codes)
+        states = {v: model.get_cpds(v).state_names[v] for v in variables}
         if joint:
-            vals = E.contract(out["joint"], ["q", E.ROW], None, None, ["q", E.ROW], combine="copy")
-            return DiscreteFactor(list(variables), [len(states[v]) for v in variables],
-                                  vals.reshape([len(states[v]) for v in variables]),
+            return DiscreteFactor(list(variables), list(plan.cards), vals,
                                   state_names={v: states[v] for v in variables})
         res = {}
         for i, v in enumerate(variables):
             a = plan.acc_off[i]
-            vals = E.contract(out["marg"][a:a + plan.cards[i]], ["s", E.ROW], None, None, ["s", E.ROW],
-                              combine="copy")
-            res[v] = DiscreteFactor([v], [plan.cards[i]], vals.reshape(plan.cards[i]), state_names={v: states[v]})
+            res[v] = DiscreteFactor([v], [plan.cards[i]], vals[a:a + plan.cards[i]], state_names={v: states[v]})
         return res
 
     def max_marginal(self, variables=None, evidence=None, elimination_order="MinFill", show_progress=True):

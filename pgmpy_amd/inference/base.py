@@ -7,6 +7,7 @@ import numpy as np
 
 from ..factors.discrete import DiscreteFactor, TabularCPD
 from ..models import DiscreteBayesianNetwork, JunctionTree
+from .dsep import prune
 
 
 def _fast_bn(nodes, edges, cpds):
@@ -14,6 +15,7 @@ def _fast_bn(nodes, edges, cpds):
     bn = DiscreteBayesianNetwork()
     nx.DiGraph.add_nodes_from(bn, nodes)
     nx.DiGraph.add_edges_from(bn, edges)
+    bn._bump()
     for cpd in cpds:
         bn.cpds.append(cpd)
         bn._cpd_index[cpd.variable] = cpd
@@ -21,22 +23,11 @@ def _fast_bn(nodes, edges, cpds):
 
 
 def prune_structure(model, variables, evidence_vars):
-    """Nodes kept by d-separation + ancestral pruning (inference/base.py:154-197).
+    """Nodes kept by d-separation + ancestral pruning (inference/base.py:154-197), on the
+    integer-indexed DAG (pgmpy_amd.inference.dsep.prune).
 
     Returns (kept_nodes in model order, evidence vars kept)."""
-    variables = list(model.nodes()) if len(variables) == 0 else list(variables)
-    d_connected = model.active_trail_nodes(variables=variables, observed=list(evidence_vars), include_latents=True)
-    d_connected = set.union(*d_connected.values()).union(evidence_vars)
-    ev = [v for v in evidence_vars if v in d_connected]
-    sub = nx.DiGraph()
-    sub.add_nodes_from(n for n in model.nodes() if n in d_connected)
-    sub.add_edges_from((u, v) for u, v in model.edges() if u in d_connected and v in d_connected)
-    targets = list(variables) + list(ev)
-    anc = set(targets)
-    for t in targets:
-        anc.update(nx.ancestors(sub, t))
-    kept = [n for n in sub.nodes() if n in anc]
-    return kept, ev
+    return prune(model, list(variables), list(evidence_vars))
 
 
 class Inference(object):

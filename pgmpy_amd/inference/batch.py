@@ -8,6 +8,7 @@ grouped by evidence pattern, and each pattern runs as one compiled device plan
 (pgmpy_amd.inference.plan.PatternPlan).
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -124,18 +125,26 @@ def group_patterns(codes):
 
 
 _PLAN_CACHE_ATTR = "_pgmpy_amd_plan_cache"
+_PLAN_CACHE_MAX = 64
+_plan_cache_lock = threading.Lock()
 
 
 def get_plan(model, variables, evidence_vars, col_of):
-    cache = getattr(model, _PLAN_CACHE_ATTR, None)
-    if cache is None:
-        cache = {}
-        setattr(model, _PLAN_CACHE_ATTR, cache)
+    """The compiled plan of an evidence pattern, cached on the model (at most 64, least recently
+    used dropped first).  A cached plan is reused only while PatternPlan.is_current(): the model's
+    structure and the values of the CPDs it read are unchanged (a CPD edited, replaced, added or
+    removed recompiles, as the reference recomputes from the current CPDs on every call)."""
     key = (tuple(variables), tuple(evidence_vars), tuple(sorted((k, v) for k, v in col_of.items()
                                                                 if k in set(evidence_vars))))
-    plan = cache.get(key)
-    if plan is None:
-        plan = PatternPlan(model, variables, evidence_vars, col_of)
+    with _plan_cache_lock:
+        cache = model.__dict__.get(_PLAN_CACHE_ATTR)
+        if cache is None:
+            cache = model.__dict__.setdefault(_PLAN_CACHE_ATTR, {})
+        plan = cache.pop(key, None)
+        if plan is None or not plan.is_current():
+            plan = PatternPlan(model, variables, evidence_vars, col_of)
+            while len(cache) >= _PLAN_CACHE_MAX:
+                cache.pop(next(iter(cache)))
         cache[key] = plan
     return plan
 

@@ -20,6 +20,7 @@ Per batch only the uint8 evidence-code columns the plan reads are touched.
 A compiled plan is immutable; run() is re-entrant on distinct outputs.
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -54,9 +55,13 @@ class PatternPlan:
 
         kept, ev = prune_structure(model, self.variables, self.evidence_vars)
         kept_set, ev_set = set(kept), set(ev)
+        self._lock = threading.RLock()  # lazy compilation and shared scratch buffers
+        self._epoch = getattr(model, "_epoch", None)
+        self._sources = []  # (cpd, value token) of every CPD the plan read: see is_current()
         factors = []  # (vars, host values C-order)
         for var in kept:
             cpd = model.get_cpds(var)
+            self._sources.append((cpd, cpd._value_token()))
             scope_diff = set(cpd.scope()) - kept_set
             if scope_diff:
                 cpd = cpd.marginalize(scope_diff, inplace=False)  # device op
@@ -90,6 +95,13 @@ class PatternPlan:
         self._handle_joint = None
         self.extra_mode = 0  # tuning bits (N.ROWS_VALUES_GLOBAL)
         self.n_comp = len(comps) if self.kind == "fused" else None
+
+    def is_current(self):
+        """True while the model structure and the values of every CPD this plan read are unchanged
+        (the reference recomputes from the current CPDs on every call)."""
+        if getattr(self.model, "_epoch", None) != self._epoch:
+            return False
+        return all(cpd._value_token() == tok for cpd, tok in self._sources)
 
     # ------------------------------------------------------------------ fused
     def components(self):
@@ -222,13 +234,18 @@ class PatternPlan:
     def _build_fused(self):
         """Upload the plan (lazily, on first run)."""
         if self._handle is None:
-            self._handle, self._plan, self.n_comp = self._make_rows_plan(split=True)
-            if self.n_comp == 1:
-                self._handle_joint = self._handle
+            with self._lock:
+                if self._handle is None:
+                    h, self._plan, self.n_comp = self._make_rows_plan(split=True)
+                    if self.n_comp == 1:
+                        self._handle_joint = h
+                    self._handle = h
 
     def _joint_handle(self):
         if self._handle_joint is None:
-            self._handle_joint, _, _ = self._make_rows_plan(split=False)
+            with self._lock:
+                if self._handle_joint is None:
+                    self._handle_joint, _, _ = self._make_rows_plan(split=False)
         return self._handle_joint
 
     def __del__(self):
@@ -423,6 +440,10 @@ class PatternPlan:
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
         """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
         replay of a compiled program (_steps_program)."""
+        with self._lock:  # the compiled programs own their scratch buffers: one caller at a time
+            return self._run_steps_locked(codes, ld, row0, n_rows, out, err)
+
+    def _run_steps_locked(self, codes, ld, row0, n_rows, out, err):
         L = N.lib()
         s = N.stream_handle()
         outs = frozenset(k for k in ("marg", "joint", "map") if k in out)
@@ -465,6 +486,44 @@ class PatternPlan:
                 "factors": [list(v) for v, _ in self.factors], "hidden": self.hidden,
                 "evidence_columns": len(self.ev_used), "query_space": self.P, "hidden_space": self.H,
                 "values": int(sum(int(np.prod(c.cardinality)) for _, c in self.factors))}
+
+
+class QueryRunner:
+    """One evidence row through a compiled plan, results back on the host (VariableElimination.query
+    on a Bayesian network, ExactInference.py:246-457).  Owns its device codes/output buffers and a
+    pinned host staging buffer; a lock makes concurrent queries from several threads on one
+    VariableElimination safe (the reference calls map_query from joblib threads on one object,
+    DiscreteBayesianNetwork.py:871)."""
+
+    def __init__(self, plan, joint):
+        import torch
+
+        self.plan = plan
+        self.joint = bool(joint)
+        self.lock = threading.Lock()
+        n_ev = max(1, len(plan.evidence_vars))
+        dev = E.device()
+        self.d_codes = torch.zeros((n_ev, 1), dtype=torch.uint8, device=dev)
+        self.h_codes = torch.zeros((n_ev, 1), dtype=torch.uint8, pin_memory=True)
+        self.out = plan.alloc_outputs(1, marginals=not joint, joint=joint)
+        self.key = "joint" if joint else "marg"
+        self.h_out = torch.empty(tuple(self.out[self.key].shape), dtype=torch.float64, pin_memory=True)
+
+    def run(self, codes):
+        """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
+        the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
+        L = N.lib()
+        with self.lock:
+            s = N.stream_handle()
+            hc = self.h_codes.numpy()
+            hc[:len(codes), 0] = codes
+            N.check(L.pgm_memcpy_h2d(N.ptr(self.d_codes), ctypes.c_void_p(self.h_codes.data_ptr()),
+                                     hc.nbytes, s), "memcpy_h2d")
+            self.plan.run(self.d_codes, 1, 0, 1, self.out)
+            dst = self.out[self.key]
+            N.check(L.pgm_memcpy_d2h(ctypes.c_void_p(self.h_out.data_ptr()), N.ptr(dst),
+                                     dst.numel() * 8, s), "memcpy_d2h")
+            return self.h_out.numpy().reshape(-1).copy()
 
 
 class BoundRows:

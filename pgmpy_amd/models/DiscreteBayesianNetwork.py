@@ -30,6 +30,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         self._cpd_index = {}
         self.cardinalities = defaultdict(int)
         self.latents = set(latents)
+        self._epoch = 0  # bumped on every structural / CPD change (plan caches key on it)
         if ebunch:
             self.add_edges_from(ebunch)
 
@@ -40,6 +41,34 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         if u in self.nodes() and v in self.nodes() and nx.has_path(self, v, u):
             raise ValueError(f"Loops are not allowed. Adding the edge from ({u}->{v}) forms a loop.")
         super().add_edge(u, v, **kwargs)
+        self._bump()
+
+    def _bump(self):
+        self.__dict__["_epoch"] = self.__dict__.get("_epoch", 0) + 1
+
+    def add_node(self, node, **kwargs):
+        super().add_node(node, **kwargs)
+        self._bump()
+
+    def add_nodes_from(self, nodes, **kwargs):
+        super().add_nodes_from(nodes, **kwargs)
+        self._bump()
+
+    def remove_edge(self, u, v):
+        super().remove_edge(u, v)
+        self._bump()
+
+    def remove_edges_from(self, ebunch):
+        super().remove_edges_from(ebunch)
+        self._bump()
+
+    def remove_node(self, n):
+        super().remove_node(n)
+        self._bump()
+
+    def remove_nodes_from(self, nodes):
+        super().remove_nodes_from(nodes)
+        self._bump()
 
     def add_edges_from(self, ebunch, **kwargs):
         for e in ebunch:
@@ -80,6 +109,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
             else:
                 self.cpds.append(cpd)
             self._cpd_index[cpd.variable] = cpd
+        self._bump()
 
     def get_cpds(self, node=None):
         if node is not None:
@@ -94,6 +124,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
                 cpd = self.get_cpds(cpd)
             self.cpds.remove(cpd)
             self._cpd_index.pop(cpd.variable, None)
+        self._bump()
 
     def get_cardinality(self, node=None):
         if node is not None:
@@ -149,41 +180,17 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         return anc
 
     def active_trail_nodes(self, variables, observed=None, include_latents=False):
-        """Reachable nodes by active trails (Koller & Friedman Alg. 3.1; DAG.py:864-950)."""
-        if observed:
-            if isinstance(observed, set):
-                observed = list(observed)
-            observed_list = observed if isinstance(observed, (list, tuple)) else [observed]
-        else:
-            observed_list = []
-        observed_set = set(observed_list)
-        ancestors_list = self._get_ancestors_of(observed_list)
-        active_trails = {}
-        for start in variables if isinstance(variables, list) else [variables]:
-            visit_list = {(start, "up")}
-            traversed = set()
-            active_nodes = set()
-            while visit_list:
-                node, direction = visit_list.pop()
-                if (node, direction) in traversed:
-                    continue
-                if node not in observed_set:
-                    active_nodes.add(node)
-                traversed.add((node, direction))
-                if direction == "up" and node not in observed_set:
-                    for parent in self.predecessors(node):
-                        visit_list.add((parent, "up"))
-                    for child in self.successors(node):
-                        visit_list.add((child, "down"))
-                elif direction == "down":
-                    if node not in observed_set:
-                        for child in self.successors(node):
-                            visit_list.add((child, "down"))
-                    if node in ancestors_list:
-                        for parent in self.predecessors(node):
-                            visit_list.add((parent, "up"))
-            active_trails[start] = active_nodes if include_latents else active_nodes - self.latents
-        return active_trails
+        """{variable: nodes reachable from it by an active trail given `observed`} (DAG.py:864-950).
+
+        Computed on the integer-indexed DAG (pgmpy_amd.inference.dsep, Bayes-ball)."""
+        from ..inference.dsep import active_trails
+
+        if observed is None or (not isinstance(observed, (str, int)) and len(observed) == 0):
+            observed = []
+        elif isinstance(observed, (str, int)) or not hasattr(observed, "__iter__"):
+            observed = [observed]
+        starts = variables if isinstance(variables, (list, tuple, set)) else [variables]
+        return active_trails(self, list(starts), list(observed), include_latents=include_latents)
 
     def get_ancestral_graph(self, nodes):
         anc = self._get_ancestors_of(list(nodes))
