@@ -44,21 +44,29 @@ def log(*a):
 _BACKEND = "nccl"
 
 
-def dist_setup(n_gpus, backend="nccl"):
+def dist_setup(n_gpus, backend="auto"):
     """One rank per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*).
 
-    backend "nccl" is RCCL on ROCm; "gloo" lets several ranks share one GPU for a rehearsal."""
+    backend "nccl" is RCCL on ROCm.  "auto" picks it when every rank has its own GPU, else "gloo"
+    (several ranks sharing one GPU: a plumbing rehearsal on the one-GPU box, never a scaling
+    number)."""
     global _BACKEND
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}: launch N ranks (torchrun) or let "
+                         f"bench.py start them itself (WORLD_SIZE unset)")
     if world > 1:
         import torch.distributed as dist
 
-        dev = local % max(1, torch.cuda.device_count())
+        n_dev = max(1, torch.cuda.device_count())
+        dev = local % n_dev
         torch.cuda.set_device(dev)
+        if backend == "auto":
+            backend = "nccl" if n_dev >= world else "gloo"
         _BACKEND = backend
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -68,6 +76,24 @@ def dist_setup(n_gpus, backend="nccl"):
     if torch.cuda.is_available():
         torch.cuda.set_device(0)
     return None, 0, 1
+
+
+def launch_ranks(n):
+    """--gpus N without WORLD_SIZE: start N ranks with torch.distributed.run as a child process.
+
+    This parent never touches the GPU (no HIP call before or after): it only waits for the
+    launcher and exits with its status."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: starting", n, "ranks:", " ".join(cmd))
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 def barrier(dist):
@@ -310,16 +336,147 @@ def bench_c3(args, dist, rank, world):
         if world == 1 and args.cpu_pre is not None:
             result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
-    if dist is not None and args.gather:
+    if dist is not None:
+        # the result delivery (outside the timed region in this weak-scaling line; --workload c5
+        # times it inside the step): every rank's [17, rows] marginals to rank 0
         from pgmpy_amd.distributed import gather_rows
 
         barrier(dist)
         g0 = time.perf_counter()
         src = out["marg"] if _BACKEND == "nccl" else out["marg"].cpu()
-        gathered = gather_rows(src, rows * world, dist)
+        gather_rows(src, rows * world, dist)
         torch.cuda.synchronize()
         result["gather_ms"] = (time.perf_counter() - g0) * 1e3
+        result["gather_backend"] = _BACKEND
     return result
+
+
+def bench_c5(args, dist, rank, world):
+    """C5 (BASELINE.json configs[4]): ROWS (1,000,000) munin template rows per step over all ranks,
+    contiguous blocks per rank (distributed.shard_bounds), strong scaling.  One step = every rank's
+    bound fused-plan launch over its block + the gather of the [17, rows] fp64 marginals to rank 0
+    (torch.distributed.gather: RCCL over xGMI with the nccl backend).  Rank 0 owns a [world, 17,
+    block] receive buffer allocated once; blocks are padded to the largest so one gather serves all."""
+    import torch
+
+    from pgmpy_amd.distributed import shard_bounds
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    model = get_example_model("munin")
+    missing_list = random.Random(0).sample(sorted(model.nodes()), 3)
+    variables = list(set(missing_list))
+    total = args.rows
+    lo, hi = shard_bounds(total, world, rank)
+    rows = hi - lo
+    block = max(h - l for l, h in (shard_bounds(total, world, r) for r in range(world)))
+    t0 = time.perf_counter()
+    codes_all, nodes = forward_sample_codes(model, rows, seed=(42, lo))
+    observed = [v for v in nodes if v not in set(variables)]
+    pos = {v: i for i, v in enumerate(nodes)}
+    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])
+    del codes_all
+    log(f"[rank {rank}] rows [{lo}, {hi}) sampled in {time.perf_counter() - t0:.1f}s")
+    plan = PatternPlan(model, variables, observed, {v: i for i, v in enumerate(observed)})
+    assert plan.kind == "fused", plan.describe()
+    d_codes = upload_codes(codes_ev)
+    dev = d_codes.device
+    send = torch.zeros((plan.n_acc, block), dtype=torch.float64, device=dev)  # ld = block (padded)
+    out = {"marg": send[:, :rows] if rows else send[:, :1]}
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
+    nccl = dist is not None and _BACKEND == "nccl"
+    recv = None
+    if dist is not None and rank == 0:
+        recv = [torch.empty((plan.n_acc, block), dtype=torch.float64, device=dev if nccl else "cpu")
+                for _ in range(world)]
+    host_send = None if nccl or dist is None else torch.empty((plan.n_acc, block), dtype=torch.float64)
+
+    def gather():
+        if dist is None:
+            return
+        if nccl:
+            dist.gather(send, gather_list=recv, dst=0)
+        else:  # gloo rehearsal: through host memory
+            host_send.copy_(send)
+            dist.gather(host_send, gather_list=recv, dst=0)
+
+    def step():
+        bound.run()
+        gather()
+
+    for _ in range(args.warmup):
+        step()
+    barrier(dist)
+    timer = HipTimer()
+    timer.start()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    step_ms_events = timer.stop_ms() / args.steps
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t_end - t_start)
+    assert int(err.item()) == 0
+    # the launch alone (HIP events), then the gather alone, outside the timed region
+    barrier(dist)
+    timer.start()
+    for _ in range(args.steps):
+        bound.run()
+    kern_ms = timer.stop_ms() / args.steps
+    barrier(dist)
+    g0 = time.perf_counter()
+    for _ in range(args.steps):
+        gather()
+    torch.cuda.synchronize()
+    gather_ms = max_over_ranks(dist, (time.perf_counter() - g0) * 1e3 / args.steps)
+    bpr = plan.algorithmic_bytes_per_row(marginals=True)
+    achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
+    parity = None
+    if rank == 0:
+        from oracle import ve as OVE  # checker only: first rows of rank 0's block
+        from oracle.network import load_network
+        from pgmpy_amd.inference.batch import download
+
+        net = load_network("munin")
+        got = download(send[:, :min(rows, 16)].contiguous())
+        worst = 0.0
+        for r in range(got.shape[1]):
+            ev = {v: net.states[v][codes_ev[j, r]] for j, v in enumerate(observed)}
+            m = OVE.query(net, variables, ev, joint_out=False)
+            exp = np.concatenate([m[v] for v in plan.variables])
+            worst = max(worst, float(np.max(np.abs(got[:, r] - exp) / np.maximum(np.abs(exp), 1e-300))))
+        parity = {"rows_checked": int(got.shape[1]), "max_rel_err": worst, "ok": worst <= 1e-6}
+    return {
+        "metric": METRIC,
+        "value": total * args.steps / elapsed,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))",
+        "config": {"workload": "C5 munin predict_probability template, 1M rows per step sharded over the ranks "
+                               "+ gather of the marginals to rank 0",
+                   "network": "munin", "missing": variables, "global_rows_per_step": total,
+                   "rows_per_gpu_per_step": rows, "parallelism": f"rows sharded over {world} rank(s), "
+                   f"{_BACKEND if dist is not None else 'no'} gather to rank 0"},
+        "gather_ms": gather_ms if dist is not None else 0.0,
+        "gather_backend": _BACKEND if dist is not None else None,
+        "gather_bytes_to_rank0": 8 * plan.n_acc * block * (world - 1),
+        "step_ms_events_rank0": step_ms_events,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": plan.kernel_name(),
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows},
+        "parity": parity,
+    }
 
 
 def bench_c2(args):
@@ -460,15 +617,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--rows", type=int, default=None)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c1", "c2", "c4"])
+    ap.add_argument("--rows", type=int, default=None,
+                    help="c3: rows per GPU per step (100,000); c5: rows per step over all GPUs (1,000,000)")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c5", "c1", "c2", "c4"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true", help="after timing, gather marginals to rank 0 (RCCL)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     args = ap.parse_args()
     if args.rows is None:
-        args.rows = 100_000 if args.workload == "c3" else 1000
+        args.rows = {"c3": 100_000, "c5": 1_000_000}.get(args.workload, 1000)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     from pgmpy_amd.build import build
 
     build(verbose=False)
@@ -479,6 +639,8 @@ def main():
     dist, rank, world = dist_setup(args.gpus, args.dist_backend)
     if args.workload == "c3":
         res = bench_c3(args, dist, rank, world)
+    elif args.workload == "c5":
+        res = bench_c5(args, dist, rank, world)
     elif args.workload == "c2":
         res = bench_c2(args)
     elif args.workload == "c1":

@@ -20,16 +20,19 @@ def forward_sample_codes(model, n, seed=42, order=None):
     for v in nx.topological_sort(model):
         cpd = model.get_cpds(v)
         card = int(cpd.cardinality[0])
-        table = np.asarray(cpd.values, dtype=np.float64).reshape(card, -1)  # (card, prod parent cards)
+        table = np.asarray(cpd._values_readonly(), dtype=np.float64).reshape(card, -1)  # (card, prod parent cards)
         parents = list(cpd.variables[1:])
-        col = np.zeros(n, dtype=np.int64)
+        col = np.zeros(n, dtype=np.int32)
         for p, pc in zip(parents, cpd.cardinality[1:]):
-            col = col * int(pc) + codes[idx[p]].astype(np.int64)
+            col *= int(pc)
+            col += codes[idx[p]]
         cdf = np.cumsum(table, axis=0)  # (card, cols)
         cdf /= cdf[-1:, :]
         u = rng.random(n)
-        c = (u[None, :] > cdf[:, col]).sum(axis=0)
-        codes[idx[v]] = np.minimum(c, card - 1).astype(np.uint8)
+        c = np.zeros(n, dtype=np.uint8)
+        for k in range(card - 1):  # state = number of cdf entries below u (inverse CDF)
+            c += u > np.take(cdf[k], col)
+        codes[idx[v]] = c
     return codes, nodes
 
 
