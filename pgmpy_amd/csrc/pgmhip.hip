@@ -53,6 +53,16 @@ static int fail(int code, const char *fmt, ...) {
     }                                                                                    \
   } while (0)
 
+// debugging aid (PGM_STALE_PROBE=1): report a pending HIP error left by an earlier call when a C-ABI
+// entry point starts, so a launch check is not blamed for someone else's error
+static void stale_probe(const char *fn) {
+  static const bool on = getenv("PGM_STALE_PROBE") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipPeekAtLastError();
+  if (e != hipSuccess) fprintf(stderr, "pgmhip: pending HIP error at entry of %s: %s\n", fn, hipGetErrorString(e));
+}
+#define STALE_PROBE() stale_probe(__func__)
+
 static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ----------------------------------------------------------------------------- fast division
@@ -2349,6 +2359,7 @@ int pgm_last_error(char *buf, size_t len) {
 }
 
 int pgm_device_count(int *n) {
+  STALE_PROBE();
   if (!n) return fail(PGM_EINVAL, "null pointer");
   int c = 0;
   hipError_t e = hipGetDeviceCount(&c);
@@ -2362,11 +2373,13 @@ int pgm_device_count(int *n) {
 }
 
 int pgm_set_device(int device) {
+  STALE_PROBE();
   HIP_TRY(hipSetDevice(device));
   return PGM_OK;
 }
 
 int pgm_alloc(void **ptr, size_t bytes) {
+  STALE_PROBE();
   if (!ptr) return fail(PGM_EINVAL, "null pointer");
   *ptr = nullptr;
   if (bytes == 0) return PGM_OK;
@@ -2375,17 +2388,20 @@ int pgm_alloc(void **ptr, size_t bytes) {
 }
 
 int pgm_free(void *ptr) {
+  STALE_PROBE();
   if (ptr) HIP_TRY(hipFree(ptr));
   return PGM_OK;
 }
 
 int pgm_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+  STALE_PROBE();
   if (bytes == 0) return PGM_OK;
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
   return PGM_OK;
 }
 
 int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+  STALE_PROBE();
   if (bytes == 0) return PGM_OK;
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)));
   HIP_TRY(hipStreamSynchronize(S(stream)));
@@ -2393,23 +2409,27 @@ int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
 }
 
 int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
+  STALE_PROBE();
   if (bytes == 0) return PGM_OK;
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
   return PGM_OK;
 }
 
 int pgm_memset(void *dst, int value, size_t bytes, void *stream) {
+  STALE_PROBE();
   if (bytes == 0) return PGM_OK;
   HIP_TRY(hipMemsetAsync(dst, value, bytes, S(stream)));
   return PGM_OK;
 }
 
 int pgm_stream_sync(void *stream) {
+  STALE_PROBE();
   HIP_TRY(hipStreamSynchronize(S(stream)));
   return PGM_OK;
 }
 
 int pgm_event_create(void **ev) {
+  STALE_PROBE();
   if (!ev) return fail(PGM_EINVAL, "null pointer");
   hipEvent_t e;
   HIP_TRY(hipEventCreate(&e));
@@ -2418,22 +2438,26 @@ int pgm_event_create(void **ev) {
 }
 
 int pgm_event_destroy(void *ev) {
+  STALE_PROBE();
   if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
   return PGM_OK;
 }
 
 int pgm_event_record(void *ev, void *stream) {
+  STALE_PROBE();
   HIP_TRY(hipEventRecord((hipEvent_t)ev, S(stream)));
   return PGM_OK;
 }
 
 int pgm_event_elapsed_ms(void *start, void *stop, float *ms) {
+  STALE_PROBE();
   HIP_TRY(hipEventSynchronize((hipEvent_t)stop));
   HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
   return PGM_OK;
 }
 
 int pgm_contract_workspace(const pgm_contract_desc *d, size_t *bytes) {
+  STALE_PROBE();
   if (!bytes) return fail(PGM_EINVAL, "null pointer");
   ContractLaunch L;
   int rc = plan_contract(d, L);
@@ -2444,6 +2468,7 @@ int pgm_contract_workspace(const pgm_contract_desc *d, size_t *bytes) {
 
 int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, double *C, void *workspace,
                  size_t workspace_bytes, void *stream) {
+  STALE_PROBE();
   ContractLaunch L;
   int rc = plan_contract(d, L);
   if (rc) return rc;
@@ -2531,6 +2556,7 @@ static int plan_prodn(const pgm_productn_desc *d, const double *const *ops, Prod
 extern "C" {
 
 int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream) {
+  STALE_PROBE();
   if (!d || !ops || !C) return fail(PGM_EINVAL, "product_n: null argument");
   ProdNK k;
   const int prc = plan_prodn(d, ops, k);
@@ -2583,6 +2609,7 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
 
 int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *ops, const double *C,
                               const int64_t *marg_s, const double *M) {
+  STALE_PROBE();
   ProdMK k;
   dim3 g;
   return plan_product_marg(d, ops, C, marg_s, M, k, g) == 1 ? 1 : 0;
@@ -2590,6 +2617,7 @@ int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *o
 
 int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops, double *C, const int64_t *marg_s,
                            int32_t reduce, double *M, void *stream) {
+  STALE_PROBE();
   if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
     return fail(PGM_EINVAL, "product_n_marginal: reduce must be PGM_RED_SUM or PGM_RED_MAX");
   ProdMK k;
@@ -2640,12 +2668,14 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
 }
 
 int pgm_graph_capture_begin(void *stream) {
+  STALE_PROBE();
   if (!stream) return fail(PGM_EINVAL, "graph capture needs a non-default stream");
   HIP_TRY(hipStreamBeginCapture(S(stream), hipStreamCaptureModeRelaxed));
   return PGM_OK;
 }
 
 int pgm_graph_capture_end(void *stream, void **graph_exec) {
+  STALE_PROBE();
   if (!graph_exec) return fail(PGM_EINVAL, "null pointer");
   hipGraph_t g = nullptr;
   HIP_TRY(hipStreamEndCapture(S(stream), &g));
@@ -2661,12 +2691,14 @@ int pgm_graph_capture_end(void *stream, void **graph_exec) {
 }
 
 int pgm_graph_launch(void *graph_exec, void *stream) {
+  STALE_PROBE();
   if (!graph_exec) return fail(PGM_EINVAL, "null graph");
   HIP_TRY(hipGraphLaunch((hipGraphExec_t)graph_exec, S(stream)));
   return PGM_OK;
 }
 
 int pgm_graph_destroy(void *graph_exec) {
+  STALE_PROBE();
   if (graph_exec) HIP_TRY(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return PGM_OK;
 }
@@ -2714,6 +2746,7 @@ extern "C" {
 
 int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C, int32_t *err_flag,
                void *stream) {
+  STALE_PROBE();
   if (!d || !A || !C) return fail(PGM_EINVAL, "gather: null argument");
   if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "gather: null codes");
   GatherK k;
@@ -2727,6 +2760,7 @@ int pgm_gather(const pgm_gather_desc *d, const double *A, const uint8_t *codes, 
 }
 
 int pgm_batch_create(void **handle) {
+  STALE_PROBE();
   if (!handle) return fail(PGM_EINVAL, "batch_create: null handle");
   *handle = new (std::nothrow) BatchHandle;
   return *handle ? PGM_OK : fail(PGM_ENOMEM, "batch_create: host allocation");
@@ -2744,6 +2778,7 @@ static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads) {
 }
 
 int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const double *A, const double *B, double *C) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h || !A || !C) return fail(PGM_EINVAL, "batch_add_contract: null argument");
   if (d && d->combine != PGM_COMBINE_COPY && !B) return fail(PGM_EINVAL, "batch_add_contract: null B");
@@ -2788,6 +2823,7 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
 
 int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
                          int32_t *err_flag) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h || !d || !A || !C) return fail(PGM_EINVAL, "batch_add_gather: null argument");
   if (d->n_ev > 0 && !codes) return fail(PGM_EINVAL, "batch_add_gather: null codes");
@@ -2805,6 +2841,7 @@ int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A
 }
 
 int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const double *const *ops, double *C) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h || !C) return fail(PGM_EINVAL, "batch_add_product_n: null argument");
   BatchJob J;
@@ -2830,6 +2867,7 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
 
 int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
                             int64_t s_state, int64_t s_row, int32_t *err_flag) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h || !codes || !out) return fail(PGM_EINVAL, "batch_add_indicator: null argument");
   if (n_rows <= 0 || card <= 0) return PGM_OK;
@@ -2847,6 +2885,7 @@ int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, 
 }
 
 int pgm_batch_finalize(void *handle) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "batch_finalize: null handle");
   if (h->d_jobs || h->jobs.empty()) return PGM_OK;
@@ -2868,6 +2907,7 @@ int pgm_batch_finalize(void *handle) {
 }
 
 int pgm_batch_run(void *handle, void *stream) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "batch_run: null handle");
   if (h->jobs.empty()) return PGM_OK;
@@ -2878,6 +2918,7 @@ int pgm_batch_run(void *handle, void *stream) {
 }
 
 int pgm_batch_destroy(void *handle) {
+  STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return PGM_OK;
   if (h->d_jobs) (void)hipFree(h->d_jobs);
@@ -2888,6 +2929,7 @@ int pgm_batch_destroy(void *handle) {
 
 int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *out, int64_t s_state, int64_t s_row,
                   int32_t *err_flag, void *stream) {
+  STALE_PROBE();
   if (!codes || !out) return fail(PGM_EINVAL, "indicator: null argument");
   if (n_rows <= 0 || card <= 0) return PGM_OK;
   uint64_t blocks = std::min<uint64_t>((uint64_t)(n_rows * card + 255) / 256, 65535);
@@ -2899,6 +2941,7 @@ int pgm_indicator(const uint8_t *codes, int64_t n_rows, int64_t card, double *ou
 
 int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, int64_t s_elem, int64_t *out_idx,
                int32_t *out_idx32, void *stream) {
+  STALE_PROBE();
   if (!X || (!out_idx && !out_idx32)) return fail(PGM_EINVAL, "argmax: null argument");
   if (n_rows <= 0) return PGM_OK;
   if (row_len <= 0) return fail(PGM_EINVAL, "argmax: empty rows (np.argmax of an empty sequence)");
@@ -2914,6 +2957,7 @@ int pgm_argmax(const double *X, int64_t n_rows, int64_t row_len, int64_t s_row, 
 }
 
 int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream) {
+  STALE_PROBE();
   if (!d || !A || !B || !C || !d->offsets) return fail(PGM_EINVAL, "gemm: null argument");
   if (d->batch < 0 || d->m < 0 || d->n < 0 || d->k < 0) return fail(PGM_EINVAL, "gemm: negative extent");
   if (d->batch == 0 || d->m == 0 || d->n == 0) return PGM_OK;
@@ -2974,6 +3018,7 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
 
 int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32_t *cols, int32_t n_cols,
                      int64_t n_rows, uint8_t *out, void *stream) {
+  STALE_PROBE();
   if (n_cols <= 0 || n_rows <= 0) return PGM_OK;
   if (!codes || !cols || !out) return fail(PGM_EINVAL, "codes_select: null argument");
   if (n_cols > 65535) return fail(PGM_EINVAL, "codes_select: too many columns");
@@ -2986,6 +3031,7 @@ int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32
 }
 
 int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, void **handle) {
+  STALE_PROBE();
   if (!pl || !handle || (!host_values && pl->n_values > 0)) return fail(PGM_EINVAL, "rows_plan_create: null argument");
   *handle = nullptr;
   if (pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP || pl->n_query < 0 || pl->n_query > pl->n_loop ||
@@ -3192,6 +3238,7 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
 }
 
 int pgm_rows_plan_source(const pgm_rows_plan *pl, char *buf, size_t len, size_t *needed) {
+  STALE_PROBE();
   if (!pl) return fail(PGM_EINVAL, "rows_plan_source: null plan");
   if (pl->n_comp < 1 || pl->n_comp > PGM_ROWS_MAX_COMP || pl->n_fac < 0 || pl->n_fac > PGM_ROWS_MAX_FAC ||
       pl->n_ev < 0 || pl->n_ev > PGM_ROWS_MAX_EV || pl->n_loop < 0 || pl->n_loop > PGM_ROWS_MAX_LOOP)
@@ -3211,6 +3258,7 @@ int pgm_rows_plan_source(const pgm_rows_plan *pl, char *buf, size_t len, size_t 
 }
 
 int pgm_rows_plan_destroy(void *handle) {
+  STALE_PROBE();
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
   if (h->d_values) (void)hipFree(h->d_values);
@@ -3312,6 +3360,7 @@ extern "C" {
 int pgm_rows_plan_run(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
                       double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap, int32_t *err_flag,
                       void *stream) {
+  STALE_PROBE();
   return rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag, stream,
                        false);
 }
@@ -3352,6 +3401,7 @@ struct RowsBound {
 int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0,
                        int64_t n_rows, double *marg, double *joint, int64_t ld_out, int32_t *map, double *gap,
                        int32_t *err_flag, void *stream, void **bound) {
+  STALE_PROBE();
   if (!bound) return fail(PGM_EINVAL, "rows_plan_bind: null output pointer");
   *bound = nullptr;
   const int st = rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag,
@@ -3387,6 +3437,7 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
 }
 
 int pgm_rows_bound_run(void *bound) {
+  STALE_PROBE();
   RowsBound *b = (RowsBound *)bound;
   if (!b) return fail(PGM_EINVAL, "rows_bound_run: null handle");
   if (b->fn) {
@@ -3400,6 +3451,7 @@ int pgm_rows_bound_run(void *bound) {
 }
 
 int pgm_rows_bound_destroy(void *bound) {
+  STALE_PROBE();
   delete (RowsBound *)bound;
   return PGM_OK;
 }

@@ -10,12 +10,32 @@ This module replaces the reference's numpy calls (pgmpy/utils/compat_fns.py:
 einsum L63-67, max L53-60, argmax L70-74) with the C-ABI of include/pgmhip.h.
 """
 import ctypes
+import functools
+import threading
 
 import numpy as np
 
 from . import _native as N
 
 ROW = "__row__"  # label of the evidence-row (batch) axis
+
+# SURVEY.md §8(b) threading: the reference calls map_query from joblib threads on one shared
+# object (DiscreteBayesianNetwork.py:871) and ctypes releases the GIL.  A first query of a pattern
+# captures a HIP graph, and HIP rejects work on the legacy stream from another thread while a
+# stream is capturing.  So the public inference entry points (and every capture) run under one
+# process-wide re-entrant lock: the Python side takes a lock, as §8(b) allows.
+device_lock = threading.RLock()
+
+
+def serialized(fn):
+    """Run `fn` holding device_lock (re-entrant: nested public calls are free)."""
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        with device_lock:
+            return fn(*args, **kwargs)
+
+    return wrapper
 
 _REDUCE = {None: N.RED_NONE, "sum": N.RED_SUM, "max": N.RED_MAX}
 _COMBINE = {"mul": N.COMBINE_MUL, "add": N.COMBINE_ADD, "div": N.COMBINE_DIV, "copy": N.COMBINE_COPY,

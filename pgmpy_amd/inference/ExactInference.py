@@ -116,6 +116,7 @@ class VariableElimination(Inference):
         return out
 
     # ------------------------------------------------------------------ queries
+    @E.serialized
     def query(self, variables, evidence=None, virtual_evidence=None, elimination_order="greedy", joint=True,
               show_progress=True):
         """P(variables | evidence) (ExactInference.py:246-457)."""
@@ -211,6 +212,7 @@ class VariableElimination(Inference):
             res[v] = DiscreteFactor([v], [plan.cards[i]], vals[a:a + plan.cards[i]], state_names={v: states[v]})
         return res
 
+    @E.serialized
     def max_marginal(self, variables=None, evidence=None, elimination_order="MinFill", show_progress=True):
         # ExactInference.py:459-526
         if not variables:
@@ -230,6 +232,7 @@ class VariableElimination(Inference):
         return float(E.to_host(E.contract(final._d(), final.variables, None, None, [], reduce="max",
                                           combine="copy")))
 
+    @E.serialized
     def map_query(self, variables=None, evidence=None, virtual_evidence=None, elimination_order="MinFill",
                   show_progress=True):
         """argmax of the joint of `variables` (ExactInference.py:528-624)."""
@@ -285,6 +288,7 @@ class VariableElimination(Inference):
         return max((len(c) for c in nx.find_cliques(g))) - 1
 
     # ------------------------------------------------------------------ batched evidence (new API)
+    @E.serialized
     def query_batch(self, variables, evidence, joint=False):
         """Batched P(variables | evidence row) over a DataFrame of evidence rows.
 
@@ -341,9 +345,11 @@ class BeliefPropagation(Inference):
         for parent, child in order:  # distribute: root -> leaves
             self._update_beliefs(parent, child, operation)
 
+    @E.serialized
     def calibrate(self):
         self._calibrate_junction_tree(operation="marginalize")
 
+    @E.serialized
     def max_calibrate(self):
         self._calibrate_junction_tree(operation="maximize")
 
@@ -392,6 +398,7 @@ class BeliefPropagation(Inference):
             return ve.query(variables=variables, evidence=evidence, joint=joint, show_progress=show_progress)
         return ve.map_query(variables=variables, evidence=evidence, show_progress=show_progress)
 
+    @E.serialized
     def query(self, variables, evidence=None, virtual_evidence=None, joint=True, show_progress=True):
         """P(variables | evidence) via BP (ExactInference.py:1117-1220)."""
         evidence = evidence if evidence is not None else dict()
@@ -415,6 +422,7 @@ class BeliefPropagation(Inference):
             return result.normalize(inplace=False)
         return result
 
+    @E.serialized
     def map_query(self, variables=None, evidence=None, virtual_evidence=None, show_progress=True):
         # ExactInference.py:1222-1317
         variables = [] if variables is None else variables
@@ -439,6 +447,7 @@ class BeliefPropagation(Inference):
         self.model = orig_model
         return final
 
+    @E.serialized
     def calibrate_batch(self, evidence, operation="marginalize"):
         """Batched calibration: one calibration per evidence row.
 
@@ -531,6 +540,7 @@ class BeliefPropagationWithMessagePassing(Inference):
                 incoming_messages.append(msg)
             return self.bp.calc_factor_node_message(factor, incoming_messages, from_variable)
 
+    @E.serialized
     def query(self, variables, evidence=None, virtual_evidence=None, get_messages=False, precomp_messages=None):
         # ExactInference.py:1509-1627
         common_vars = set(evidence if evidence is not None else []).intersection(set(variables))

@@ -18,6 +18,7 @@ from collections import defaultdict
 import networkx as nx
 import numpy as np
 
+from .. import engine as E
 from ..factors.discrete import TabularCPD
 
 logger = logging.getLogger("pgmpy")
@@ -213,6 +214,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         return junction_tree_from_model(self)
 
     # ------------------------------------------------------------------ data-parallel callers
+    @E.serialized
     def predict(self, data, algo=None, stochastic=False, n_jobs=-1, seed=None, **kwargs):
         """MAP of the missing variables per row (DiscreteBayesianNetwork.py:731-910).
 
@@ -234,6 +236,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
             raise NotImplementedError("stochastic=True (sampling from the posterior) is outside the accelerated path")
         return predict_frame(self, data)
 
+    @E.serialized
     def predict_probability(self, data):
         """Per-row marginals of every missing variable (DiscreteBayesianNetwork.py:912-989)."""
         from ..inference.batch import predict_probability_frame

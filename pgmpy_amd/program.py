@@ -311,8 +311,9 @@ class Program:
         for step in self._steps:
             step(s)
 
+    @E.serialized
     def capture(self):
-        """Record the steps into one HIP graph (captured on a private stream)."""
+        """Record the steps into one HIP graph (captured on a private stream, under engine.device_lock)."""
         import torch
 
         if self._graph is not None:
