@@ -137,6 +137,39 @@ class HipTimer:
         return float(ms.value)
 
 
+class Launcher:
+    """The timed launch of a bound fused row plan.  "direct" (default): one AQL dispatch packet per
+    step on a user-mode HSA queue (pgm_dq_launch; kernel time = the queue's dispatch timestamps
+    from the first to the last timed dispatch).  "hip": hipModuleLaunchKernel per step
+    (pgm_rows_bound_run; kernel time = HIP events on the launch stream)."""
+
+    def __init__(self, bound, kind):
+        self.kind = kind
+        if kind == "direct":
+            self.r = bound.direct()
+            self.q = self.r.queue
+        else:
+            self.r = bound
+            self.timer = HipTimer()
+        self.run = self.r.run
+
+    def sync(self):
+        import torch
+
+        if self.kind == "direct":
+            self.q.sync()
+        torch.cuda.synchronize()
+
+    def timer_start(self):
+        if self.kind == "direct":
+            self.q.timer_start()
+        else:
+            self.timer.start()
+
+    def timer_stop_ms(self):
+        return self.q.timer_stop_ms() if self.kind == "direct" else self.timer.stop_ms()
+
+
 def load_traffic(kernel):
     """HBM bytes/launch from a committed rocprofv3 PMC summary (profiles/pmc_<kernel>.json), if present."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
@@ -269,18 +302,19 @@ def bench_c3(args, dist, rank, world):
     # one step = one pass of the fused row plan over the resident batch, launched through the
     # prepared (bound) C-ABI entry: validated and marshalled once, one argument-free call per step
     bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
+    launcher = Launcher(bound, args.launch)
     for _ in range(args.warmup):
-        bound.run()
-    torch.cuda.synchronize()
+        launcher.run()
+    launcher.sync()
     barrier(dist)
-    # HIP events on the launch stream bracketing the timed region: average launch duration
-    # (includes the ~1 us gap between back-to-back launches that rocprofv3's kernel time omits)
-    timer = HipTimer()
-    timer.start()
+    # GPU span of the timed dispatches (queue timestamps or HIP events on the launch stream):
+    # average launch duration, including the gap between back-to-back launches that rocprofv3's
+    # kernel time omits
+    launcher.timer_start()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        bound.run()
-    kern_ms_total = timer.stop_ms()
+        launcher.run()
+    kern_ms_total = launcher.timer_stop_ms()
     torch.cuda.synchronize()
     t_end = time.perf_counter()
     barrier(dist)
@@ -289,6 +323,8 @@ def bench_c3(args, dist, rank, world):
     total_rows = rows * world * args.steps
     value = total_rows / elapsed
     kern_ms = kern_ms_total / args.steps
+    if kern_ms <= 0:  # queue timestamps off (PGM_DQ_PROFILE=0): the wall time per step
+        kern_ms = (t_end - t_start) * 1e3 / args.steps
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
     kname = plan.kernel_name()
@@ -310,7 +346,9 @@ def bench_c3(args, dist, rank, world):
         "data": "synthetic (forward-sampled munin evidence rows, seed 42+rank)",
         "config": {
             "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, "
-                        "fused row plan (pgm_rows_plan_bind / pgm_rows_bound_run)",
+                        "fused row plan (pgm_rows_plan_bind; one launch per step)",
+            "launch": {"direct": "AQL packet on a user-mode HSA queue (pgm_dq_launch)",
+                       "hip": "hipModuleLaunchKernel (pgm_rows_bound_run)"}[args.launch],
             "network": "munin",
             "missing": variables,
             "rows_per_gpu_per_step": rows,
@@ -387,6 +425,7 @@ def bench_c5(args, dist, rank, world):
     out = {"marg": send[:, :rows] if rows else send[:, :1]}
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
+    launcher = Launcher(bound, args.launch)
     nccl = dist is not None and _BACKEND == "nccl"
     recv = None
     if dist is not None and rank == 0:
@@ -397,6 +436,8 @@ def bench_c5(args, dist, rank, world):
     def gather():
         if dist is None:
             return
+        if launcher.kind == "direct":
+            launcher.q.sync()  # the marginals are complete before the collective reads them
         if nccl:
             dist.gather(send, gather_list=recv, dst=0)
         else:  # gloo rehearsal: through host memory
@@ -404,29 +445,30 @@ def bench_c5(args, dist, rank, world):
             dist.gather(host_send, gather_list=recv, dst=0)
 
     def step():
-        bound.run()
+        launcher.run()
         gather()
 
     for _ in range(args.warmup):
         step()
+    launcher.sync()
     barrier(dist)
-    timer = HipTimer()
-    timer.start()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    launcher.sync()
     t_end = time.perf_counter()
-    step_ms_events = timer.stop_ms() / args.steps
     barrier(dist)
     elapsed = max_over_ranks(dist, t_end - t_start)
     assert int(err.item()) == 0
-    # the launch alone (HIP events), then the gather alone, outside the timed region
+    # the launch alone (GPU span of the dispatches), then the gather alone, outside the timed region
     barrier(dist)
-    timer.start()
+    launcher.timer_start()
     for _ in range(args.steps):
-        bound.run()
-    kern_ms = timer.stop_ms() / args.steps
+        launcher.run()
+    kern_ms = launcher.timer_stop_ms() / args.steps
+    if kern_ms <= 0:
+        kern_ms = elapsed * 1e3 / args.steps
+    launcher.sync()
     barrier(dist)
     g0 = time.perf_counter()
     for _ in range(args.steps):
@@ -466,12 +508,12 @@ def bench_c5(args, dist, rank, world):
         "config": {"workload": "C5 munin predict_probability template, 1M rows per step sharded over the ranks "
                                "+ gather of the marginals to rank 0",
                    "network": "munin", "missing": variables, "global_rows_per_step": total,
+                   "launch": args.launch,
                    "rows_per_gpu_per_step": rows, "parallelism": f"rows sharded over {world} rank(s), "
                    f"{_BACKEND if dist is not None else 'no'} gather to rank 0"},
         "gather_ms": gather_ms if dist is not None else 0.0,
         "gather_backend": _BACKEND if dist is not None else None,
         "gather_bytes_to_rank0": 8 * plan.n_acc * block * (world - 1),
-        "step_ms_events_rank0": step_ms_events,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": plan.kernel_name(),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows},
@@ -624,6 +666,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    ap.add_argument("--launch", default="direct", choices=["direct", "hip"],
+                    help="c3/c5: AQL packets on a user-mode HSA queue (direct) or hipModuleLaunchKernel (hip)")
     args = ap.parse_args()
     if args.rows is None:
         args.rows = {"c3": 100_000, "c5": 1_000_000}.get(args.workload, 1000)

@@ -330,6 +330,25 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
 int pgm_rows_bound_run(void *bound);
 int pgm_rows_bound_destroy(void *bound);
 
+/* Direct AQL dispatch (pgmpy_amd/csrc/pgmdq.cpp).  A user-mode HSA queue on the GPU agent of a HIP
+ * device; a bound launch of the plan-specialised kernel (pgm_rows_plan_bind) is re-bound to it and
+ * each pgm_dq_launch writes one kernel-dispatch packet (barrier bit set) and rings the doorbell — no
+ * HIP runtime on the launch path.  Same kernel, same arguments, same results as pgm_rows_bound_run.
+ * Ordering: pgm_dq_bind_rows waits for the device (inputs complete); dispatches on one queue run in
+ * order; inputs may change only between pgm_dq_sync and the next launch (HIP writes complete); call
+ * pgm_dq_sync (a system-scope release barrier + wait) before HIP work reads the outputs.  The timer reports
+ * the GPU span (queue profiling timestamps) from the first dispatch after pgm_dq_timer_start to the
+ * last one issued.  The queue must outlive its bound launches.  Serves the same caller as
+ * pgm_rows_bound_run (pgmpy/models/DiscreteBayesianNetwork.py:867-910, repeated batches). */
+int pgm_dq_create(int hip_device, void **dq);
+int pgm_dq_destroy(void *dq);
+int pgm_dq_bind_rows(void *dq, void *bound, void **dbound);
+int pgm_dq_launch(void *dbound);
+int pgm_dq_sync(void *dq);
+int pgm_dq_timer_start(void *dq);
+int pgm_dq_timer_stop_ms(void *dq, float *ms);
+int pgm_dq_bound_destroy(void *dbound);
+
 #ifdef __cplusplus
 }
 #endif

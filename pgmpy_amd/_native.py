@@ -183,6 +183,14 @@ _SIGS = {
     "pgm_rows_plan_source": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
                              ctypes.c_int),
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
+    "pgm_dq_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "pgm_dq_destroy": ([_P], ctypes.c_int),
+    "pgm_dq_bind_rows": ([_P, _P, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "pgm_dq_launch": ([_P], ctypes.c_int),
+    "pgm_dq_sync": ([_P], ctypes.c_int),
+    "pgm_dq_timer_start": ([_P], ctypes.c_int),
+    "pgm_dq_timer_stop_ms": ([_P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "pgm_dq_bound_destroy": ([_P], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -552,10 +552,95 @@ class BoundRows:
             N.check(st, "rows_bound_run")
         return self.out
 
+    def direct(self, queue=None):
+        """The same launch dispatched on a DirectQueue (pgm_dq_bind_rows): one AQL packet per
+        run(), no HIP runtime on the launch path.  Needs the plan-specialised kernel."""
+        return DirectRows(self, queue or DirectQueue.default())
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             try:
                 N.load_library().pgm_rows_bound_destroy(h)
+            except Exception:
+                pass
+
+
+class DirectQueue:
+    """A user-mode HSA queue on the current HIP device (pgm_dq_create, pgmpy_amd/csrc/pgmdq.cpp).
+    Dispatches on it run in order; sync() before HIP work reads their outputs."""
+
+    _default = {}
+
+    def __init__(self, device=None):
+        import ctypes
+
+        import torch
+
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        N.check(N.lib().pgm_dq_create(self.device, ctypes.byref(h)), "dq_create")
+        self._h = h
+
+    @classmethod
+    def default(cls):
+        import torch
+
+        d = torch.cuda.current_device()
+        q = cls._default.get(d)
+        if q is None:
+            q = cls._default[d] = cls(d)
+        return q
+
+    def sync(self):
+        N.check(N.lib().pgm_dq_sync(self._h), "dq_sync")
+
+    def timer_start(self):
+        N.check(N.lib().pgm_dq_timer_start(self._h), "dq_timer_start")
+
+    def timer_stop_ms(self):
+        import ctypes
+
+        ms = ctypes.c_float()
+        N.check(N.lib().pgm_dq_timer_stop_ms(self._h, ctypes.byref(ms)), "dq_timer_stop")
+        return float(ms.value)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.load_library().pgm_dq_destroy(h)
+            except Exception:
+                pass
+
+
+class DirectRows:
+    """A bound row-plan launch re-bound to a DirectQueue (pgm_dq_bind_rows / pgm_dq_launch)."""
+
+    def __init__(self, bound, queue):
+        import ctypes
+
+        self._keep = (bound, queue)
+        self.queue = queue
+        self.out = bound.out
+        h = ctypes.c_void_p()
+        N.check(N.lib().pgm_dq_bind_rows(queue._h, bound._h, ctypes.byref(h)), "dq_bind_rows")
+        self._h = h
+        self._launch = N.lib().pgm_dq_launch
+
+    def run(self):
+        st = self._launch(self._h)
+        if st != 0:
+            N.check(st, "dq_launch")
+        return self.out
+
+    def sync(self):
+        self.queue.sync()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.load_library().pgm_dq_bound_destroy(h)
             except Exception:
                 pass

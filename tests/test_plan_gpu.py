@@ -144,6 +144,77 @@ def test_bound_rows_launch_matches_run(gpu):
                                                           device=d.device)})
 
 
+@pytest.mark.parametrize("rows", [1000, 100_000, 1_000_000])
+def test_direct_queue_launch_matches_bound(gpu, rows):
+    """pgm_dq_bind_rows / pgm_dq_launch (the AQL-packet launch of the same specialised kernel on a
+    user-mode HSA queue) writes bit-for-bit what the HIP-launched bound run writes, including after
+    many back-to-back dispatches (the completion-signal ring wraps) and on new codes in place; the
+    queue timer reports a positive GPU span."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import DirectQueue, PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    codes, nodes = forward_sample_codes(m, rows, seed=11)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+    plan.bind(d, rows, 0, rows, ref).run()
+    torch.cuda.synchronize()
+    out = plan.alloc_outputs(rows, marginals=True, map_=True)
+    q = DirectQueue()
+    direct = plan.bind(d, rows, 0, rows, out).direct(q)
+    q.timer_start()
+    for _ in range(300):  # > the 256-signal ring
+        direct.run()
+    ms = q.timer_stop_ms()
+    q.sync()
+    assert ms > 0.0
+    assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    d.copy_(upload_codes(np.ascontiguousarray(ev[:, ::-1])))  # new evidence in the same buffer
+    torch.cuda.synchronize()
+    out["marg"].zero_()
+    torch.cuda.synchronize()
+    direct.run()
+    direct.sync()
+    plan.bind(d, rows, 0, rows, ref).run()
+    torch.cuda.synchronize()
+    assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+
+
+def test_direct_queue_needs_specialised_kernel(gpu):
+    """A bound launch that runs an AOT kernel (no hipRTC code object) cannot be re-bound to the
+    direct queue: ValueError, nothing dispatched."""
+    import random
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    codes, nodes = forward_sample_codes(m, 256, seed=12)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    plan.extra_mode = N.ROWS_GENERIC
+    d = upload_codes(np.ascontiguousarray(codes[[pos[v] for v in obs]]))
+    bound = plan.bind(d, 256, 0, 256, plan.alloc_outputs(256, marginals=True))
+    with pytest.raises(ValueError):
+        bound.direct()
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_specialised_kernel_bit_identical(gpu, seed):
     """The plan-specialised (hipRTC) row kernel agrees with the AOT kernels (k_rows_affine and the
