@@ -166,6 +166,18 @@ typedef struct {
 
 int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C, void *stream);
 
+/* Evidence ingestion: per-column int8 category indices raw[col * ld_raw + row]
+ * (pandas Categorical codes / Arrow dictionary indices, -1 = NaN) -> uint8 state codes
+ * out[col * ld_out + row] through a per-column LUT lut[col * lut_stride + category] (254 marks a
+ * category that is not a state name: err_flag is set), 255 for NaN.  When row_key is given (zeroed
+ * by the caller, with row_nmiss), row_key[row] ^= col_key[col] and row_nmiss[row] += 1 for every
+ * missing column: the row's evidence-pattern key, from which predict() groups rows.  Replaces the
+ * per-cell state-name lookups of the reference (state_name.py:71-84 via DiscreteFactor.py:589-597,
+ * called per row from DiscreteBayesianNetwork.py:871-878 / :974-979). */
+int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n_rows, const uint8_t *lut,
+                    int32_t lut_stride, const uint64_t *col_key, uint8_t *out, int64_t ld_out, uint64_t *row_key,
+                    uint32_t *row_nmiss, int32_t *err_flag, void *stream);
+
 /* ---------------------------------------------------------------- evidence column select
  * out[j * n_rows + r] = codes[cols[j] * ld + row0 + r]: copies the evidence columns a compiled
  * plan reads into its own fixed buffer (so the captured graph never sees caller pointers).

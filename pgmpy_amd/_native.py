@@ -183,6 +183,8 @@ _SIGS = {
     "pgm_rows_plan_source": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
                              ctypes.c_int),
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
+    "pgm_codes_remap": ([_P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32, _P, _P,
+                         ctypes.c_int64, _P, _P, _P, _P], ctypes.c_int),
     "pgm_dq_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "pgm_dq_destroy": ([_P], ctypes.c_int),
     "pgm_dq_bind_rows": ([_P, _P, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),

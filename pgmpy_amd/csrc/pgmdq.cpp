@@ -53,6 +53,7 @@ struct DirectQueue {
   // none: its output lines are past the L2 when it completes); pgm_dq_sync ends with one
   // system-scope release barrier packet.  PGM_DQ_ACQ / PGM_DQ_REL override (A/B knobs).
   uint16_t acq_scope = HSA_FENCE_SCOPE_NONE;
+  uint16_t fresh_acq_scope = HSA_FENCE_SCOPE_SYSTEM;
   int rel_override = -1;
   bool fresh = true;          // next dispatch is the first since bind/sync
   bool need_release = false;  // dispatches since the last system-scope release
@@ -247,6 +248,7 @@ int pgm_dq_create(int hip_device, void **out) {
     return dflt;
   };
   dq->acq_scope = scope_env("PGM_DQ_ACQ", dq->acq_scope);
+  dq->fresh_acq_scope = scope_env("PGM_DQ_FRESH_ACQ", dq->fresh_acq_scope);
   if (getenv("PGM_DQ_REL")) dq->rel_override = scope_env("PGM_DQ_REL", HSA_FENCE_SCOPE_AGENT);
   *out = dq;
   return PGM_OK;
@@ -416,7 +418,7 @@ int pgm_dq_launch(void *dbound) {
   pkt->kernarg_address = db->kernarg;
   pkt->reserved2 = 0;
   pkt->completion_signal = sig;
-  const uint16_t acq = dq->fresh ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : dq->acq_scope;
+  const uint16_t acq = dq->fresh ? dq->fresh_acq_scope : dq->acq_scope;
   dq->fresh = false;
   dq->need_release = dq->need_release || db->rel_scope != HSA_FENCE_SCOPE_SYSTEM;
   dq->last_kernel = dq->issued;

@@ -1562,6 +1562,51 @@ __global__ __launch_bounds__(256) void k_codes_select(const uint8_t *__restrict_
   if (r < n_rows) out[(int64_t)j * n_rows + r] = codes[(int64_t)cols[j] * ld + row0 + r];
 }
 
+// ----------------------------------------------------------------------------- evidence ingestion
+// DataFrame columns -> evidence codes (the reference maps each state name with
+// name_to_no per row and evidence variable, state_name.py:71-84, DiscreteFactor.py:589-597).  Input:
+// per-column int8 indices into that column's categories (pandas Categorical / Arrow dictionary
+// indices, -1 = NaN); a per-column LUT maps a category index to the variable's state number (254 =
+// a category that is not a state name of the variable).  Output: uint8 state codes (255 = NaN) and,
+// per row, the key of its missing-column pattern (XOR of the missing columns' 64-bit keys) and its
+// number of missing columns, from which the host groups rows by evidence pattern.  One thread per
+// row over a chunk of columns (blockIdx.y); byte accesses along the rows are coalesced.
+__global__ __launch_bounds__(256) void k_codes_remap(const int8_t *__restrict__ raw, int64_t ld_raw,
+                                                     const uint8_t *__restrict__ lut, int32_t lut_stride,
+                                                     int32_t n_cols, int64_t n_rows, int32_t chunk,
+                                                     const uint64_t *__restrict__ col_key, uint8_t *__restrict__ out,
+                                                     int64_t ld_out, unsigned long long *__restrict__ row_key,
+                                                     uint32_t *__restrict__ row_nmiss, int32_t *__restrict__ err) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rows) return;
+  const int c0 = blockIdx.y * chunk;
+  const int c1 = min(n_cols, c0 + chunk);
+  unsigned long long key = 0;
+  uint32_t nm = 0;
+  bool bad = false;
+  for (int c = c0; c < c1; ++c) {
+    const int v = raw[(int64_t)c * ld_raw + r];
+    uint8_t st;
+    if (v < 0) {
+      st = 255;
+      key ^= col_key[c];
+      ++nm;
+    } else if (v >= lut_stride) {
+      st = 254;
+      bad = true;
+    } else {
+      st = lut[(int64_t)c * lut_stride + v];
+      bad |= st == 254;
+    }
+    out[(int64_t)c * ld_out + r] = st;
+  }
+  if (nm && row_key) {
+    atomicXor(&row_key[r], key);
+    atomicAdd(&row_nmiss[r], nm);
+  }
+  if (bad && err) atomicOr(err, 1);
+}
+
 // ----------------------------------------------------------------------------- fused row plan
 // One workgroup owns 64 evidence rows (one per lane) for RG consecutive row groups; its waves split
 // the plan's independent components (wave w takes components w, w+W, ...), so every descriptor
@@ -3069,6 +3114,28 @@ int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32
   if (bx > 0x7fffffffull) return fail(PGM_EINVAL, "codes_select: too many rows");
   hipLaunchKernelGGL(k_codes_select, dim3((unsigned)bx, (unsigned)n_cols), dim3(256), 0, S(stream), codes, ld, row0,
                      cols, n_rows, out);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n_rows, const uint8_t *lut,
+                    int32_t lut_stride, const uint64_t *col_key, uint8_t *out, int64_t ld_out, uint64_t *row_key,
+                    uint32_t *row_nmiss, int32_t *err_flag, void *stream) {
+  STALE_PROBE();
+  if (n_cols <= 0 || n_rows <= 0) return PGM_OK;
+  if (!raw || !lut || !out || (row_key && (!row_nmiss || !col_key)))
+    return fail(PGM_EINVAL, "codes_remap: null argument");
+  if (ld_raw < n_rows || ld_out < n_rows || lut_stride < 1 || lut_stride > 256)
+    return fail(PGM_EINVAL, "codes_remap: bad leading dimension or LUT stride");
+  const uint64_t bx = ((uint64_t)n_rows + 255) / 256;
+  if (bx > 0x7fffffffull) return fail(PGM_EINVAL, "codes_remap: too many rows");
+  // enough (row block x column chunk) workgroups to fill the chip, each chunk >= 16 columns
+  int chunks = 1;
+  while (chunks < 64 && bx * chunks < 2048 && n_cols / (chunks * 2) >= 16) chunks *= 2;
+  const int chunk = (n_cols + chunks - 1) / chunks;
+  hipLaunchKernelGGL(k_codes_remap, dim3((unsigned)bx, (unsigned)chunks), dim3(256), 0, S(stream), raw, ld_raw, lut,
+                     lut_stride, n_cols, n_rows, chunk, col_key, out, ld_out, (unsigned long long *)row_key, row_nmiss,
+                     err_flag);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

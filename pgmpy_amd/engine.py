@@ -79,6 +79,19 @@ def to_device_i64(arr):
     return t
 
 
+def to_device_raw(arr):
+    """Host numpy array of any fixed-size dtype -> device tensor of the same dtype and shape."""
+    torch = _torch()
+    a = np.ascontiguousarray(arr)
+    dt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int8): torch.int8, np.dtype(np.int32): torch.int32,
+          np.dtype(np.int64): torch.int64, np.dtype(np.float64): torch.float64}[a.dtype]
+    t = torch.empty(a.shape, dtype=dt, device=device())
+    if a.size:
+        N.check(N.lib().pgm_memcpy_h2d(N.ptr(t), a.ctypes.data_as(ctypes.c_void_p), a.nbytes, N.stream_handle()),
+                "memcpy_h2d")
+    return t
+
+
 def to_host(t):
     """Device tensor -> numpy (C-order copy of its logical contents)."""
     L = N.lib()

@@ -81,6 +81,133 @@ def encode_frame(model, data, columns=None):
     return codes
 
 
+_COL_KEY_SEED = 0x5eed_cafe  # fixed: pattern keys are comparable across calls
+
+
+class Evidence:
+    """A DataFrame's evidence on the device: uint8 state codes [n_cols, n] (255 = NaN) and the rows
+    grouped by evidence pattern, [(observed column mask, row indices)]."""
+
+    def __init__(self, codes, groups, n):
+        self.codes, self.groups, self.n = codes, groups, n
+
+    def rows_codes(self, rows):
+        """Device codes of a subset of rows (one evidence pattern), [n_cols, len(rows)]."""
+        import torch
+
+        if len(rows) == self.n:
+            return self.codes
+        idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=self.codes.device)
+        return self.codes.index_select(1, idx).contiguous()
+
+
+def _column_raw(v, st, col):
+    """(int8 raw indices, LUT) of one column: pandas Categorical codes and a category -> state LUT,
+    or, for any other dtype, the state numbers themselves (one host hash pass) and the identity LUT.
+    None when the column does not fit int8 indices (the host encoder handles the frame)."""
+    import pandas as pd
+
+    if isinstance(v.dtype, pd.CategoricalDtype):
+        cats = np.asarray(v.cat.categories, dtype=object)
+        raw = v.cat.codes.to_numpy()
+        if raw.dtype != np.int8 or len(cats) > 127:
+            return None
+        lut = _lookup_codes(cats, st) if len(cats) else np.zeros(0, dtype=np.int64)
+        miss = np.nonzero(lut < 0)[0]
+        if len(miss):  # the reference's str() fallback per category; 254 = not a state name
+            sm = {str(x): i for i, x in enumerate(st)}
+            for i in miss:
+                lut[i] = sm.get(str(cats[i]), 254)
+        return raw, lut.astype(np.uint8)
+    if len(st) > 127:
+        return None
+    vals = v.to_numpy(dtype=object)
+    c = _lookup_codes(vals, st)
+    miss = np.nonzero(c < 0)[0]
+    if len(miss):
+        sub = vals[miss]
+        na = pd.isna(sub)
+        c[miss[na]] = -1
+        rest = miss[~na]
+        if len(rest):
+            sm = {str(x): i for i, x in enumerate(st)}
+            for i in rest:
+                k = sm.get(str(vals[i]))
+                if k is None:
+                    raise KeyError(f"state: {vals[i]} is an unknown for variable: {col}. It must be one of {st}")
+                c[i] = k
+    return c.astype(np.int8), np.arange(len(st), dtype=np.uint8)
+
+
+def ingest_frame(model, data, columns=None):
+    """Evidence of a DataFrame on the device.
+
+    Host: per column, its int8 category indices (pandas Categorical codes, zero-copy of the frame's
+    own codes) or one hash pass for object columns, into a pinned [n_cols, n] buffer, plus a small
+    category -> state LUT.  Device (pgm_codes_remap): one pass maps every cell to its uint8 state
+    code and keys each row by its missing-column pattern; the host groups rows by (key, count)
+    from 12 B per row.  Falls back to the host encoder (encode_frame) for variables with > 127
+    states or categoricals with > 127 categories."""
+    import torch
+
+    columns = list(data.columns) if columns is None else list(columns)
+    states = model.states
+    n = len(data)
+    nc = len(columns)
+    raws, luts = [], []
+    for col in columns:
+        st = list(states[col])
+        if len(st) >= MISSING:
+            raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
+        r = _column_raw(data[col], st, col)
+        if r is None:
+            codes = encode_frame(model, data, columns)
+            return Evidence(upload_codes(codes), group_patterns(codes), n)
+        raws.append(r[0])
+        luts.append(r[1])
+    L = N.lib()
+    dev = E.device()
+    s = N.stream_handle()
+    h_raw = torch.empty((nc, n), dtype=torch.int8, pin_memory=True)
+    hr = h_raw.numpy()
+    for j, r in enumerate(raws):
+        hr[j] = r
+    lut = np.full((nc, 128), 254, dtype=np.uint8)
+    for j, t in enumerate(luts):
+        lut[j, :len(t)] = t
+    keys = np.random.default_rng(_COL_KEY_SEED).integers(1, 2 ** 63, size=max(nc, 1), dtype=np.int64)
+    d_raw = torch.empty((nc, n), dtype=torch.int8, device=dev)
+    d_codes = torch.empty((nc, n), dtype=torch.uint8, device=dev)
+    d_lut = E.to_device_raw(lut)
+    d_key = E.to_device_raw(keys)
+    d_rk = torch.zeros(n, dtype=torch.int64, device=dev)
+    d_nm = torch.zeros(n, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if n and nc:
+        N.check(L.pgm_memcpy_h2d(N.ptr(d_raw), ctypes.c_void_p(h_raw.data_ptr()), h_raw.numel(), s), "memcpy_h2d")
+        N.check(L.pgm_codes_remap(N.ptr(d_raw), n, nc, n, N.ptr(d_lut), 128, N.ptr(d_key), N.ptr(d_codes), n,
+                                  N.ptr(d_rk), N.ptr(d_nm), N.ptr(err), s), "codes_remap")
+    nm = download(d_nm)
+    if int(download(err)[0]):
+        encode_frame(model, data, columns)  # raises the reference's KeyError for the offending cell
+        raise KeyError("evidence holds a category that is not a state name")
+    if not nm.any():
+        groups = [(np.ones(nc, dtype=bool), np.arange(n))]
+    else:
+        rk = download(d_rk)
+        pair = np.stack([rk, nm.astype(np.int64)], axis=1)
+        _, first, inv = np.unique(pair, axis=0, return_index=True, return_inverse=True)
+        inv = inv.reshape(-1)
+        order = np.argsort(inv, kind="stable")
+        bounds = np.searchsorted(inv[order], np.arange(len(first) + 1))
+        groups = []
+        for g in range(len(first)):
+            rows = order[bounds[g]:bounds[g + 1]]
+            groups.append((hr[:, rows[0]] >= 0, rows))
+        groups.sort(key=lambda gr: gr[1][0])
+    return Evidence(d_codes, groups, n)
+
+
 def upload_codes(codes):
     """Host uint8 [n_cols, n] -> device (through pgm_memcpy_h2d)."""
     import torch
@@ -153,14 +280,13 @@ def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars):
     """Yield (plan, rows, outputs-on-host) per evidence pattern."""
     columns = list(data.columns)
     col_of = {c: i for i, c in enumerate(columns)}
-    codes = encode_frame(model, data, columns)
-    for mask, rows in group_patterns(codes):
+    ev = ingest_frame(model, data, columns)
+    for mask, rows in ev.groups:
         observed = [columns[j] for j in range(len(columns)) if mask[j]]
         nan_cols = [columns[j] for j in range(len(columns)) if not mask[j]]
         variables = list(base_vars) + ([c for c in nan_cols if c not in base_vars] if extra_nan_vars else [])
         plan = get_plan(model, variables, observed, col_of)
-        sub = codes if len(rows) == codes.shape[1] else codes[:, rows]
-        dcodes = upload_codes(sub)
+        dcodes = ev.rows_codes(rows)
         n = len(rows)
         out = plan.alloc_outputs(n, marginals=want_marg, map_=want_map)
         err = None
@@ -200,7 +326,9 @@ def predict_frame(model, data):
     missing_variables = set(model.nodes()) - set(data.columns)
     order = list(missing_variables)
     vals = {c: np.full(len(data), np.nan, dtype=object) for c in order}
-    base = data.astype(object, copy=False)  # no copy when every column already holds objects
+    # the observed columns keep their dtype (object frames stay object, as the reference's merge
+    # leaves them; a categorical frame is not expanded to 10^8 Python objects)
+    base = data
     filled = {}  # observed columns whose NaN cells receive MAP states, as in the reference
     for plan, rows, host in _run_groups(model, data, order, False, True, True):
         idx = host["map"].astype(np.int64)
@@ -237,14 +365,13 @@ def query_batch(model, variables, evidence, joint=False):
         res = {v: np.empty((n, c)) for v, c in zip(variables, cards)}
     columns = list(evidence.columns)
     col_of = {c: i for i, c in enumerate(columns)}
-    codes = encode_frame(model, evidence, columns)
+    ev = ingest_frame(model, evidence, columns)
     import torch
 
-    for mask, rows in group_patterns(codes):
+    for mask, rows in ev.groups:
         observed = [columns[j] for j in range(len(columns)) if mask[j]]
         plan = get_plan(model, list(variables), observed, col_of)
-        sub = codes if len(rows) == codes.shape[1] else codes[:, rows]
-        dcodes = upload_codes(sub)
+        dcodes = ev.rows_codes(rows)
         m = len(rows)
         out = plan.alloc_outputs(m, marginals=not joint, joint=joint)
         err = torch.zeros(1, dtype=torch.int32, device=dcodes.device)
