@@ -102,14 +102,26 @@ class Evidence:
 
 
 def _column_raw(v, st, col):
-    """(int8 raw indices, LUT) of one column: pandas Categorical codes and a category -> state LUT,
-    or, for any other dtype, the state numbers themselves (one host hash pass) and the identity LUT.
+    """(int8 raw indices, LUT) of one column: pandas Categorical codes or Arrow dictionary indices
+    and a category -> state LUT, or, for any other dtype, the state numbers themselves (one host hash
+    pass) and the identity LUT.
     None when the column does not fit int8 indices (the host encoder handles the frame)."""
     import pandas as pd
 
+    cats = raw = None
     if isinstance(v.dtype, pd.CategoricalDtype):
         cats = np.asarray(v.cat.categories, dtype=object)
         raw = v.cat.codes.to_numpy()
+    elif isinstance(v.dtype, pd.ArrowDtype):
+        import pyarrow as pa
+
+        if pa.types.is_dictionary(v.dtype.pyarrow_dtype):  # Arrow dictionary-encoded column
+            da = v.array.__arrow_array__().unify_dictionaries().combine_chunks()
+            if not pa.types.is_int8(da.indices.type):
+                return None
+            cats = np.asarray(da.dictionary.to_pylist(), dtype=object)
+            raw = np.asarray(da.indices.fill_null(-1).to_numpy(zero_copy_only=False), dtype=np.int8)
+    if raw is not None:
         if raw.dtype != np.int8 or len(cats) > 127:
             return None
         lut = _lookup_codes(cats, st) if len(cats) else np.zeros(0, dtype=np.int64)
