@@ -29,7 +29,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 9  // 9: pgm_gemm_desc.lane_order, pgm_batch_add_product_n / _indicator
+#define PGM_ABI_VERSION 10  // 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 9
+    assert lib.pgm_version() == 10
 
 
 def test_struct_layouts_match_header():
@@ -265,3 +265,23 @@ def test_program_dependency_levels():
     for f in prog._steps:
         f(None)
     assert ran == ["w_a", "w_b", "r_ab_w_c", "w_d", "inplace_c", "w_a_view"]
+
+
+def test_hip_backend_config_mirrors_pgmpy_config():
+    """pgmpy_amd.compat.Config: pgmpy's set_backend validation (global_vars.py:82-122) plus "hip";
+    without a device the hip backend fails loudly (no CPU fallback)."""
+    from pgmpy_amd import compat
+    from pgmpy_amd._native import NativeUnavailable
+
+    cfg = compat.Config()
+    assert cfg.get_backend() == "numpy" and cfg.get_dtype() == "float64"
+    with pytest.raises(ValueError):
+        cfg.set_backend("jax")
+    import torch
+
+    if not torch.cuda.is_available():
+        with pytest.raises(NativeUnavailable):
+            cfg.set_backend("hip")
+        assert compat.get_compute_backend() is np  # module config untouched
+    cfg.set_backend("numpy")
+    assert cfg.get_device() is None
