@@ -171,12 +171,21 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
  * out[col * ld_out + row] through a per-column LUT lut[col * lut_stride + category] (254 marks a
  * category that is not a state name: err_flag is set), 255 for NaN.  When row_key is given (zeroed
  * by the caller, with row_nmiss), row_key[row] ^= col_key[col] and row_nmiss[row] += 1 for every
- * missing column: the row's evidence-pattern key, from which predict() groups rows.  Replaces the
+ * missing column: the row's evidence-pattern key, from which predict() groups rows.  When row_hash
+ * is given (zeroed, 2 x uint64 per row) it receives a 128-bit hash of the row's codes (predict's
+ * de-duplication of identical rows, DiscreteBayesianNetwork.py:867-870).  Replaces the
  * per-cell state-name lookups of the reference (state_name.py:71-84 via DiscreteFactor.py:589-597,
  * called per row from DiscreteBayesianNetwork.py:871-878 / :974-979). */
 int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n_rows, const uint8_t *lut,
                     int32_t lut_stride, const uint64_t *col_key, uint8_t *out, int64_t ld_out, uint64_t *row_key,
-                    uint32_t *row_nmiss, int32_t *err_flag, void *stream);
+                    uint32_t *row_nmiss, uint64_t *row_hash, int32_t *err_flag, void *stream);
+
+/* predict(stochastic=True): for each output row r, numpy's Generator.choice over the joint column
+ * joint[i * ld + group[r]] (i < P): cdf = cumsum(p); cdf /= cdf[-1]; out_idx[r] = searchsorted(cdf,
+ * u[r], "right") (DiscreteFactor.sample, DiscreteFactor.py:868-912, called per unique evidence row at
+ * DiscreteBayesianNetwork.py:889-892).  u: the uniforms of the reference's seeded stream. */
+int pgm_sample_joint(const double *joint, int64_t ld, int64_t P, const int32_t *group, const double *u, int64_t n,
+                     int32_t *out_idx, void *stream);
 
 /* ---------------------------------------------------------------- evidence column select
  * out[j * n_rows + r] = codes[cols[j] * ld + row0 + r]: copies the evidence columns a compiled

@@ -184,7 +184,8 @@ _SIGS = {
                              ctypes.c_int),
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
     "pgm_codes_remap": ([_P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32, _P, _P,
-                         ctypes.c_int64, _P, _P, _P, _P], ctypes.c_int),
+                         ctypes.c_int64, _P, _P, _P, _P, _P], ctypes.c_int),
+    "pgm_sample_joint": ([_P, ctypes.c_int64, ctypes.c_int64, _P, _P, ctypes.c_int64, _P, _P], ctypes.c_int),
     "pgm_dq_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "pgm_dq_destroy": ([_P], ctypes.c_int),
     "pgm_dq_bind_rows": ([_P, _P, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),

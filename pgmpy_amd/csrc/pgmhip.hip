@@ -1562,6 +1562,12 @@ __global__ __launch_bounds__(256) void k_codes_select(const uint8_t *__restrict_
   if (r < n_rows) out[(int64_t)j * n_rows + r] = codes[(int64_t)cols[j] * ld + row0 + r];
 }
 
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
 // ----------------------------------------------------------------------------- evidence ingestion
 // DataFrame columns -> evidence codes (the reference maps each state name with
 // name_to_no per row and evidence variable, state_name.py:71-84, DiscreteFactor.py:589-597).  Input:
@@ -1576,12 +1582,14 @@ __global__ __launch_bounds__(256) void k_codes_remap(const int8_t *__restrict__ 
                                                      int32_t n_cols, int64_t n_rows, int32_t chunk,
                                                      const uint64_t *__restrict__ col_key, uint8_t *__restrict__ out,
                                                      int64_t ld_out, unsigned long long *__restrict__ row_key,
-                                                     uint32_t *__restrict__ row_nmiss, int32_t *__restrict__ err) {
+                                                     uint32_t *__restrict__ row_nmiss,
+                                                     unsigned long long *__restrict__ row_hash,
+                                                     int32_t *__restrict__ err) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= n_rows) return;
   const int c0 = blockIdx.y * chunk;
   const int c1 = min(n_cols, c0 + chunk);
-  unsigned long long key = 0;
+  unsigned long long key = 0, h0 = 0, h1 = 0;
   uint32_t nm = 0;
   bool bad = false;
   for (int c = c0; c < c1; ++c) {
@@ -1599,12 +1607,44 @@ __global__ __launch_bounds__(256) void k_codes_remap(const int8_t *__restrict__ 
       bad |= st == 254;
     }
     out[(int64_t)c * ld_out + r] = st;
+    if (row_hash) {  // row content: XOR of two independent mixes of (column, state)
+      const unsigned long long x = ((unsigned long long)c << 8) | st;
+      h0 ^= mix64(x ^ 0x9e3779b97f4a7c15ull);
+      h1 ^= mix64(x ^ 0xc2b2ae3d27d4eb4full);
+    }
   }
   if (nm && row_key) {
     atomicXor(&row_key[r], key);
     atomicAdd(&row_nmiss[r], nm);
   }
+  if (row_hash) {
+    atomicXor(&row_hash[2 * r], h0);
+    atomicXor(&row_hash[2 * r + 1], h1);
+  }
   if (bad && err) atomicOr(err, 1);
+}
+
+// predict(stochastic=True) (DiscreteBayesianNetwork.py:889-892 -> DiscreteFactor.sample L868-912):
+// numpy's Generator.choice(P, p=joint) for each output row r: cdf = cumsum(p); cdf /= cdf[-1];
+// index = searchsorted(cdf, u[r], side="right") — the same sequential sums, the uniforms u drawn on
+// the host from the reference's seeded stream.  joint column group[r] (a deduplicated evidence row).
+__global__ __launch_bounds__(256) void k_sample_joint(const double *__restrict__ joint, int64_t ld, int64_t P,
+                                                      const int32_t *__restrict__ group,
+                                                      const double *__restrict__ u, int64_t n,
+                                                      int32_t *__restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const double *p = joint + group[r];
+  double total = 0.0;
+  for (int64_t i = 0; i < P; ++i) total += p[i * ld];
+  const double x = u[r];
+  double acc = 0.0;
+  int64_t idx = 0;
+  for (int64_t i = 0; i < P; ++i) {
+    acc += p[i * ld];
+    if (acc / total <= x) idx = i + 1;
+  }
+  out[r] = (int32_t)(idx < P ? idx : P - 1);
 }
 
 // ----------------------------------------------------------------------------- fused row plan
@@ -3120,7 +3160,7 @@ int pgm_codes_select(const uint8_t *codes, int64_t ld, int64_t row0, const int32
 
 int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n_rows, const uint8_t *lut,
                     int32_t lut_stride, const uint64_t *col_key, uint8_t *out, int64_t ld_out, uint64_t *row_key,
-                    uint32_t *row_nmiss, int32_t *err_flag, void *stream) {
+                    uint32_t *row_nmiss, uint64_t *row_hash, int32_t *err_flag, void *stream) {
   STALE_PROBE();
   if (n_cols <= 0 || n_rows <= 0) return PGM_OK;
   if (!raw || !lut || !out || (row_key && (!row_nmiss || !col_key)))
@@ -3135,7 +3175,19 @@ int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n
   const int chunk = (n_cols + chunks - 1) / chunks;
   hipLaunchKernelGGL(k_codes_remap, dim3((unsigned)bx, (unsigned)chunks), dim3(256), 0, S(stream), raw, ld_raw, lut,
                      lut_stride, n_cols, n_rows, chunk, col_key, out, ld_out, (unsigned long long *)row_key, row_nmiss,
-                     err_flag);
+                     (unsigned long long *)row_hash, err_flag);
+  HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_sample_joint(const double *joint, int64_t ld, int64_t P, const int32_t *group, const double *u, int64_t n,
+                     int32_t *out_idx, void *stream) {
+  STALE_PROBE();
+  if (n <= 0) return PGM_OK;
+  if (!joint || !group || !u || !out_idx || P <= 0 || P > 0x7fffffff) return fail(PGM_EINVAL, "sample_joint: bad argument");
+  const uint64_t bx = ((uint64_t)n + 255) / 256;
+  if (bx > 0x7fffffffull) return fail(PGM_EINVAL, "sample_joint: too many rows");
+  hipLaunchKernelGGL(k_sample_joint, dim3((unsigned)bx), dim3(256), 0, S(stream), joint, ld, P, group, u, n, out_idx);
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

@@ -151,7 +151,7 @@ def _column_raw(v, st, col):
     return c.astype(np.int8), np.arange(len(st), dtype=np.uint8)
 
 
-def ingest_frame(model, data, columns=None):
+def ingest_frame(model, data, columns=None, row_hash=False):
     """Evidence of a DataFrame on the device.
 
     Host: per column, its int8 category indices (pandas Categorical codes, zero-copy of the frame's
@@ -174,7 +174,10 @@ def ingest_frame(model, data, columns=None):
         r = _column_raw(data[col], st, col)
         if r is None:
             codes = encode_frame(model, data, columns)
-            return Evidence(upload_codes(codes), group_patterns(codes), n)
+            ev = Evidence(upload_codes(codes), group_patterns(codes), n)
+            if row_hash:
+                ev.row_hash = _host_row_hash(codes)
+            return ev
         raws.append(r[0])
         luts.append(r[1])
     L = N.lib()
@@ -194,11 +197,12 @@ def ingest_frame(model, data, columns=None):
     d_key = E.to_device_raw(keys)
     d_rk = torch.zeros(n, dtype=torch.int64, device=dev)
     d_nm = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_hash = torch.zeros((n, 2), dtype=torch.int64, device=dev) if row_hash else None
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     if n and nc:
         N.check(L.pgm_memcpy_h2d(N.ptr(d_raw), ctypes.c_void_p(h_raw.data_ptr()), h_raw.numel(), s), "memcpy_h2d")
         N.check(L.pgm_codes_remap(N.ptr(d_raw), n, nc, n, N.ptr(d_lut), 128, N.ptr(d_key), N.ptr(d_codes), n,
-                                  N.ptr(d_rk), N.ptr(d_nm), N.ptr(err), s), "codes_remap")
+                                  N.ptr(d_rk), N.ptr(d_nm), N.ptr(d_hash), N.ptr(err), s), "codes_remap")
     nm = download(d_nm)
     if int(download(err)[0]):
         encode_frame(model, data, columns)  # raises the reference's KeyError for the offending cell
@@ -217,7 +221,23 @@ def ingest_frame(model, data, columns=None):
             rows = order[bounds[g]:bounds[g + 1]]
             groups.append((hr[:, rows[0]] >= 0, rows))
         groups.sort(key=lambda gr: gr[1][0])
-    return Evidence(d_codes, groups, n)
+    ev = Evidence(d_codes, groups, n)
+    if row_hash:
+        ev.row_hash = download(d_hash)
+    return ev
+
+
+def _host_row_hash(codes):
+    """[n, 2] int64 content hash of the rows of uint8 codes [n_cols, n] (host encoder path)."""
+    rng = np.random.default_rng(_COL_KEY_SEED + 1)
+    mult = rng.integers(1, 2 ** 63, size=(2, codes.shape[0]), dtype=np.int64) | 1
+    h = np.zeros((codes.shape[1], 2), dtype=np.int64)
+    with np.errstate(over="ignore"):
+        for c in range(codes.shape[0]):
+            x = codes[c].astype(np.int64) + 1
+            h[:, 0] += x * mult[0, c]
+            h[:, 1] ^= (x * mult[1, c]) >> 3
+    return h
 
 
 def upload_codes(codes):
@@ -364,6 +384,78 @@ def predict_frame(model, data):
     if out.index.is_monotonic_increasing:
         return out
     return out.sort_index()
+
+
+def predict_stochastic_frame(model, data, seed=None):
+    """DiscreteBayesianNetwork.predict(stochastic=True) (DiscreteBayesianNetwork.py:866-910).
+
+    The reference de-duplicates identical rows (groupby over every column, L867-870), queries the
+    joint of the missing variables (plus the row's NaN columns) once per unique row, and draws
+    len(group) samples from it with a fresh numpy Generator(seed) per group (DiscreteFactor.sample,
+    L868-912: Generator.choice = inverse CDF of fresh uniforms).  Here: rows are keyed by a 128-bit
+    content hash computed in the ingestion pass, one joint per unique row comes from the pattern's
+    compiled plan, and pgm_sample_joint inverts each row's CDF on the device with the uniform the
+    reference's stream gives that row (its position in its group)."""
+    import pandas as pd
+    import torch
+
+    columns = list(data.columns)
+    col_of = {c: i for i, c in enumerate(columns)}
+    missing_variables = set(model.nodes()) - set(data.columns)
+    order = list(missing_variables)
+    n = len(data)
+    ev = ingest_frame(model, data, columns, row_hash=True)
+    _, first, inv = np.unique(ev.row_hash, axis=0, return_index=True, return_inverse=True)
+    inv = inv.reshape(-1)
+    counts = np.bincount(inv, minlength=len(first))
+    srt = np.argsort(inv, kind="stable")
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    pos = np.empty(n, dtype=np.int64)
+    pos[srt] = np.arange(n) - np.repeat(starts, counts)
+    if seed is None:  # a fresh entropy-seeded Generator per group: independent uniforms
+        u = np.random.default_rng().random(n)
+    else:  # every group restarts Generator(seed): a row's uniform is the stream at its position
+        u = np.random.default_rng(seed).random(int(counts.max()) if n else 0)[pos]
+    vals = {c: np.full(n, np.nan, dtype=object) for c in order}
+    filled = {}
+    L = N.lib()
+    s = N.stream_handle()
+    for mask, rows in ev.groups:
+        observed = [columns[j] for j in range(len(columns)) if mask[j]]
+        nan_cols = [columns[j] for j in range(len(columns)) if not mask[j]]
+        variables = list(missing_variables.union(set(nan_cols)))  # the reference's query variables (L873-875)
+        plan = get_plan(model, variables, observed, col_of)
+        uniq = np.unique(inv[rows])
+        reps = first[uniq]
+        n_u = len(uniq)
+        out = plan.alloc_outputs(n_u, marginals=False, joint=True)
+        err = torch.zeros(1, dtype=torch.int32, device=ev.codes.device)
+        plan.run(ev.rows_codes(reps), n_u, 0, n_u, out, err=err)
+        if int(download(err)[0]) != 0:
+            raise IndexError("evidence state code out of range")
+        joint = out["joint"]  # [P, n_u], C-order over plan.variables
+        if np.isnan(float(E.to_host(E.contract(joint, ["q", E.ROW], None, None, [], reduce="sum", combine="copy")))):
+            raise ValueError("probabilities contain NaN")  # Generator.choice on an impossible row's joint
+        grp = E.to_device_raw(np.searchsorted(uniq, inv[rows]).astype(np.int32))
+        d_u = E.to_device_raw(np.ascontiguousarray(u[rows]))
+        d_idx = torch.empty(len(rows), dtype=torch.int32, device=joint.device)
+        N.check(L.pgm_sample_joint(N.ptr(joint), int(joint.stride(0)), int(plan.P), N.ptr(grp), N.ptr(d_u),
+                                   len(rows), N.ptr(d_idx), s), "sample_joint")
+        idx = download(d_idx).astype(np.int64)
+        for i in reversed(range(len(plan.variables))):
+            var = plan.variables[i]
+            c = plan.cards[i]
+            st = np.array(plan.states[var], dtype=object)
+            if var in vals:
+                vals[var][rows] = st[idx % c]
+            else:
+                if var not in filled:
+                    filled[var] = data[var].to_numpy(object).copy()
+                filled[var][rows] = st[idx % c]
+            idx = idx // c
+    base = data.assign(**filled) if filled else data
+    out = pd.concat([base, pd.DataFrame(vals, index=data.index, columns=order)], axis=1)
+    return out if out.index.is_monotonic_increasing else out.sort_index()
 
 
 def query_batch(model, variables, evidence, joint=False):

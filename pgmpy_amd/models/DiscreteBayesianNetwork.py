@@ -233,7 +233,9 @@ class DiscreteBayesianNetwork(nx.DiGraph):
             if not (isinstance(algo, type) and issubclass(algo, Inference)):
                 raise TypeError(f"Algorithm should be a valid pgmpy inference method. Got {type(algo)} instead.")
         if stochastic:
-            raise NotImplementedError("stochastic=True (sampling from the posterior) is outside the accelerated path")
+            from ..inference.batch import predict_stochastic_frame
+
+            return predict_stochastic_frame(self, data, seed=seed)
         return predict_frame(self, data)
 
     @E.serialized

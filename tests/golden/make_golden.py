@@ -21,6 +21,7 @@ Fixture inventory (SURVEY.md §8(c) "Golden vectors"):
   unit_cases.json              hand-sized unit expectations of the reference tests
   alarm_queries.json           C1: HISTORY|CVP=LOW + 50 seeded query patterns (+ MAP)
   alarm_predict.json           predict / predict_probability on alarm rows (with NaN)
+  alarm_predict_stochastic.json  predict(stochastic=True, seed=7) on duplicated alarm rows
   alarm_bp.npz / .json         BP calibration on a min-fill JT of alarm (full beliefs)
   munin_predict.npz            C3 template rows, MAP codes and marginals
   munin_c2_query.json          C2: 100 leaf findings -> 1 root posterior
@@ -319,6 +320,37 @@ def gen_alarm_predict():
     })
 
 
+def gen_alarm_predict_stochastic():
+    """predict(stochastic=True, seed=...) (DiscreteBayesianNetwork.py:866-910): duplicated rows (the
+    reference draws len(group) samples per unique row, each group from a fresh Generator(seed)).
+    Case "one": a single missing variable (factor order is trivial).  Case "two": two missing
+    variables and NaN cells (extra query variables); its factor order follows set iteration under
+    PYTHONHASHSEED=0, so the test replays it in a PYTHONHASHSEED=0 subprocess."""
+    import pandas as pd
+    from pgmpy.sampling import BayesianModelSampling
+
+    m = _model("alarm")
+    df = BayesianModelSampling(m).forward_sample(size=60, seed=11, show_progress=False)
+    rng = np.random.default_rng(11)
+    picks = np.concatenate([np.arange(40), rng.choice(40, size=35)])
+    rng.shuffle(picks)
+    out = {"seed": 7}
+    for case, missing, nan_col in (("one", ["LVFAILURE"], None), ("two", ["HYPOVOLEMIA", "STROKEVOLUME"], "CVP")):
+        data = df.iloc[picks].drop(columns=missing).astype(object).reset_index(drop=True)
+        if nan_col is not None:
+            for r in range(0, len(data), 9):
+                data.iat[r, data.columns.get_loc(nan_col)] = np.nan
+        pred = m.predict(data, stochastic=True, seed=7, n_jobs=1)
+        out[case] = {
+            "columns": list(data.columns),
+            "rows": [[None if (isinstance(x, float) and np.isnan(x)) else str(x) for x in row] for row in data.values],
+            "missing": missing,
+            "predict_columns": list(pred.columns),
+            "predict": [[None if (isinstance(x, float) and np.isnan(x)) else str(x) for x in row] for row in pred.values],
+        }
+    _dump("alarm_predict_stochastic.json", out)
+
+
 # ----------------------------------------------------------------------------- junction trees
 def minfill_junction_tree(model):
     """Min-fill JT used as the BP oracle input (SURVEY.md §8(c) "BP oracle caveat")."""
@@ -562,6 +594,7 @@ GENS = {
     "alarm_predict": gen_alarm_predict,
     "alarm_bp": gen_alarm_bp,
     "pathfinder_bp": gen_pathfinder_bp,
+    "alarm_predict_stochastic": gen_alarm_predict_stochastic,
     "munin_predict": gen_munin_predict,
     "munin_c2": gen_munin_c2,
 }
