@@ -93,7 +93,16 @@ def launch_ranks(n):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     log("bench.py: starting", n, "ranks:", " ".join(cmd))
-    return subprocess.call(cmd, env=dict(os.environ))
+    # rank 0's JSON line is the only stdout line; library chatter (gloo's connection messages go to
+    # stdout) is forwarded to stderr
+    p = subprocess.Popen(cmd, env=dict(os.environ), stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        if line.lstrip().startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
 
 
 def barrier(dist):

@@ -52,10 +52,13 @@ class TabularCPD(DiscreteFactor):
         return var_str + ev + f") at {hex(id(self))}>"
 
     def get_values(self):
-        # CPD.py:198-223
+        # CPD.py:198-223 (a view of values: editing it edits the CPD, so the values are exposed)
+        return self._shape2d(self.values)
+
+    def _shape2d(self, v):
         if self.variable in self.variables:
-            return self.values.reshape(tuple([self.cardinality[0], int(np.prod(self.cardinality[1:]))]))
-        return self.values.reshape(tuple([int(np.prod(self.cardinality)), 1]))
+            return v.reshape(tuple([self.cardinality[0], int(np.prod(self.cardinality[1:]))]))
+        return v.reshape(tuple([int(np.prod(self.cardinality)), 1]))
 
     def get_evidence(self):
         return self.variables[:0:-1]
@@ -63,7 +66,7 @@ class TabularCPD(DiscreteFactor):
     def copy(self):
         evidence = self.variables[1:] if len(self.variables) > 1 else None
         evidence_card = self.cardinality[1:] if len(self.variables) > 1 else None
-        return TabularCPD(self.variable, self.variable_card, np.array(self.get_values()), evidence, evidence_card,
+        return TabularCPD(self.variable, self.variable_card, np.array(self._shape2d(self._values_readonly())), evidence, evidence_card,
                           state_names=self.state_names.copy())
 
     def normalize(self, inplace=True):
@@ -116,5 +119,5 @@ class TabularCPD(DiscreteFactor):
         return f
 
     def is_valid_cpd(self):
-        v = self.get_values()
+        v = self._shape2d(self._values_readonly())  # internal read: does not expose the values
         return bool(np.allclose(v.sum(axis=0), np.ones(v.shape[1]), atol=0.01))

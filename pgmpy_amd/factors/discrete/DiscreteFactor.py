@@ -70,12 +70,15 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
             self._dev_crc = _crc(self._host)
         elif not self._exposed and self._dev is not None:
             self._dev_crc = _crc(self._host)
-        self._exposed = True
+        if not self._exposed:
+            self._exposed = True
+            _VALUES_EPOCH[0] += 1
         return self._host
 
     @values.setter
     def values(self, v):
         self._version += 1
+        _VALUES_EPOCH[0] += 1
         if _is_device(v):
             self._dev = v
             self._host = None
@@ -109,6 +112,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
             if crc != self._dev_crc:
                 self._dev = None
                 self._version += 1
+                _VALUES_EPOCH[0] += 1
         if self._dev is None:
             h = self._host.reshape(tuple(int(c) for c in self.cardinality))
             self._dev = E.to_device(h)
@@ -118,6 +122,7 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
 
     def _set_d(self, t):
         self._version += 1
+        _VALUES_EPOCH[0] += 1
         self._dev = t
         self._host = None
         self._exposed = False
@@ -455,6 +460,15 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
         card = np.array(self.cardinality)[order] if order else np.array(self.cardinality)
         return hash(str(sorted(variable_hashes)) + str(hash(np.ascontiguousarray(vals).tobytes()))
                     + str(hash(np.ascontiguousarray(card).tobytes())) + str(hash(frozenset(self.state_names))))
+
+
+# bumped whenever any factor's values may change without a CRC check seeing it: a values setter
+# call, a device replacement, or a host array handed out for the first time (values_epoch())
+_VALUES_EPOCH = [0]
+
+
+def values_epoch():
+    return _VALUES_EPOCH[0]
 
 
 def _crc(a):

@@ -99,9 +99,20 @@ class PatternPlan:
     def is_current(self):
         """True while the model structure and the values of every CPD this plan read are unchanged
         (the reference recomputes from the current CPDs on every call)."""
+        from ..factors.discrete.DiscreteFactor import values_epoch
+
         if getattr(self.model, "_epoch", None) != self._epoch:
             return False
-        return all(cpd._value_token() == tok for cpd, tok in self._sources)
+        ve = values_epoch()
+        if ve == self.__dict__.get("_vepoch"):
+            # no factor's values were replaced or newly handed out since the last full check: only
+            # the exposed sources (host arrays a caller may edit in place) need their CRC compared
+            return all(cpd._value_token() == tok for cpd, tok in self._exposed_sources)
+        if not all(cpd._value_token() == tok for cpd, tok in self._sources):
+            return False
+        self._vepoch = ve
+        self._exposed_sources = [(cpd, tok) for cpd, tok in self._sources if cpd._exposed]
+        return True
 
     # ------------------------------------------------------------------ fused
     def components(self):
