@@ -569,7 +569,7 @@ def bench_c2(args):
             "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
             "plan": {"kind": plan.kind, **ps},
             "achieved": {"GB/s": ps["bytes"] / dt / 1e9, "TFLOP/s": ps["flops"] / dt / 1e12,
-                         "note": "algorithmic bytes / flops of the executed greedy plan (SURVEY §8(d) C2) per query"},
+                         "note": "algorithmic bytes / flops of the executed plan (contraction.choose_path; SURVEY §8(d) C2) per query"},
             "reference": {"value": 52.7, "unit": "s/query", "note": "pgmpy numpy path, survey container (not this host)"},
             "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
                     "same query/evidence variables); first_query_s includes pruning, planning and graph capture",

@@ -12,6 +12,10 @@ vendored) plans a greedy path; its published greedy strategy is restated here:
   3. with no pair sharing a label left, take outer products of the two
      smallest operands.
 
+The executed path is the cheaper (by an MI355X cost estimate) of that greedy path and a
+min-weight variable-elimination path (elimination_path; on munin's C2 query 32 MB / 18 MFLOP
+instead of greedy's 1.5 GB / 19.9 GFLOP) — the values do not depend on the path beyond rounding.
+
 Every pairwise step is ONE fused product+marginalize kernel (pgm_contract,
 combine=MUL, reduce=SUM): the broadcast product is never materialised.  Steps
 that are dense GEMMs (shared summed variables of total cardinality >= 8, each
@@ -119,10 +123,129 @@ def greedy_path(operand_labels, out_labels, dims):
     return steps, final_id
 
 
+def elimination_path(operand_labels, out_labels, dims):
+    """A contraction path from a variable-elimination order (returns greedy_path's format).
+
+    opt_einsum's greedy rule (greedy_path) looks one pairwise step ahead; on munin's C2 query it
+    builds 36 M-entry intermediates and does 19.9 GFLOP.  Classic VE instead eliminates, at each
+    step, the variable whose elimination clique is smallest — the MinWeight heuristic
+    (pgmpy/inference/EliminationOrder.py:136-150: the product of the cardinalities of the
+    variable's neighbours) measured on the current factors — multiplying the factors that hold it
+    smallest-first and summing it out with the last product.  On C2 that is 18 MFLOP and 32 MB
+    with a 168 K-entry largest intermediate.  Values do not depend on the path beyond rounding."""
+    out_set = set(out_labels)
+    ops = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    holders = {}
+    for i, ls in ops.items():
+        for l in ls:
+            holders.setdefault(l, set()).add(i)
+    steps = []
+    ids = count(len(operand_labels))
+
+    def kept(labels, exclude):
+        return [l for l in labels if l in out_set or len(holders[l] - exclude) > 0]
+
+    def retire(olds, keep, kind, extra=()):
+        nid = next(ids)
+        steps.append((kind,) + tuple(olds[:1] if kind == "reduce" else olds) + (keep, nid))
+        touched = set()
+        for o in olds:
+            for l in ops[o]:
+                holders[l].discard(o)
+                touched.add(l)
+            del ops[o]
+        for l in keep:
+            holders[l].add(nid)
+        ops[nid] = keep
+        return nid, touched
+
+    for i in list(ops):  # 1. private labels, as in greedy_path
+        keep = kept(ops[i], {i})
+        if keep != ops[i]:
+            retire([i], keep, "reduce")
+
+    def weight(v):
+        nb = set()
+        for i in holders[v]:
+            nb.update(ops[i])
+        return _size(nb, dims)
+
+    heap, ver, done = [], {}, set()
+    for v, h in holders.items():
+        if v not in out_set and h:
+            ver[v] = 0
+            heapq.heappush(heap, (weight(v), 0, str(v), v))
+    while heap:  # 2. eliminate the minimum-weight variable (lazy re-weighing)
+        w, vv, _, v = heapq.heappop(heap)
+        if v in done or ver.get(v) != vv or not holders[v]:
+            continue
+        cw = weight(v)
+        if cw != w:
+            ver[v] += 1
+            heapq.heappush(heap, (cw, ver[v], str(v), v))
+            continue
+        done.add(v)
+        inv = sorted(holders[v], key=lambda i: (_size(ops[i], dims), i))
+        touched = set()
+        while len(inv) > 1:
+            a, b = inv[0], inv[1]
+            nid, t = retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
+            touched |= t
+            inv = sorted([nid] + inv[2:], key=lambda i: (_size(ops[i], dims), i))
+        if v in ops[inv[0]]:
+            _, t = retire([inv[0]], [l for l in ops[inv[0]] if l != v], "reduce")
+            touched |= t
+        for l in touched:
+            if l not in done and l not in out_set and holders[l]:
+                ver[l] = ver.get(l, 0) + 1
+                heapq.heappush(heap, (weight(l), ver[l], str(l), l))
+    while len(ops) > 1:  # 3. what is left shares only output labels: smallest first
+        a, b = sorted(ops, key=lambda k: (_size(ops[k], dims), k))[:2]
+        retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
+    (final_id,) = ops.keys() if ops else (None,)
+    return steps, final_id
+
+
+def path_cost(steps, operand_labels, dims):
+    """(bytes, flops, depth) of a path: 8 (|A| + |B| + |C|) bytes and 2 |index space| flops per
+    pairwise step, |A| + |C| per reduction; depth = the longest chain of dependent steps."""
+    labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    depth = {i: 0 for i in labels}
+    nbytes = flops = maxd = 0
+    for st in steps:
+        if st[0] == "reduce":
+            _, i, keep, nid = st
+            nbytes += 8 * (_size(labels[i], dims) + _size(keep, dims))
+            flops += _size(labels[i], dims)
+            d = depth[i] + 1
+        else:
+            _, i, j, keep, nid = st
+            nbytes += 8 * (_size(labels[i], dims) + _size(labels[j], dims) + _size(keep, dims))
+            flops += 2 * _size(list(dict.fromkeys(labels[i] + labels[j])), dims)
+            d = max(depth[i], depth[j]) + 1
+        labels[nid], depth[nid] = keep, d
+        maxd = max(maxd, d)
+    return nbytes, flops, maxd
+
+
+def choose_path(operand_labels, out_labels, dims):
+    """The cheaper of opt_einsum's greedy path and the min-weight elimination path, by an MI355X
+    estimate: bytes at 3 TB/s + flops at 15 TFLOP/s + 3 us per dependency level (one batched
+    launch per level in a compiled program)."""
+    best = None
+    for planner in (greedy_path, elimination_path):
+        steps, final_id = planner(operand_labels, out_labels, dims)
+        nbytes, flops, depth = path_cost(steps, operand_labels, dims)
+        est = nbytes / 3e12 + flops / 15e12 + depth * 3e-6
+        if best is None or est < best[0]:
+            best = (est, steps, final_id)
+    return best[1], best[2]
+
+
 def plan_stats(operand_labels, out_labels, dims):
-    """Algorithmic bytes / flops of the planned path (SURVEY.md §8(d) C2 definition):
+    """Algorithmic bytes / flops of the executed path (choose_path; SURVEY.md §8(d) C2 definition):
     sum over pairwise steps of 8 (|A| + |B| + |C|) bytes and 2 |index space| flops."""
-    steps, _ = greedy_path(operand_labels, out_labels, dims)
+    steps, _ = choose_path(operand_labels, out_labels, dims)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     nbytes = flops = 0
     max_inter = sum_inter = 0
@@ -158,7 +281,7 @@ def compiled_path(operand_labels, out_labels, dims):
     if hit is not None:
         _PATHS.move_to_end(key)
         return hit
-    steps, final_id = greedy_path(operand_labels, out_labels, dims)
+    steps, final_id = choose_path(operand_labels, out_labels, dims)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     plan = []
     for st in steps:

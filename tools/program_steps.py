@@ -39,8 +39,8 @@ def main():
         ev = {v: m.states[v][0] for v in E}
         ve = VariableElimination(m)
         ve.query(q, ev, show_progress=False)
-        (plan, _), = ve._compiled.values()
-        (prog, *_), = plan._progs.values()
+        runner, = ve._compiled.values()
+        (prog, *_), = runner.plan._progs.values()
     res = prog.time_steps()
     tot = sum(us for us, _ in res)
     print(f"{len(res)} steps, {tot / 1e3:.2f} ms summed")
