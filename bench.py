@@ -660,7 +660,12 @@ def bench_c4(args):
     bpc = bjt.bytes_per_calibration()
     return {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
             "rows_per_step": n, "ms_per_step": dt * 1e3, "bytes_per_calibration": bpc,
-            "achieved_GBps": bpc * n / dt / 1e9, "cliques": len(bjt.cliques)}
+            "achieved_GBps": bpc * n / dt / 1e9, "frac_of_8TBps": bpc * n / dt / 1e9 / HBM_PEAK_GBS,
+            "reference_schedule_bytes_per_calibration": bjt.reference_bytes_per_calibration(),
+            "note": "bytes_per_calibration: every belief written once + separator messages / sigma' written and "
+                    "read once (this schedule); the reference schedule's figure reads and writes every belief "
+                    "in both passes (SURVEY §8(d) C4)",
+            "cliques": len(bjt.cliques)}
 
 
 def main():

@@ -136,7 +136,9 @@ int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *
  * PGM_RED_MAX (max-calibration).  Only shapes with pgm_product_n_marginal_ok() == 1 run fused
  * (<= 4 operands, rows innermost with an even count >= 64, <= 512 reduced states per kept state,
  * enough kept states to fill the chip); others return PGM_EINVAL without launching and the caller
- * runs pgm_product_n + pgm_contract. */
+ * runs pgm_product_n + pgm_contract.  C == NULL computes M alone (the strides of C still describe
+ * the product's index space): a batched-BP collect message without writing the clique belief, which
+ * the distribute pass then writes once. */
 int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *ops, const double *C,
                               const int64_t *marg_s, const double *M);
 int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops, double *C,

@@ -1019,7 +1019,7 @@ __global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *
           hi[i] = cur[i].y;
         }
         const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
-        ((double2 *)(C + oc + tc[j]))[x] = pr;
+        if (C) ((double2 *)(C + oc + tc[j]))[x] = pr;  // C == nullptr: the marginal only
         acc.x = red_op<RED>(acc.x, pr.x);
         acc.y = red_op<RED>(acc.y, pr.y);
 #pragma unroll
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
           hi[i] = v[u][i].y;
         }
         const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
-        if (x0 + 256u * u < p.NP) cj[x0 + 256u * u] = pr;
+        if (C && x0 + 256u * u < p.NP) cj[x0 + 256u * u] = pr;  // C == nullptr: the marginal only
         acc[u].x = red_op<RED>(acc[u].x, pr.x);
         acc[u].y = red_op<RED>(acc[u].y, pr.y);
       }
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
 // 1 = the fused kernel applies (k filled), 0 = it does not (use product_n + contract), < 0 error
 static int plan_product_marg(const pgm_productn_desc *d, const double *const *ops, const double *C,
                              const int64_t *marg_s, const double *M, ProdMK &k, dim3 &grid) {
-  if (!d || !ops || !C || !marg_s || !M) return fail(PGM_EINVAL, "product_n_marginal: null argument");
+  if (!d || !ops || !marg_s || !M) return fail(PGM_EINVAL, "product_n_marginal: null argument");
   if (d->n_ops < 1 || d->n_ops > PMAX || d->n_keep < 1 || d->n_keep > PGM_MAX_DIMS)
     return fail(PGM_EINVAL, "product_n_marginal: n_ops %d / n_keep %d out of range", d->n_ops, d->n_keep);
   if (g_no_rows2 || d->n_ops > MOPS || d->n_keep < 2) return 0;

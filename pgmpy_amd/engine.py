@@ -346,10 +346,11 @@ def product_n(operands, out_labels, out=None, kinds=None):
     return out
 
 
-def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None):
+def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None, store=True):
     """(descriptor, operand pointers, C, marginal strides, M, fused?) for C = product_n(...) and
     M[marg_labels] = reduce of C over the other labels (pgm_product_n_marginal); marg_labels must
-    be a subset of out_labels.  fused is False when the fused kernel does not apply."""
+    be a subset of out_labels.  fused is False when the fused kernel does not apply.  store=False:
+    M alone (C's buffer only describes the index space)."""
     d, ptrs, out = prepare_product_n(operands, out_labels, out, kinds)
     out_labels, marg_labels = list(out_labels), list(marg_labels)
     if any(l not in out_labels for l in marg_labels):
@@ -357,7 +358,7 @@ def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kind
     M = empty([int(out.shape[out_labels.index(l)]) for l in marg_labels])
     ms = (ctypes.c_int64 * len(out_labels))(*[int(M.stride(marg_labels.index(l))) if l in marg_labels else 0
                                                for l in out_labels])
-    ok = bool(N.lib().pgm_product_n_marginal_ok(ctypes.byref(d), ptrs, N.ptr(out), ms, N.ptr(M)))
+    ok = bool(N.lib().pgm_product_n_marginal_ok(ctypes.byref(d), ptrs, N.ptr(out) if store else None, ms, N.ptr(M)))
     return d, ptrs, out, ms, M, ok
 
 

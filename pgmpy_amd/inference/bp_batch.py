@@ -7,15 +7,17 @@ and one distribute (root -> leaves) sweep of Lauritzen-Spiegelhalter belief
 update — the fixed point of the reference's _calibrate_junction_tree
 (pgmpy/inference/ExactInference.py:770-895):
 
-  collect    beta_c = psi_c x findings_c x prod_{children k} sigma_k   (one n-ary product, written once)
-             sigma_c = marg_{C_c \\ S}(beta_c)                         (message to the parent; mu = sigma)
-  distribute sigma' = marg_{C_p \\ S}(beta_p);  beta_c *= sigma' / mu (0/0 -> 0, DiscreteFactor.py:859-863)
+  collect    mu_c = marg_{C_c \\ S}(psi_c x findings_c x prod_{children k} mu_k)   (message to the parent;
+             the clique-sized product is NOT written: the fused kernel's marginal-only mode)
+  distribute sigma' = marg_{C_p \\ S}(beta_p);  beta_c = psi_c x findings_c x prod mu_k x sigma' / mu_c
+             (0/0 -> 0, DiscreteFactor.py:859-863), written once
 
 Findings enter as 0/1 indicators (pgm_indicator) of the first clique holding
 each observed variable.  A compiled schedule (per batch size and evidence
 columns) is a pgmpy_amd.program.Program: all buffers preallocated, replayed as
-one HIP graph.  Algorithmic bytes per calibration: 8 (4 sum|C| + 4 sum|S|)
-(SURVEY.md §8(d)).
+one HIP graph.  Algorithmic bytes per calibration: 8 (sum|C| + 4 sum|S|) — every belief written once,
+every separator message and sigma' written and read once; SURVEY.md §8(d)'s 8 (4 sum|C| + 4 sum|S|)
+counts the reference's schedule, which reads and writes each belief in both passes.
 """
 import os
 
@@ -128,7 +130,11 @@ class BPSchedule:
             return max(scs, key=lambda x: (scope_size(x), len(x)))
 
         premarg = {}  # clique -> (scope, marginal of its final belief) made in the finalising pass
-        # collect: post-order (children before parents)
+        operands = {}  # clique -> its collect operands: [psi_c] + aggregated findings / child messages
+        # collect: post-order (children before parents).  A clique's message to its parent is the
+        # marginal of psi_c x aggregates computed WITHOUT writing the clique-sized product (the
+        # fused kernel's marginal-only mode): the belief is written once, in distribute.  The root's
+        # belief is final after collect (its largest child-separator marginal in the same pass).
         post = [c for _, c in reversed(bjt.order)] + [bjt.root]
         for c in post:
             t, ls = bjt.pot[c]
@@ -140,23 +146,25 @@ class BPSchedule:
             ops = [(t, ls)] + _aggregate(prog, small, ls, scope_size)
             if len(ops) == 1:
                 ops.append((E.to_device(np.ones(n_rows)), [R]))  # broadcast psi over the rows
-            # the belief and its message to the parent (at the root: its largest child-separator
-            # marginal) in one pass over the clique
+            operands[c] = ops
             if c in parent:
                 sep = [v for v in ls if v in parent[c]]
-                bt, m = prog.product_n_marginal(ops, ls + [R], sep + [R], reduce=red)
-                beliefs[c] = (bt, ls)
+                bt, m, _ = prog.product_n_marginal(ops, ls + [R], sep + [R], reduce=red, store=False)
+                beliefs[c] = (bt, ls)  # the buffer distribute writes (the fallback path filled it already)
                 msgs[c] = (m, sep + [R])
             elif c in kids:
                 sc = largest_kid_scope(c)
-                bt, m = prog.product_n_marginal(ops, ls + [R], list(sc) + [R], reduce=red)
+                bt, m, _ = prog.product_n_marginal(ops, ls + [R], list(sc) + [R], reduce=red)
                 beliefs[c] = (bt, ls)
                 premarg[c] = (sc, m)
             else:
                 beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
-        # distribute: root -> leaves; one sigma per distinct separator scope of a parent, each
-        # marginalised from the smallest already-computed containing scope (or the belief); a
-        # child's update beta_c *= sigma / mu also yields its own largest child-separator marginal
+        # distribute: root -> leaves; one sigma' per distinct separator scope of a parent, each
+        # marginalised from the smallest already-computed containing scope (or the belief).  A child's
+        # final belief beta_c = psi_c x aggregates x sigma'/mu (0/0 -> 0) is written in ONE pass from
+        # its collect operands (the separator-sized ratio folded into them), with its own largest
+        # child-scope marginal in the same pass — the reference's beta_c *= sigma'/mu
+        # (ExactInference.py:798-802) on a belief that was never materialised before.
         for p in [bjt.root] + [c for _, c in bjt.order]:
             if p not in kids:
                 continue
@@ -179,16 +187,14 @@ class BPSchedule:
                 for c in scopes[sc]:
                     tc, lc = beliefs[c]
                     mu, sl = msgs[c]
-                    # beta_c *= sigma / mu (0/0 -> 0) in one pass (+ its largest child-scope marginal)
-                    upd = [(tc, lc + [R]), (sigma, sl), (mu, sl)]
-                    kinds = [N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN]
+                    ratio = prog.product_n([(sigma, sl), (mu, sl)], sl, kinds=[N.PRODN_RATIO, N.PRODN_DEN])
+                    ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(ratio, sl)], lc, scope_size)
                     if c in kids:
                         sc_c = largest_kid_scope(c)
-                        _, m = prog.product_n_marginal(upd, lc + [R], list(sc_c) + [R], out=tc, kinds=kinds,
-                                                       reduce=red)
+                        _, m, _ = prog.product_n_marginal(ops_c, lc + [R], list(sc_c) + [R], out=tc, reduce=red)
                         premarg[c] = (sc_c, m)
                     else:
-                        prog.product_n(upd, lc + [R], out=tc, kinds=kinds)
+                        prog.product_n(ops_c, lc + [R], out=tc)
                     seps[(p, c)] = (sigma, sl[:-1])
         marg = {}
         if marginals:
@@ -245,12 +251,18 @@ class BatchedJunctionTree:
         self.sizes = {c: int(np.prod([self.card[v] for v in c])) for c in self.cliques}
         self._schedules = {}
 
+    def _sum_sep(self):
+        return sum(int(np.prod([self.card[v] for v in c if v in p])) for p, c in self.order)
+
     def bytes_per_calibration(self):
-        """SURVEY.md §8(d) C4 algorithmic bytes: 8 (4 sum|C| + 4 sum|S|)."""
-        s = 0
-        for p, c in self.order:
-            s += int(np.prod([self.card[v] for v in c if v in p]))
-        return 8 * (4 * sum(self.sizes.values()) + 4 * s)
+        """Algorithmic HBM bytes of this schedule per calibration: 8 (sum|C| + 4 sum|S|) (each belief
+        written once in distribute; each separator message and sigma' written and read once)."""
+        return 8 * (sum(self.sizes.values()) + 4 * self._sum_sep())
+
+    def reference_bytes_per_calibration(self):
+        """SURVEY.md §8(d) C4's figure for the two-pass schedule that reads and writes every belief
+        in both sweeps: 8 (4 sum|C| + 4 sum|S|)."""
+        return 8 * (4 * sum(self.sizes.values()) + 4 * self._sum_sep())
 
     def schedule(self, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True):
         key = (n_rows, tuple(ev_vars), operation, marginals, graph)

@@ -205,25 +205,28 @@ class Program:
                    f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job)
         return out
 
-    def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum"):
+    def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum",
+                           store=True):
         """Recorded C = product_n(...) with M = reduce(C) onto marg_labels in the same pass
         (pgm_product_n_marginal) when the fused kernel applies, else product_n + contract.
-        Returns (C, M)."""
+        store=False asks for M alone: the fused kernel then writes nothing to C (the fallback
+        still materialises C).  Returns (C, M, stored)."""
         ops = list(operands)
         if len(ops) <= 4:
-            d, ptrs, out2, ms, M, ok = E.prepare_product_n_marginal(ops, out_labels, marg_labels, out, kinds)
+            d, ptrs, out2, ms, M, ok = E.prepare_product_n_marginal(ops, out_labels, marg_labels, out, kinds, store)
             if ok:
                 L = N.lib()
                 self._keep.extend([d, ptrs, out2, ms, M] + [t for t, _ in ops])
-                args = (ctypes.byref(d), ptrs, N.ptr(out2), ms, E._REDUCE[reduce], N.ptr(M))
+                args = (ctypes.byref(d), ptrs, N.ptr(out2) if store else None, ms, E._REDUCE[reduce], N.ptr(M))
                 self._emit(lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal"),
-                           f"product_n_marginal {[(list(ls), tuple(t.shape)) for t, ls in ops]} "
+                           f"product_n_marginal{'' if store else ' (marginal only)'} "
+                           f"{[(list(ls), tuple(t.shape)) for t, ls in ops]} "
                            f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}",
-                           [t for t, _ in ops], [out2, M])
-                return out2, M
+                           [t for t, _ in ops], [out2, M] if store else [M])
+                return out2, M, store
         C = self.product_n(ops, out_labels, out, kinds)
         M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")
-        return C, M
+        return C, M, True
 
     def indicator(self, codes_col, card, n_rows, err=None):
         out = E.empty([card, n_rows])
