@@ -165,6 +165,7 @@ class BPSchedule:
         # its collect operands (the separator-sized ratio folded into them), with its own largest
         # child-scope marginal in the same pass — the reference's beta_c *= sigma'/mu
         # (ExactInference.py:798-802) on a belief that was never materialised before.
+        final = {bjt.root: (operands[bjt.root], None)}  # clique -> (operands, kinds) its belief is the product of
         for p in [bjt.root] + [c for _, c in bjt.order]:
             if p not in kids:
                 continue
@@ -181,20 +182,36 @@ class BPSchedule:
                     sigma = have[sc]
                 else:
                     src = min((h for h in have if set(sc) <= set(h)), key=scope_size)
-                    sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
-                                          combine="copy")
+                    sigma = None
+                    if src == tuple(lp):  # not from the belief (a clique-sized read): from its operands,
+                        fops, fk = final[p]  # marginal only (the fused kernel writes nothing but sigma')
+                        d_, p_, o_, ms_, M_, ok = E.prepare_product_n_marginal(fops, lp + [R], list(sc) + [R], tp,
+                                                                               fk, store=False)
+                        if ok:
+                            _, sigma, _ = prog.product_n_marginal(fops, lp + [R], list(sc) + [R], out=tp, kinds=fk,
+                                                                  reduce=red, store=False)
+                    if sigma is None:
+                        sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
+                                              combine="copy")
                     have[sc] = sigma
                 for c in scopes[sc]:
                     tc, lc = beliefs[c]
                     mu, sl = msgs[c]
-                    ratio = prog.product_n([(sigma, sl), (mu, sl)], sl, kinds=[N.PRODN_RATIO, N.PRODN_DEN])
-                    ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(ratio, sl)], lc, scope_size)
+                    if len(operands[c]) + 2 <= 4:  # sigma' / mu enter as a ratio operand pair (0/0 -> 0)
+                        ops_c = operands[c] + [(sigma, sl), (mu, sl)]
+                        kinds = [N.PRODN_MUL] * len(operands[c]) + [N.PRODN_RATIO, N.PRODN_DEN]
+                    else:  # the separator-sized ratio folded into the aggregates
+                        ratio = prog.product_n([(sigma, sl), (mu, sl)], sl, kinds=[N.PRODN_RATIO, N.PRODN_DEN])
+                        ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(ratio, sl)], lc, scope_size)
+                        kinds = None
+                    final[c] = (ops_c, kinds)
                     if c in kids:
                         sc_c = largest_kid_scope(c)
-                        _, m, _ = prog.product_n_marginal(ops_c, lc + [R], list(sc_c) + [R], out=tc, reduce=red)
+                        _, m, _ = prog.product_n_marginal(ops_c, lc + [R], list(sc_c) + [R], out=tc, kinds=kinds,
+                                                          reduce=red)
                         premarg[c] = (sc_c, m)
                     else:
-                        prog.product_n(ops_c, lc + [R], out=tc)
+                        prog.product_n(ops_c, lc + [R], out=tc, kinds=kinds)
                     seps[(p, c)] = (sigma, sl[:-1])
         marg = {}
         if marginals:
