@@ -1427,7 +1427,8 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   const int wy = wave / WX, wx = wave % WX;
   const uint32_t t = blockIdx.x;  // n fastest within an m row of tiles (A rows stay hot in L2)
   const int64_t n0 = (int64_t)(t % p.tiles_n) * BN, m0 = (int64_t)(t / p.tiles_n) * BM;
-  const int64_t b = blockIdx.y;
+  const int64_t b = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;  // batches beyond 65,535 continue in z
+  if (b >= p.batch) return;  // (whole block: uniform)
   const double *Ab = A + goff<TA>(p.s_ab, p.a_b, b);
   const double *Bb = B + goff<TB>(p.s_bb, p.b_b, b);
   // this thread's tile elements per operand and k tile (e = tid + 256 i), lanes along the operand's
@@ -3121,7 +3122,7 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   const int cfg = tile64 ? 0 : d->m <= 16 ? 1 : tall_ok ? 2 : 0;
   const uint64_t BM = cfg == 1 ? 16 : cfg == 2 ? 128 : 64, BN = cfg == 1 ? 128 : 64;
   const uint64_t tn = ((uint64_t)d->n + BN - 1) / BN, tm = ((uint64_t)d->m + BM - 1) / BM;
-  if (tn * tm > 0x7fffffffull || d->batch > 65535) return fail(PGM_EINVAL, "gemm: grid too large");
+  if (tn * tm > 0x7fffffffull || d->batch > 65535ll * 65535ll) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
   if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
   // tile-load lane order along each operand's unit-stride axis (knob PGM_GEMM_FIXED_ORDER: k-fast A,
@@ -3135,7 +3136,8 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   const bool tb = d->stride[1] < 0 || d->stride[6] < 0 || d->stride[7] < 0;
   const bool tc = d->stride[2] < 0 || d->stride[4] < 0 || d->stride[8] < 0;
   const int tabs = (ta ? 4 : 0) | (tb ? 2 : 0) | (tc ? 1 : 0);
-  const dim3 g((unsigned)(tn * tm), (unsigned)d->batch);
+  const uint64_t gy = std::min<int64_t>(d->batch, 65535), gz = ((uint64_t)d->batch + gy - 1) / gy;
+  const dim3 g((unsigned)(tn * tm), (unsigned)gy, (unsigned)gz);
   hipStream_t s = S(stream);
   if (cfg == 1) launch_gemm<16, 128>(tabs, g, s, k, A, B, C);
   else if (cfg == 2) launch_gemm<128, 64>(tabs, g, s, k, A, B, C);

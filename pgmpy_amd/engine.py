@@ -226,7 +226,7 @@ def gemm_shape(la, lb, keep, card, force=False):
 
     nb, m, n, k = prod(batch), prod(Ms), prod(Ns), prod(Ks)
     small = 2 * nb * m * n * k < GEMM_MIN_FLOPS and not force
-    if k < GEMM_MIN_K or m < GEMM_MIN_M or n < GEMM_MIN_N or small or nb > 65535:
+    if k < GEMM_MIN_K or m < GEMM_MIN_M or n < GEMM_MIN_N or small:
         return None
     return batch, Ms, Ns, Ks
 

@@ -480,65 +480,87 @@ class BeliefPropagationWithMessagePassing(Inference):
             model.check_model()
         self.model = model
 
-    class _RecursiveMessageSchedulingQuery:
-        # ExactInference.py:1349-1507
-        def __init__(self, bp, variables, evidence, virtual_evidence, get_messages, precomp_messages):
-            self.bp = bp
-            self.variables = variables
-            self.evidence = evidence
-            self.virtual_evidence = virtual_evidence
-            self.get_messages = get_messages
-            self.all_messages = (precomp_messages.copy() if precomp_messages is not None
-                                 else {} if get_messages or len(variables) > 1 else None)
+    class _MessageSchedule:
+        """Messages toward the query variables, leaves first, with an explicit work stack (no Python
+        recursion depth limit on long chains).  A message is a directed edge (source node, target
+        node) of the factor graph; its value needs the messages into the source from every other
+        neighbour.  An observed variable sends its point mass without looking further
+        (ExactInference.py:1449-1452); virtual evidence joins a variable's outgoing messages.
+        Messages are cached under the reference's key strings ("A -> ['B', 'A']", "['B', 'A'] -> B")
+        when the reference caches them (several query variables or get_messages), so
+        get_messages returns the same dictionary (ExactInference.py:1349-1507)."""
 
-        def run(self):
-            agg_res = {}
-            for variable in self.variables:
-                res = self.schedule_variable_node_messages(variable, from_factor=None)
-                agg_res[variable] = DiscreteFactor([variable], [len(res)], res)
-            if self.get_messages:
-                return agg_res, self.all_messages
-            return agg_res
+        def __init__(self, bp, evidence, virtual_evidence, cache):
+            self.bp, self.model = bp, bp.model
+            self.evidence = evidence or {}
+            self.virtual = {}
+            if virtual_evidence is not None:
+                for cpd in virtual_evidence:
+                    self.virtual.setdefault(cpd.variables[0], []).append(np.asarray(cpd.values).reshape(-1))
+            self.cache = cache
 
-        def schedule_variable_node_messages(self, variable, from_factor):
-            if self.evidence is not None and variable in self.evidence.keys():
-                return self.bp.model.get_point_mass_message(variable, self.evidence[variable])
-            virtual_messages = []
-            if (self.virtual_evidence is not None
-                    and variable in self.bp._get_virtual_evidence_var_list(self.virtual_evidence)):
-                virtual_messages = [np.asarray(cpd.values).reshape(-1) for cpd in self.virtual_evidence
-                                    if cpd.variables[0] == variable]
-            incoming_factors = [f for f in list(self.bp.model.neighbors(variable)) if f != from_factor]
-            if len(incoming_factors) == 0:
-                message = self.bp.model.get_uniform_message(variable)
-                return self.bp.calc_variable_node_message(variable, [message] + virtual_messages)
-            incoming_messages = []
-            for factor in incoming_factors:
-                key = f"{factor.variables} -> {variable}"
-                if self.all_messages is not None and key in self.all_messages:
-                    msg = self.all_messages[key]
-                else:
-                    msg = self.schedule_factor_node_messages(factor, variable)
-                    if self.all_messages is not None:
-                        self.all_messages[key] = msg
-                incoming_messages.append(msg)
-            return self.bp.calc_variable_node_message(variable, incoming_messages + virtual_messages)
+        def _is_var(self, node):
+            return not isinstance(node, DiscreteFactor)
 
-        def schedule_factor_node_messages(self, factor, from_variable):
-            incoming_vars = [var for var in factor.variables if var != from_variable]
-            if len(incoming_vars) == 0:
-                return self.bp.calc_factor_node_message(factor, [], from_variable)
-            incoming_messages = []
-            for var in incoming_vars:
-                key = f"{var} -> {factor.variables}"
-                if self.all_messages is not None and key in self.all_messages:
-                    msg = self.all_messages[key]
-                else:
-                    msg = self.schedule_variable_node_messages(var, factor)
-                    if self.all_messages is not None:
-                        self.all_messages[key] = msg
-                incoming_messages.append(msg)
-            return self.bp.calc_factor_node_message(factor, incoming_messages, from_variable)
+        @staticmethod
+        def _key(src, dst):
+            if isinstance(src, DiscreteFactor):
+                return f"{src.variables} -> {dst}"
+            return f"{src} -> {dst.variables}"
+
+        def _inputs(self, src, dst):
+            """The messages the edge (src -> dst) is computed from: src's other neighbours -> src."""
+            if self._is_var(src) and src in self.evidence:
+                return []
+            if self._is_var(src):
+                return [(f, src) for f in self.model.neighbors(src) if f is not dst]
+            return [(v, src) for v in src.variables if v != dst]
+
+        def _value(self, src, dst, vals):
+            if self._is_var(src):
+                if src in self.evidence:
+                    return self.model.get_point_mass_message(src, self.evidence[src])
+                msgs = vals or [self.model.get_uniform_message(src)]
+                return self.bp.calc_variable_node_message(src, msgs + self.virtual.get(src, []))
+            return self.bp.calc_factor_node_message(src, vals, dst)
+
+        def belief(self, variable):
+            """Unnormalised-as-the-reference message product at `variable` (its query result)."""
+            done = {}  # (id(src), id(dst)) -> value, this query's own memo
+            lookup = {}
+
+            def get(edge):
+                k = (id(edge[0]), id(edge[1]))
+                if k in done:
+                    return done[k]
+                if self.cache is not None:
+                    ck = self._key(*edge)
+                    if ck in self.cache:
+                        return self.cache[ck]
+                return None
+
+            root = (variable, None)
+            stack = [(root, False)]
+            while stack:
+                edge, expanded = stack.pop()
+                src, dst = edge
+                if edge is not root and get(edge) is not None:
+                    continue
+                deps = self._inputs(src, dst) if edge is not root else (
+                    [] if src in self.evidence else [(f, src) for f in self.model.neighbors(src)])
+                missing = [e for e in deps if get(e) is None]
+                if missing and not expanded:
+                    stack.append((edge, True))
+                    stack.extend((e, False) for e in missing)
+                    continue
+                vals = [get(e) for e in deps]
+                val = self._value(src, dst, vals)
+                if edge is root:
+                    return val
+                done[(id(src), id(dst))] = val
+                if self.cache is not None:
+                    self.cache[self._key(src, dst)] = val
+            raise AssertionError("message schedule did not reach the query variable")
 
     @E.serialized
     def query(self, variables, evidence=None, virtual_evidence=None, get_messages=False, precomp_messages=None):
@@ -554,8 +576,14 @@ class BeliefPropagationWithMessagePassing(Inference):
             if common_vars:
                 raise ValueError(f"Can't have the same variables in both `evidence` and `virtual_evidence`. "
                                  f"Found in both: {common_vars}")
-        return self._RecursiveMessageSchedulingQuery(self, variables, evidence, virtual_evidence, get_messages,
-                                                     precomp_messages).run()
+        cache = (dict(precomp_messages) if precomp_messages is not None
+                 else {} if get_messages or len(variables) > 1 else None)
+        sched = self._MessageSchedule(self, evidence, virtual_evidence, cache)
+        res = {}
+        for variable in variables:
+            b = sched.belief(variable)
+            res[variable] = DiscreteFactor([variable], [len(b)], b)
+        return (res, cache) if get_messages else res
 
     def calc_variable_node_message(self, variable, incoming_messages):
         """ExactInference.py:1629-1657: one message passes through; several are multiplied and

@@ -276,6 +276,8 @@ def test_product_n_and_graph_replay(gpu):
     # the 16 x 128 tile (M <= 16) and the 128 x 64 tile (64 < M <= 128), ragged edges, table groups
     ({"b": 4}, {"m": 16}, {"n": 300}, {"k": 37}),
     ({"b": 2}, {"m1": 10, "m2": 10}, {"n": 200}, {"k1": 5, "k2": 25}),
+    # more than 65,535 batch entries: the batch continues in grid.z
+    ({"b1": 300, "b2": 250}, {"m": 16}, {"n": 16}, {"k": 8}),
 ])
 def test_pair_gemm_matches_einsum(gpu, shape):
     """FP64 MFMA dense steps (pgm_gemm) vs numpy, with permuted / non-contiguous operands."""
