@@ -1186,6 +1186,39 @@ static int plan_product_marg(const pgm_productn_desc *d, const double *const *op
     }
   }
   if (n_red > RMAX_MARG || n_outer >= (1ull << 31)) return 0;
+  // kept-dim order of the block schedule: blocks are dispatched with the LAST kept dim fastest.  A
+  // row-dim operand that lacks a kept dim is read again by every block along that dim, so the dims
+  // lacked by the largest such operands go innermost: the blocks sharing an operand slice then run
+  // back to back and find it in L2 (pathfinder's root: 129-258 MB separator aggregates broadcast over
+  // its other variables).  Knob PGM_MARG_KORDER=0 keeps the clique's label order.
+  static const bool korder = !(getenv("PGM_MARG_KORDER") && atoi(getenv("PGM_MARG_KORDER")) == 0);
+  if (korder && k.nk > 1) {
+    double score[KMAX];
+    for (int i = 0; i < k.nk; ++i) {
+      score[i] = 0.0;
+      for (int t = 0; t < d->n_ops; ++t) {
+        if (!k.vec[t] || k.ks[t][i] != 0) continue;
+        double size = 1.0;  // the operand's elements per row
+        for (int q = 0; q < k.nk; ++q)
+          if (k.ks[t][q] != 0) size *= (double)k.kdiv[q].d;
+        for (int r = 0; r < k.nr; ++r)
+          if (k.rs[t][r] != 0) size *= (double)k.rdiv[r].d;
+        score[i] += size;
+      }
+    }
+    int ord[KMAX];
+    for (int i = 0; i < k.nk; ++i) ord[i] = i;
+    std::stable_sort(ord, ord + k.nk, [&](int a, int b) { return score[a] < score[b]; });
+    ProdMK k2 = k;
+    for (int i = 0; i < k.nk; ++i) {
+      const int o = ord[i];
+      k2.kdiv[i] = k.kdiv[o];
+      k2.ksc[i] = k.ksc[o];
+      k2.ksm[i] = k.ksm[o];
+      for (int t = 0; t < MOPS; ++t) k2.ks[t][i] = k.ks[t][o];
+    }
+    k = k2;
+  }
   for (int t = 0; t < MOPS; ++t) {
     k.jvar[t] = 0;
     for (int r = 0; t < d->n_ops && r < k.nr; ++r) k.jvar[t] |= k.rs[t][r] != 0;
