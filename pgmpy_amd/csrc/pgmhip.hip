@@ -2451,7 +2451,8 @@ static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, i
   static const bool off = getenv("PGM_NO_JIT2") != nullptr;  // testing / tuning
   // measured (MI355X): one row per thread is faster while the launch is latency-bound (100k rows:
   // 4.6 vs 5.2 us), two rows with 16-B stores once it is HBM-bound (4M rows: 110 vs 126 us)
-  if (off || n_rows < 400000 || n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
+  static const int64_t min_rows = getenv("PGM_JIT2_MIN_ROWS") ? atoll(getenv("PGM_JIT2_MIN_ROWS")) : 400000;
+  if (off || n_rows < min_rows || n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
   if ((mode & PGM_ROWS_MARGINALS) && (((uintptr_t)marg & 15) || ld_out % 2)) return false;
   if (map && ((uintptr_t)map & 7)) return false;
   if ((mode & PGM_ROWS_MAPGAP) && gap && ((uintptr_t)gap & 15)) return false;
