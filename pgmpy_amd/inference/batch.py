@@ -339,6 +339,8 @@ def predict_probability_frame(model, data):
     missing_variables = set(model.nodes()) - set(data.columns)
     order = list(missing_variables)  # the reference's set iteration order (column order of its output)
     n = len(data)
+    if n == 0:  # the reference builds its frame from empty per-column lists: no columns at all
+        return pd.DataFrame({}, index=data.index)
     cols = {}
     for var in order:
         for s in model.get_cpds(var).state_names[var]:
@@ -357,6 +359,8 @@ def predict_frame(model, data):
 
     missing_variables = set(model.nodes()) - set(data.columns)
     order = list(missing_variables)
+    if len(data) == 0:  # the reference indexes the first group of an empty groupby
+        raise IndexError("list index out of range (predict on an empty DataFrame)")
     vals = {c: np.full(len(data), np.nan, dtype=object) for c in order}
     # the observed columns keep their dtype (object frames stay object, as the reference's merge
     # leaves them; a categorical frame is not expanded to 10^8 Python objects)
@@ -404,6 +408,8 @@ def predict_stochastic_frame(model, data, seed=None):
     missing_variables = set(model.nodes()) - set(data.columns)
     order = list(missing_variables)
     n = len(data)
+    if n == 0:
+        raise IndexError("list index out of range (predict on an empty DataFrame)")
     ev = ingest_frame(model, data, columns, row_hash=True)
     _, first, inv = np.unique(ev.row_hash, axis=0, return_index=True, return_inverse=True)
     inv = inv.reshape(-1)
