@@ -144,6 +144,23 @@ int pgm_product_n_marginal_ok(const pgm_productn_desc *d, const double *const *o
 int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops, double *C,
                            const int64_t *marg_s, int32_t reduce, double *M, void *stream);
 
+/* The same fused step bound to its pointers with the plan compiled in (hipRTC, gfx950): kept /
+ * reduced index spaces, strides and operand kinds as literals, the reduced entries as unrolled loops.
+ * *bound = NULL (PGM_OK) when the generic kernel should run instead (clique below the size threshold,
+ * or PGM_PM_JIT=0 / PGM_NO_JIT set, or the compile failed); the same shape errors as
+ * pgm_product_n_marginal otherwise.  pgm_pm_bound_run launches it on stream (capturable in a
+ * graph); the pointers must stay valid until pgm_pm_bound_destroy.  Replaces the per-step
+ * DiscreteFactor.product / marginalize pair of a batched calibration (ExactInference.py:784-802). */
+int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                const int64_t *marg_s, int32_t reduce, double *M, void **bound);
+/* The generated kernel source for the same arguments (no compile, no GPU): returns its length (0
+ * when the generic kernel would run), copies at most len-1 bytes + NUL into buf.  Inspection and
+ * host-side tests. */
+int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                  const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len);
+int pgm_pm_bound_run(void *bound, void *stream);
+int pgm_pm_bound_destroy(void *bound);
+
 /* ---------------------------------------------------------------- dense pairwise step (FP64 MFMA)
  * C[b, m, n] = sum_k A[b, m, k] * B[b, k, n] where each index is a GROUP of variables laid out in
  * any order inside its tensor: the element offsets come from a DEVICE int64 table,

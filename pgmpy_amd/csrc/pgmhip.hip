@@ -29,7 +29,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 10  // 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 11  // 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -2508,6 +2508,200 @@ static bool rows_jit_ready(RowsHandle *h) {
   return true;
 }
 
+// ----------------------------------------------------------------------------- specialised product+marginal
+// The fused batched-BP step (k_productn_marg_jx) with its plan baked in as literals: outer digits
+// decoded with constant divisors, the reduced entries walked as nested loops with literal bounds and
+// strides (inner ones unrolled, so several entries' operand loads are in flight together), operands
+// that lack the row axis read at wave-uniform addresses (scalar loads), one 1-D grid with an optional
+// XCD-grouped block order.  Compiled once per shape (hipRTC, cached by source), bound to its
+// pointers, launched by pgm_pm_bound_run (capturable in a HIP graph).
+struct PMBound {
+  hipFunction_t fn = nullptr;
+  unsigned blocks = 0;
+  const double *ops[MOPS] = {};
+  double *C = nullptr, *M = nullptr;
+};
+
+static int pm_knob(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+static std::string pm_source(const ProdMK &k, int red, int XI, bool store, unsigned gx, uint64_t total, bool xcd,
+                             bool nt, int unroll) {
+  std::string o =
+      "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
+      "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
+      "__device__ __forceinline__ double pgm_ratio(double a, double b) { const double r = a / b; "
+      "return r != r ? 0.0 : r; }\n"
+      "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
+  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const double *__restrict__ o0, "
+       "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
+       "double *__restrict__ C, double *__restrict__ M) {\n";
+  o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
+  o += "  unsigned b = blockIdx.x;\n";
+  if (xcd) appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n",
+                   (unsigned long long)(total / 8));
+  appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
+  o += "  unsigned idx = ob;\n  long long oc = 0, om = 0";
+  for (int i = 0; i < k.n_ops; ++i) appendf(o, ", f%d = 0", i);
+  o += ";\n  (void)oc; (void)idx;\n";
+  const int kx = k.nk - 1;  // kept outer dims 0..kx-1 (kx-1 fastest), the row dim last
+  for (int q = kx - 1; q >= 0; --q) {
+    const unsigned dq = k.kdiv[q].d;
+    appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", dq, dq);
+    if (k.ksc[q]) appendf(o, " oc += (long long)g * %lldLL;", (long long)k.ksc[q]);
+    if (k.ksm[q]) appendf(o, " om += (long long)g * %lldLL;", (long long)k.ksm[q]);
+    for (int i = 0; i < k.n_ops; ++i)
+      if (k.ks[i][q]) appendf(o, " f%d += (long long)g * %lldLL;", i, (long long)k.ks[i][q]);
+    o += " }\n";
+  }
+  const uint32_t NP = k.NP;
+  const bool tail = NP % (256u * XI) != 0;
+  appendf(o, "  const unsigned xbase = xb * %uu + threadIdx.x;\n", 256u * XI);
+  for (int u = 0; u < XI; ++u) {
+    appendf(o, "  const unsigned x%d = xbase + %uu;\n", u, 256u * u);
+    if (tail)
+      appendf(o, "  const unsigned c%d = x%d < %uu ? x%d : %uu;\n", u, u, NP, u, NP - 1);
+    else
+      appendf(o, "  const unsigned c%d = x%d;\n", u, u);
+  }
+  // operands constant over the reduced entries: once per block
+  for (int i = 0; i < k.n_ops; ++i) {
+    if (k.jvar[i]) continue;
+    if (k.vec[i]) {
+      for (int u = 0; u < XI; ++u)
+        appendf(o, "  const pgm_d2 h%d_%d = ((const pgm_d2 *)(o%d + f%d))[c%d];\n", i, u, i, i, u);
+    } else {
+      appendf(o, "  const double h%d = o%d[f%d];\n", i, i, i);
+    }
+  }
+  const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
+  for (int u = 0; u < XI; ++u) appendf(o, "  pgm_d2 a%d = {%s, %s};\n", u, init, init);
+  // reduced dims as nested loops (dim 0 outermost: the generic kernel's entry order); the innermost
+  // dims whose trip product stays within `unroll` are unrolled
+  int first_unrolled = k.nr;
+  {
+    uint64_t prod = 1;
+    for (int r = k.nr - 1; r >= 0; --r) {
+      prod *= k.rdiv[r].d;
+      if (prod > (uint64_t)unroll) break;
+      first_unrolled = r;
+    }
+  }
+  std::string ind = "  ";
+  for (int r = 0; r < k.nr; ++r) {
+    if (r >= first_unrolled)
+      appendf(o, "%s#pragma unroll\n", ind.c_str());
+    else if (r == k.nr - 1)  // an innermost loop too long to unroll fully: `unroll` entries at a time
+      appendf(o, "%s#pragma unroll %d\n", ind.c_str(), std::max(1, unroll));
+    else
+      appendf(o, "%s#pragma unroll 1\n", ind.c_str());
+    appendf(o, "%sfor (int r%d = 0; r%d < %u; ++r%d) {\n", ind.c_str(), r, r, k.rdiv[r].d, r);
+    ind += "  ";
+  }
+  auto lin = [&](const int64_t *s) {  // literal offset of the current reduced entry
+    std::string e = "0LL";
+    for (int r = 0; r < k.nr; ++r)
+      if (s[r]) e += " + (long long)r" + std::to_string(r) + " * " + std::to_string((long long)s[r]) + "LL";
+    return e;
+  };
+  for (int i = 0; i < k.n_ops; ++i) {
+    if (!k.jvar[i]) continue;
+    const std::string J = lin(k.rs[i]);
+    if (k.vec[i]) {
+      appendf(o, "%sconst pgm_d2 *p%d = (const pgm_d2 *)(o%d + f%d + %s);\n", ind.c_str(), i, i, i, J.c_str());
+      for (int u = 0; u < XI; ++u) appendf(o, "%sconst pgm_d2 v%d_%d = p%d[c%d];\n", ind.c_str(), i, u, i, u);
+    } else {
+      appendf(o, "%sconst double s%d = o%d[f%d + %s];\n", ind.c_str(), i, i, i, J.c_str());
+    }
+  }
+  for (int u = 0; u < XI; ++u) {
+    for (int h = 0; h < 2; ++h) {
+      const char cx = h ? 'y' : 'x';
+      auto term = [&](int i) {
+        char buf[64];
+        if (k.jvar[i] && k.vec[i]) snprintf(buf, sizeof buf, "v%d_%d.%c", i, u, cx);
+        else if (k.jvar[i]) snprintf(buf, sizeof buf, "s%d", i);
+        else if (k.vec[i]) snprintf(buf, sizeof buf, "h%d_%d.%c", i, u, cx);
+        else snprintf(buf, sizeof buf, "h%d", i);
+        return std::string(buf);
+      };
+      std::string e = "1.0";
+      for (int i = 0; i < k.n_ops; ++i) {
+        if (k.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
+        else if (k.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
+          e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+      }
+      appendf(o, "%sconst double w%d%c = %s;\n", ind.c_str(), u, cx, e.c_str());
+    }
+    appendf(o, "%sconst pgm_d2 w%d = {w%dx, w%dy};\n", ind.c_str(), u, u, u);
+  }
+  if (store) {
+    appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
+    for (int u = 0; u < XI; ++u) {
+      const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
+      if (nt)
+        appendf(o, "%s%s__builtin_nontemporal_store(w%d, cj + x%d);\n", ind.c_str(), guard.c_str(), u, u);
+      else
+        appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
+    }
+  }
+  for (int u = 0; u < XI; ++u) {
+    if (red == PGM_RED_MAX)
+      appendf(o, "%sa%d.x = pgm_maxn(a%d.x, w%d.x); a%d.y = pgm_maxn(a%d.y, w%d.y);\n", ind.c_str(), u, u, u, u,
+              u, u);
+    else
+      appendf(o, "%sa%d += w%d;\n", ind.c_str(), u, u);
+  }
+  for (int r = k.nr - 1; r >= 0; --r) {
+    ind.resize(ind.size() - 2);
+    appendf(o, "%s}\n", ind.c_str());
+  }
+  for (int u = 0; u < XI; ++u) {
+    const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
+    appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
+  }
+  o += "}\n";
+  return o;
+}
+
+static std::mutex g_pm_mu;
+static std::vector<std::pair<std::string, hipFunction_t>> g_pm_cache;  // source -> kernel (process lifetime)
+
+static hipFunction_t pm_compile(const std::string &src) {
+  std::lock_guard<std::mutex> lk(g_pm_mu);
+  for (auto &e : g_pm_cache)
+    if (e.first == src) return e.second;
+  std::lock_guard<std::mutex> lk2(g_rtc_mu);
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_pm.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return nullptr;
+  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    fprintf(stderr, "pgmhip: specialised product+marginal kernel did not compile (generic kernel used):\n%s\n",
+            log.c_str());
+    hiprtcDestroyProgram(&prog);
+    return nullptr;
+  }
+  size_t sz = 0;
+  hiprtcGetCodeSize(prog, &sz);
+  std::vector<char> code(sz);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "pgm_pm") != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  g_pm_cache.emplace_back(src, fn);
+  return fn;
+}
+
 // ============================================================================= C-ABI
 extern "C" {
 
@@ -2827,6 +3021,100 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
   }
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double *C, const int64_t *marg_s,
+                   int32_t reduce, double *M, void **bound, std::string *src_out) {
+  *bound = nullptr;
+  if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
+    return fail(PGM_EINVAL, "product_n_marginal: reduce must be PGM_RED_SUM or PGM_RED_MAX");
+  ProdMK k;
+  dim3 g;
+  const int r = plan_product_marg(d, ops, C, marg_s, M, k, g);
+  if (r < 0) return r;
+  if (r == 0)
+    return fail(PGM_EINVAL, "product_n_marginal: shape not supported by the fused kernel "
+                            "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
+  // knobs: PGM_PM_JIT=0 keeps the generic kernel; PGM_PM_JIT_MIN = smallest clique (entries incl.
+  // rows) specialised; PGM_PM_XI row pairs per lane; PGM_PM_UNROLL entries unrolled; PGM_PM_XCD
+  // block order grouped by XCD; PGM_PM_NT nontemporal belief stores
+  static const int on = pm_knob("PGM_PM_JIT", 1);
+  // defaults measured on MI355X, pathfinder C4 (4,000 / 1,000 rows: generic 781K / 515K calibrations/s;
+  // specialised above 2M entries 911K / 601K; + one row pair per lane, nontemporal belief stores and
+  // XCD-grouped blocks 933K; threshold 256K entries 648K at 1,000 rows)
+  static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 18);
+  static const int xi_knob = pm_knob("PGM_PM_XI", 1);
+  static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
+  static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
+  static const int nt = pm_knob("PGM_PM_NT", 1);
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
+  const uint64_t entries = (uint64_t)k.n_outer * (uint64_t)k.n_red * 2ull * k.NP;
+  if (!on || no_jit || entries < (uint64_t)min_entries) return PGM_OK;  // *bound NULL: generic kernel
+  const int XI = xi_knob == 2 || xi_knob == 4 ? xi_knob : 1;
+  const uint64_t gx = (k.NP + 256ull * XI - 1) / (256ull * XI);
+  const uint64_t total = gx * (uint64_t)k.n_outer;
+  if (total >= (1ull << 31)) return PGM_OK;
+  const bool xcd = xcd_knob && total % 8 == 0;
+  const std::string src = pm_source(k, reduce, XI, C != nullptr, (unsigned)gx, total, xcd, nt != 0, unroll);
+  if (src_out) {
+    *src_out = src;
+    return PGM_OK;
+  }
+  hipFunction_t fn = pm_compile(src);
+  if (!fn) return PGM_OK;
+  PMBound *b = new (std::nothrow) PMBound;
+  if (!b) return fail(PGM_ENOMEM, "product_n_marginal_bind: out of host memory");
+  b->fn = fn;
+  b->blocks = (unsigned)total;
+  for (int t = 0; t < MOPS; ++t) b->ops[t] = k.ops[t];
+  b->C = C;
+  b->M = M;
+  *bound = b;
+  return PGM_OK;
+}
+
+int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                const int64_t *marg_s, int32_t reduce, double *M, void **bound) {
+  STALE_PROBE();
+  if (!bound) return fail(PGM_EINVAL, "product_n_marginal_bind: null bound");
+  return pm_bind(d, ops, C, marg_s, reduce, M, bound, nullptr);
+}
+
+int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                  const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len) {
+  STALE_PROBE();
+  if (!buf || len == 0) return fail(PGM_EINVAL, "product_n_marginal_source: null buffer");
+  void *unused = nullptr;
+  std::string src;
+  const int r = pm_bind(d, ops, C, marg_s, reduce, M, &unused, &src);
+  if (r < 0) return r;
+  const size_t n = std::min(len - 1, src.size());
+  memcpy(buf, src.data(), n);
+  buf[n] = 0;
+  return (int)src.size();
+}
+
+int pgm_pm_bound_run(void *bound, void *stream) {
+  STALE_PROBE();
+  PMBound *b = (PMBound *)bound;
+  if (!b) return fail(PGM_EINVAL, "pm_bound_run: null bound");
+  struct {
+    const double *o[MOPS];
+    double *C, *M;
+  } args;
+  for (int t = 0; t < MOPS; ++t) args.o[t] = b->ops[t];
+  args.C = b->C;
+  args.M = b->M;
+  size_t sz = sizeof args;
+  void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(stream), nullptr, extra));
+  return PGM_OK;
+}
+
+int pgm_pm_bound_destroy(void *bound) {
+  STALE_PROBE();
+  delete (PMBound *)bound;
   return PGM_OK;
 }
 

@@ -61,6 +61,7 @@ class Program:
         self._stream = None
         self._batch = None
         self._handles = []
+        self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
@@ -218,7 +219,14 @@ class Program:
                 L = N.lib()
                 self._keep.extend([d, ptrs, out2, ms, M] + [t for t, _ in ops])
                 args = (ctypes.byref(d), ptrs, N.ptr(out2) if store else None, ms, E._REDUCE[reduce], N.ptr(M))
-                self._emit(lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal"),
+                bound = ctypes.c_void_p()
+                N.check(L.pgm_product_n_marginal_bind(*args, ctypes.byref(bound)), "product_n_marginal_bind")
+                if bound.value:  # the plan compiled into a specialised kernel
+                    self._pm_bound.append(bound)
+                    fn = lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
+                else:
+                    fn = lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal")
+                self._emit(fn,
                            f"product_n_marginal{'' if store else ' (marginal only)'} "
                            f"{[(list(ls), tuple(t.shape)) for t, ls in ops]} "
                            f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}",
@@ -347,6 +355,8 @@ class Program:
                 L.pgm_graph_destroy(g)
             for h in getattr(self, "_handles", []):
                 L.pgm_batch_destroy(h)
+            for h in getattr(self, "_pm_bound", []):
+                L.pgm_pm_bound_destroy(h)
         except Exception:
             pass
 

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 10
+    assert lib.pgm_version() == 11
 
 
 def test_struct_layouts_match_header():
@@ -285,3 +285,63 @@ def test_hip_backend_config_mirrors_pgmpy_config():
         assert compat.get_compute_backend() is np  # module config untouched
     cfg.set_backend("numpy")
     assert cfg.get_device() is None
+
+
+def _pm_desc(N, shapes_labels, out_labels, card, kinds=None):
+    """ProductNDesc for C-order operands (numpy element strides), out C-order over out_labels."""
+    import numpy as np
+
+    d = N.ProductNDesc()
+    d.n_ops, d.n_keep = len(shapes_labels), len(out_labels)
+    for i, k in enumerate(kinds or []):
+        d.op_kind[i] = int(k)
+    out_shape = [card[l] for l in out_labels]
+    out_st = [s // 8 for s in np.empty(out_shape).strides]
+    for i, l in enumerate(out_labels):
+        d.keep_card[i], d.keep_sc[i] = card[l], out_st[i]
+        for t, ls in enumerate(shapes_labels):
+            st = [s // 8 for s in np.empty([card[x] for x in ls]).strides]
+            d.keep_s[t][i] = st[ls.index(l)] if l in ls else 0
+    return d
+
+
+@pytest.mark.parametrize("red,store,ratio", [(1, True, False), (2, True, True), (1, False, True)])
+def test_product_marginal_specialised_source_compiles(tmp_path, red, store, ratio):
+    """The specialised product+marginal kernel the bind entry point would compile (hipRTC on the
+    GPU box) is generated on the host and compiles for gfx950 with hipcc: literal outer decode,
+    nested reduced loops, ratio operands, marginal-only form."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    import numpy as np
+
+    from pgmpy_amd import _native as N
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    L = N.load_library()
+    R = "__row__"
+    card = dict(zip(list("abcdef") + [R], (8, 2, 3, 8, 5, 9, 2100)))
+    cl = list("abcdef") + [R]
+    ops = [list("abcdef"), ["a", "c", "f", R]]
+    kinds = None
+    if ratio:
+        ops = [cl, ["a", "d", "f", R], ["a", "d", "f", R]]
+        kinds = [N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN]
+    d = _pm_desc(N, ops, cl, card, kinds)
+    marg = ["a", "d", "e", R]
+    m_st = [s // 8 for s in np.empty([card[x] for x in marg]).strides]
+    ms = (ctypes.c_int64 * len(cl))(*[m_st[marg.index(l)] if l in marg else 0 for l in cl])
+    fake = [0x10000000 * (i + 1) for i in range(len(ops))]  # 16-B aligned, never dereferenced
+    ptrs = (ctypes.c_void_p * len(ops))(*fake)
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = L.pgm_product_n_marginal_source(ctypes.byref(d), ptrs, ctypes.c_void_p(0x70000000) if store else None, ms,
+                                        red, ctypes.c_void_p(0x60000000), buf, len(buf))
+    assert n > 0, "shape should specialise"
+    src = buf.value.decode()
+    assert "pgm_pm" in src and ("* pgm_ratio(" in src) == ratio and ("cj[" in src or "nontemporal" in src) == store
+    f = tmp_path / "pm.hip"
+    f.write_text("#include <hip/hip_runtime.h>\n" + src)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-c", str(f), "-o",
+                        str(tmp_path / "pm.o")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -506,6 +506,73 @@ def test_product_n_marginal_fused(gpu, rows, red):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("rows,red,store", [(1000, "sum", True), (2048, "sum", True), (2100, "max", True),
+                                            (2100, "sum", False), (4000, "sum", True)])
+def test_product_n_marginal_bound_matches_generic(gpu, rows, red, store):
+    """pgm_product_n_marginal_bind: the plan compiled into a specialised kernel gives the generic
+    fused kernel's C bit for bit and M to 1e-14 (same product and reduction order; only FMA
+    contraction may differ): row tails (rows/2 not a
+    multiple of the block's row pairs), 1 and 2 row pairs per lane, max-product, marginal only, and
+    the in-place ratio update beta *= sigma / mu (0/0 -> 0) with operands that lack the row axis."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    L = NN.lib()
+    rng = np.random.default_rng(rows)
+    cl = list("abcdef")
+    card = dict(zip(cl, (8, 2, 3, 8, 5, 9)))
+    sh = [card[v] for v in cl]
+    R = E.ROW
+    psi = E.to_device(rng.random(sh))
+    msg = E.to_device(rng.random([card["a"], card["c"], card["f"], rows]))
+    sig = rng.random([card["a"], card["d"], card["f"], rows])
+    mu = rng.random([card["a"], card["d"], card["f"], rows])
+    sig[0, 0, 0, :5] = 0.0
+    mu[0, 0, 0, :5] = 0.0
+    sig, mu = E.to_device(sig), E.to_device(mu)
+    red_c = E._REDUCE[red]
+
+    def both(ops, marg, kinds=None, inplace=None):
+        outs = []
+        for bound_path in (False, True):
+            base = inplace.clone() if inplace is not None else None
+            o = [(base, ls) if t is inplace else (t, ls) for t, ls in ops]
+            d, ptrs, C, ms, M, ok = E.prepare_product_n_marginal(o, cl + [R], marg, base, kinds, store)
+            assert ok
+            args = (ctypes.byref(d), ptrs, NN.ptr(C) if store else None, ms, red_c, NN.ptr(M))
+            s = NN.stream_handle()
+            if bound_path:
+                b = ctypes.c_void_p()
+                NN.check(L.pgm_product_n_marginal_bind(*args, ctypes.byref(b)), "bind")
+                assert b.value, "shape above the specialisation threshold must bind"
+                NN.check(L.pgm_pm_bound_run(b, s), "run")
+                torch.cuda.synchronize()
+                L.pgm_pm_bound_destroy(b)
+            else:
+                NN.check(L.pgm_product_n_marginal(*args, s), "generic")
+            outs.append((E.to_host(C) if store else None, E.to_host(M)))
+        (c0, m0), (c1, m1) = outs
+        if store:
+            np.testing.assert_array_equal(c1, c0)
+        # same summation order; the generic kernel may fuse a product into the running sum (FMA)
+        np.testing.assert_allclose(m1, m0, rtol=1e-14, atol=0)
+        return c0, m0
+
+    c0, m0 = both([(psi, cl), (msg, ["a", "c", "f", R])], ["a", "d", "f", R])
+    if store:
+        full = E.to_host(psi)[..., None] * E.to_host(msg)[:, None, :, None, None, :, :]
+        np.testing.assert_array_equal(c0, full)
+    beta = E.to_device(rng.random(sh + [rows]))
+    both([(beta, cl + [R]), (sig, ["a", "d", "f", R]), (mu, ["a", "d", "f", R])], ["a", "d", "e", R],
+         kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN], inplace=beta)
+    both([(psi, cl), (sig, ["a", "d", "f", R]), (mu, ["a", "d", "f", R]), (msg, ["a", "c", "f", R])],
+         ["a", "c", "e", "f", R], kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN, NN.PRODN_MUL])
+
+
 def test_bp_fused_marginals_many_rows(gpu):
     """Batched BP with >= 64 evidence rows takes the fused belief + separator-marginal kernels;
     calibrated beliefs must equal the unfused schedule's (single-row calibrations)."""
