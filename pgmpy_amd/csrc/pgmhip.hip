@@ -26,6 +26,9 @@
 #include <string>
 #include <vector>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
@@ -2465,6 +2468,93 @@ static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, i
 
 static std::mutex g_rtc_mu;  // hipRTC program creation is serialised (one compile at a time)
 
+// On-disk cache of specialised code objects: directory PGM_KERNEL_CACHE (default
+// $XDG_CACHE_HOME/pgmpy_amd or ~/.cache/pgmpy_amd; "0" disables), one file per source hash holding
+// the full source (compared on load, so a hash collision only misses) and the gfx950 code object.
+static std::string rtc_cache_dir() {
+  static const std::string dir = [] {
+    const char *e = getenv("PGM_KERNEL_CACHE");
+    if (e) return std::string(strcmp(e, "0") == 0 ? "" : e);
+    const char *x = getenv("XDG_CACHE_HOME");
+    if (x && *x) return std::string(x) + "/pgmpy_amd";
+    const char *h = getenv("HOME");
+    return h && *h ? std::string(h) + "/.cache/pgmpy_amd" : std::string();
+  }();
+  return dir;
+}
+
+static std::string rtc_cache_path(const std::string &src) {
+  const std::string dir = rtc_cache_dir();
+  if (dir.empty()) return dir;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the source and the ABI version
+  for (unsigned char c : src) h = (h ^ c) * 1099511628211ull;
+  h = (h ^ (uint64_t)PGM_ABI_VERSION) * 1099511628211ull;
+  char name[64];
+  snprintf(name, sizeof name, "/k%016llx.co", (unsigned long long)h);
+  return dir + name;
+}
+
+static bool rtc_cache_load(const std::string &path, const std::string &src, std::vector<char> &code) {
+  if (path.empty()) return false;
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint64_t n = 0, m = 0;
+  bool ok = fread(&n, 8, 1, f) == 1 && n == src.size();
+  std::string s2;
+  if (ok) {
+    s2.resize(n);
+    ok = fread(&s2[0], 1, n, f) == n && s2 == src && fread(&m, 8, 1, f) == 1 && m > 0 && m < (1ull << 30);
+  }
+  if (ok) {
+    code.resize(m);
+    ok = fread(code.data(), 1, m, f) == m;
+  }
+  fclose(f);
+  return ok;
+}
+
+static void rtc_cache_store(const std::string &path, const std::string &src, const std::vector<char> &code) {
+  if (path.empty()) return;
+  const std::string dir = path.substr(0, path.rfind('/'));
+  // mkdir -p: create each component
+  for (size_t i = 1; i <= dir.size(); ++i)
+    if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+  const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
+  FILE *f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const uint64_t n = src.size(), m = code.size();
+  const bool ok = fwrite(&n, 8, 1, f) == 1 && fwrite(src.data(), 1, n, f) == n && fwrite(&m, 8, 1, f) == 1 &&
+                  fwrite(code.data(), 1, m, f) == m;
+  if (fclose(f) == 0 && ok) (void)rename(tmp.c_str(), path.c_str());
+  else (void)remove(tmp.c_str());
+}
+
+// gfx950 code object of a specialised kernel source: the disk cache, else hipRTC (then cached)
+static bool rtc_code(const std::string &src, const char *what, std::vector<char> &code) {
+  const std::string path = rtc_cache_path(src);
+  if (rtc_cache_load(path, src, code)) return true;
+  std::lock_guard<std::mutex> lk(g_rtc_mu);
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return false;
+  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    fprintf(stderr, "pgmhip: %s did not compile (generic kernel used):\n%s\n", what, log.c_str());
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t sz = 0;
+  hiprtcGetCodeSize(prog, &sz);
+  code.resize(sz);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  rtc_cache_store(path, src, code);
+  return true;
+}
+
 // compile + load the handle's specialised kernel once; false when unavailable (AOT kernels run)
 static bool rows_jit_ready(RowsHandle *h) {
   if (h->jit_src.empty()) return false;
@@ -2473,26 +2563,8 @@ static bool rows_jit_ready(RowsHandle *h) {
   h->jit_state = -1;
   static const bool disabled = getenv("PGM_NO_JIT") != nullptr;  // testing: AOT kernels only
   if (disabled) return false;
-  std::lock_guard<std::mutex> lk2(g_rtc_mu);
-  hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, h->jit_src.c_str(), "pgm_rows_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
-    return false;
-  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 2, opts);
-  if (rc != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    fprintf(stderr, "pgmhip: specialised row kernel did not compile (generic kernels used):\n%s\n", log.c_str());
-    hiprtcDestroyProgram(&prog);
-    return false;
-  }
-  size_t sz = 0;
-  hiprtcGetCodeSize(prog, &sz);
-  std::vector<char> code(sz);
-  hiprtcGetCode(prog, code.data());
-  hiprtcDestroyProgram(&prog);
+  std::vector<char> code;
+  if (!rtc_code(h->jit_src, "specialised row kernel", code)) return false;
   h->jit_code = code;
   if (hipModuleLoadData(&h->jit_mod, code.data()) != hipSuccess) {
     (void)hipGetLastError();
@@ -2673,25 +2745,8 @@ static hipFunction_t pm_compile(const std::string &src) {
   std::lock_guard<std::mutex> lk(g_pm_mu);
   for (auto &e : g_pm_cache)
     if (e.first == src) return e.second;
-  std::lock_guard<std::mutex> lk2(g_rtc_mu);
-  hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_pm.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return nullptr;
-  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    fprintf(stderr, "pgmhip: specialised product+marginal kernel did not compile (generic kernel used):\n%s\n",
-            log.c_str());
-    hiprtcDestroyProgram(&prog);
-    return nullptr;
-  }
-  size_t sz = 0;
-  hiprtcGetCodeSize(prog, &sz);
-  std::vector<char> code(sz);
-  hiprtcGetCode(prog, code.data());
-  hiprtcDestroyProgram(&prog);
+  std::vector<char> code;
+  if (!rtc_code(src, "specialised product+marginal kernel", code)) return nullptr;
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
   if (hipModuleLoadData(&mod, code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "pgm_pm") != hipSuccess) {

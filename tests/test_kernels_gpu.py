@@ -692,3 +692,25 @@ def test_bp_levelled_findings_batch_flags_bad_codes(gpu):
     sch.run(codes)
     torch.cuda.synchronize()
     assert int(sch.err.item()) != 0
+
+
+def test_specialised_kernel_disk_cache(gpu, tmp_path):
+    """Specialised kernels are written to the code-object cache (PGM_KERNEL_CACHE) on first use and
+    loaded from it by a later process: same kernels, no new files, identical beliefs."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PGM_KERNEL_CACHE=str(tmp_path / "kc"))
+    runs = []
+    for _ in range(2):
+        r = subprocess.run([sys.executable, os.path.join(root, "tests", "workers", "pm_cache.py")], cwd=root,
+                           env=env, timeout=240, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    a, b = runs
+    assert a["bound"] > 0 and a["files"] >= a["bound"] // 2, a  # shapes may repeat across steps
+    assert b["bound"] == a["bound"] and b["files"] == a["files"], (a, b)
+    assert b["checksum"] == a["checksum"]
