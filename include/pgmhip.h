@@ -159,6 +159,11 @@ int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const 
 int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
                                   const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len);
 int pgm_pm_bound_run(void *bound, void *stream);
+/* Several bound steps with no dependence between them (one level of a batched-BP sweep) as ONE
+ * launch: a kernel whose block ranges run the steps' bodies.  *merged = NULL (PGM_OK) when the merge
+ * is not possible (grid too large, compile failed): launch the steps separately.  The inputs stay
+ * valid and owned by the caller; destroy the merged handle with pgm_pm_bound_destroy. */
+int pgm_pm_merge(void *const *bounds, int32_t n, void **merged);
 int pgm_pm_bound_destroy(void *bound);
 
 /* ---------------------------------------------------------------- dense pairwise step (FP64 MFMA)

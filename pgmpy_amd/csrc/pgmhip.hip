@@ -2587,11 +2587,22 @@ static bool rows_jit_ready(RowsHandle *h) {
 // that lack the row axis read at wave-uniform addresses (scalar loads), one 1-D grid with an optional
 // XCD-grouped block order.  Compiled once per shape (hipRTC, cached by source), bound to its
 // pointers, launched by pgm_pm_bound_run (capturable in a HIP graph).
+struct PMSpec {  // one fused step's specialisation
+  ProdMK k;
+  int red = PGM_RED_SUM, XI = 1, unroll = 8;
+  bool store = true, xcd = false, nt = false;
+  unsigned gx = 1;
+  uint64_t total = 0;  // blocks
+};
+
+// a bound launch: one step, or several independent steps merged into one kernel (pgm_pm_merge:
+// body i runs on blocks [start_i, start_i + total_i), starts padded to multiples of 8 so each body's
+// XCD grouping holds)
 struct PMBound {
   hipFunction_t fn = nullptr;
   unsigned blocks = 0;
-  const double *ops[MOPS] = {};
-  double *C = nullptr, *M = nullptr;
+  std::vector<PMSpec> specs;
+  std::vector<const double *> ptrs;  // 6 per body: o0..o3, C, M
 };
 
 static int pm_knob(const char *name, int dflt) {
@@ -2599,19 +2610,18 @@ static int pm_knob(const char *name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-static std::string pm_source(const ProdMK &k, int red, int XI, bool store, unsigned gx, uint64_t total, bool xcd,
-                             bool nt, int unroll) {
-  std::string o =
-      "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
-      "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
-      "__device__ __forceinline__ double pgm_ratio(double a, double b) { const double r = a / b; "
-      "return r != r ? 0.0 : r; }\n"
-      "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
-  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const double *__restrict__ o0, "
-       "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
-       "double *__restrict__ C, double *__restrict__ M) {\n";
+// body `name` of one step: a device function of its block index within the step
+static std::string pm_body(const PMSpec &sp, const std::string &name) {
+  const ProdMK &k = sp.k;
+  const int red = sp.red, XI = sp.XI, unroll = sp.unroll;
+  const bool store = sp.store, xcd = sp.xcd, nt = sp.nt;
+  const unsigned gx = sp.gx;
+  const uint64_t total = sp.total;
+  std::string o;
+  appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
+             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
+             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
   o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
-  o += "  unsigned b = blockIdx.x;\n";
   if (xcd) appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n",
                    (unsigned long long)(total / 8));
   appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
@@ -2733,6 +2743,42 @@ static std::string pm_source(const ProdMK &k, int red, int XI, bool store, unsig
   for (int u = 0; u < XI; ++u) {
     const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
     appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
+  }
+  o += "}\n";
+  return o;
+}
+
+// kernel pgm_pm over the bodies (kernel argument: 6 pointers per body); starts[i] = first block of
+// body i, returns the grid size through *blocks
+static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint64_t> &starts, uint64_t *blocks) {
+  std::string o =
+      "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
+      "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
+      "__device__ __forceinline__ double pgm_ratio(double a, double b) { const double r = a / b; "
+      "return r != r ? 0.0 : r; }\n"
+      "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
+  const size_t n = specs.size();
+  starts.assign(n, 0);
+  uint64_t at = 0;
+  for (size_t i = 0; i < n; ++i) {
+    at = (at + 7) / 8 * 8;
+    starts[i] = at;
+    at += specs[i].total;
+    o += pm_body(specs[i], "pm" + std::to_string(i));
+  }
+  *blocks = at;
+  appendf(o, "struct pgm_pm_args { const double *p[%zu][6]; };\n", n);
+  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const pgm_pm_args a) {\n"
+       "  const unsigned b = blockIdx.x;\n";
+  for (size_t i = 0; i < n; ++i) {
+    if (n == 1) {
+      o += "  pm0(b, a.p[0][0], a.p[0][1], a.p[0][2], a.p[0][3], (double *)a.p[0][4], (double *)a.p[0][5]);\n";
+      break;
+    }
+    appendf(o, "  if (b >= %lluu && b < %lluu) { pm%zu(b - %lluu, a.p[%zu][0], a.p[%zu][1], a.p[%zu][2], "
+               "a.p[%zu][3], (double *)a.p[%zu][4], (double *)a.p[%zu][5]); return; }\n",
+            (unsigned long long)starts[i], (unsigned long long)(starts[i] + specs[i].total), i,
+            (unsigned long long)starts[i], i, i, i, i, i, i);
   }
   o += "}\n";
   return o;
@@ -3110,8 +3156,19 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   const uint64_t gx = (k.NP + 256ull * XI - 1) / (256ull * XI);
   const uint64_t total = gx * (uint64_t)k.n_outer;
   if (total >= (1ull << 31)) return PGM_OK;
-  const bool xcd = xcd_knob && total % 8 == 0;
-  const std::string src = pm_source(k, reduce, XI, C != nullptr, (unsigned)gx, total, xcd, nt != 0, unroll);
+  PMSpec sp;
+  sp.k = k;
+  sp.red = reduce;
+  sp.XI = XI;
+  sp.unroll = unroll;
+  sp.store = C != nullptr;
+  sp.xcd = xcd_knob && total % 8 == 0;
+  sp.nt = nt != 0;
+  sp.gx = (unsigned)gx;
+  sp.total = total;
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source({sp}, starts, &blocks);
   if (src_out) {
     *src_out = src;
     return PGM_OK;
@@ -3121,10 +3178,11 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   PMBound *b = new (std::nothrow) PMBound;
   if (!b) return fail(PGM_ENOMEM, "product_n_marginal_bind: out of host memory");
   b->fn = fn;
-  b->blocks = (unsigned)total;
-  for (int t = 0; t < MOPS; ++t) b->ops[t] = k.ops[t];
-  b->C = C;
-  b->M = M;
+  b->blocks = (unsigned)blocks;
+  b->specs.push_back(sp);
+  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(k.ops[t]);
+  b->ptrs.push_back(C);
+  b->ptrs.push_back(M);
   *bound = b;
   return PGM_OK;
 }
@@ -3154,16 +3212,39 @@ int pgm_pm_bound_run(void *bound, void *stream) {
   STALE_PROBE();
   PMBound *b = (PMBound *)bound;
   if (!b) return fail(PGM_EINVAL, "pm_bound_run: null bound");
-  struct {
-    const double *o[MOPS];
-    double *C, *M;
-  } args;
-  for (int t = 0; t < MOPS; ++t) args.o[t] = b->ops[t];
-  args.C = b->C;
-  args.M = b->M;
-  size_t sz = sizeof args;
-  void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  size_t sz = b->ptrs.size() * sizeof(void *);
+  void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)b->ptrs.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
   HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(stream), nullptr, extra));
+  return PGM_OK;
+}
+
+int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
+  STALE_PROBE();
+  if (!bounds || !merged || n < 1 || n > 64) return fail(PGM_EINVAL, "pm_merge: 1..64 bound steps");
+  *merged = nullptr;
+  std::vector<PMSpec> specs;
+  std::vector<const double *> ptrs;
+  for (int i = 0; i < n; ++i) {
+    const PMBound *b = (const PMBound *)bounds[i];
+    if (!b) return fail(PGM_EINVAL, "pm_merge: null bound %d", i);
+    specs.insert(specs.end(), b->specs.begin(), b->specs.end());
+    ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
+  }
+  if (specs.size() > 64) return fail(PGM_EINVAL, "pm_merge: more than 64 bodies");
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source(specs, starts, &blocks);
+  if (blocks >= (1ull << 31)) return PGM_OK;  // too large for one grid: keep the separate launches
+  hipFunction_t fn = pm_compile(src);
+  if (!fn) return PGM_OK;
+  PMBound *m = new (std::nothrow) PMBound;
+  if (!m) return fail(PGM_ENOMEM, "pm_merge: out of host memory");
+  m->fn = fn;
+  m->blocks = (unsigned)blocks;
+  m->specs = specs;
+  m->ptrs = ptrs;
+  *merged = m;
   return PGM_OK;
 }
 

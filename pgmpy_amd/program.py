@@ -29,12 +29,13 @@ class _Rec:
     """One recorded launch of a levelled Program: plain launch, optional batch job, buffers it
     reads / writes (storage keys)."""
 
-    __slots__ = ("fn", "note", "job", "reads", "writes", "level")
+    __slots__ = ("fn", "note", "job", "reads", "writes", "level", "pm")
 
-    def __init__(self, fn, note, job, reads, writes):
+    def __init__(self, fn, note, job, reads, writes, pm=None):
         self.fn, self.note, self.job = fn, note, job
         self.reads, self.writes = reads, writes
         self.level = 0
+        self.pm = pm  # bound specialised product+marginal step (mergeable with its level's others)
 
 
 class _Batch:
@@ -62,6 +63,7 @@ class Program:
         self._batch = None
         self._handles = []
         self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
+        self.step_levels = []  # levelled Program: the dependency level of each lowered step
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
@@ -98,14 +100,14 @@ class Program:
         self.notes.append(f"batch of {len(b.jobs)}")
 
     # ------------------------------------------------------------------ levelled recording
-    def _emit(self, fn, note, reads, writes, job=None):
+    def _emit(self, fn, note, reads, writes, job=None, pm=None):
         """Append one launch (plain `fn(stream)`), or record it for levelling."""
         if self._levels:
             if self._lowered:
                 raise RuntimeError("levelled Program: no recording after the first run / capture")
             rk = [k for k in (_key(t) for t in reads if t is not None) if k]
             wk = [k for k in (_key(t) for t in writes if t is not None) if k]
-            self._recs.append(_Rec(fn, note, job, rk, wk))
+            self._recs.append(_Rec(fn, note, job, rk, wk, pm))
         else:
             self._steps.append(fn)
             self.notes.append(note)
@@ -132,13 +134,18 @@ class Program:
         by_level = [[] for _ in range(n_lv)]
         for r in self._recs:
             by_level[r.level].append(r)
-        for recs in by_level:
+        for lv, recs in enumerate(by_level):
             small = [r for r in recs if r.job is not None]
+            n0 = len(self._steps)
+            merged = self._merge_pm([r for r in recs if r.job is None and r.pm is not None])
             for r in recs:
+                if r in merged:
+                    continue
                 if r.job is None or len(small) == 1:
                     self._steps.append(r.fn)
                     self.notes.append(r.note)
             if len(small) < 2:
+                self.step_levels.extend([lv] * (len(self._steps) - n0))
                 continue
             L = N.lib()
             h = ctypes.c_void_p()
@@ -157,6 +164,29 @@ class Program:
             N.check(L.pgm_batch_finalize(h), "batch_finalize")
             self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
             self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
+            self.step_levels.extend([lv] * (len(self._steps) - n0))
+
+    def _merge_pm(self, recs):
+        """A level's specialised product+marginal steps as one launch per 64 (pgm_pm_merge); returns
+        the records merged (their launches are emitted here).  PGM_PM_MERGE=0 keeps them apart."""
+        if len(recs) < 2 or os.environ.get("PGM_PM_MERGE", "1") == "0":
+            return set()
+        L = N.lib()
+        done = set()
+        for i in range(0, len(recs), 64):
+            part = recs[i:i + 64]
+            if len(part) < 2:
+                continue
+            arr = (ctypes.c_void_p * len(part))(*[r.pm.value for r in part])
+            m = ctypes.c_void_p()
+            N.check(L.pgm_pm_merge(arr, len(part), ctypes.byref(m)), "pm_merge")
+            if not m.value:
+                continue
+            self._pm_bound.append(m)
+            self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
+            self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
+            done.update(part)
+        return done
 
     @property
     def n_levels(self):
@@ -221,8 +251,10 @@ class Program:
                 args = (ctypes.byref(d), ptrs, N.ptr(out2) if store else None, ms, E._REDUCE[reduce], N.ptr(M))
                 bound = ctypes.c_void_p()
                 N.check(L.pgm_product_n_marginal_bind(*args, ctypes.byref(bound)), "product_n_marginal_bind")
+                pm = None
                 if bound.value:  # the plan compiled into a specialised kernel
                     self._pm_bound.append(bound)
+                    pm = bound
                     fn = lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
                 else:
                     fn = lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal")
@@ -230,7 +262,7 @@ class Program:
                            f"product_n_marginal{'' if store else ' (marginal only)'} "
                            f"{[(list(ls), tuple(t.shape)) for t, ls in ops]} "
                            f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}",
-                           [t for t, _ in ops], [out2, M] if store else [M])
+                           [t for t, _ in ops], [out2, M] if store else [M], pm=pm)
                 return out2, M, store
         C = self.product_n(ops, out_labels, out, kinds)
         M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")

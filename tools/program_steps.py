@@ -43,8 +43,44 @@ def main():
         (prog, *_), = runner.plan._progs.values()
     res = prog.time_steps()
     tot = sum(us for us, _ in res)
-    print(f"{len(res)} steps, {tot / 1e3:.2f} ms summed")
-    for us, note in sorted(res, key=lambda r: -r[0])[:25]:
+    import torch
+
+    prog.run()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        prog.run()
+    b.record()
+    torch.cuda.synchronize()
+    stream_ms = a.elapsed_time(b) / 10
+    prog.capture()
+    prog.run()
+    torch.cuda.synchronize()
+    a.record(prog._stream)
+    for _ in range(10):
+        prog.run(prog._stream)
+    b.record(prog._stream)
+    torch.cuda.synchronize()
+    print(f"{len(res)} steps, {tot / 1e3:.2f} ms summed; whole program back to back: stream launches "
+          f"{stream_ms:.2f} ms, graph replay {a.elapsed_time(b) / 10:.2f} ms")
+    if prog._recs:
+        import collections
+
+        big, small = collections.Counter(), collections.Counter()
+        for r in prog._recs:
+            (big if r.job is None else small)[r.level] += 1
+        print("levels:", prog.n_levels, " unbatched launches per level:",
+              [big[lv] for lv in range(prog.n_levels)], " batched jobs per level:",
+              [small[lv] for lv in range(prog.n_levels)])
+    if os.environ.get("LEVELS") and prog._recs:
+        for lv in range(prog.n_levels):
+            mine = [res[i] for i, l in enumerate(prog.step_levels) if l == lv]
+            print(f"-- level {lv}: {len(mine)} launches, {sum(us for us, _ in mine):.1f} us")
+            for us, note in mine:
+                print(f"   {us:8.1f} us  {note[:150]}")
+    top = int(os.environ.get("TOP", "25"))
+    for us, note in sorted(res, key=lambda r: -r[0])[:top]:
         print(f"{us:9.1f} us  {note[:220] if len(sys.argv) < 4 else note}")
 
 
