@@ -153,6 +153,11 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
  * DiscreteFactor.product / marginalize pair of a batched calibration (ExactInference.py:784-802). */
 int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const *ops, double *C,
                                 const int64_t *marg_s, int32_t reduce, double *M, void **bound);
+/* pgm_product_n as a bound specialised step (no marginal; every dim kept), mergeable with the other
+ * bound steps of its level (pgm_pm_merge); *bound = NULL when the shape is not one the fused
+ * kernel handles (rows innermost, even, >= 64) or is too small. */
+int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, double *C, void **bound);
+
 /* The generated kernel source for the same arguments (no compile, no GPU): returns its length (0
  * when the generic kernel would run), copies at most len-1 bytes + NUL into buf.  Inspection and
  * host-side tests. */

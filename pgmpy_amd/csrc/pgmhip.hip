@@ -2591,6 +2591,7 @@ struct PMSpec {  // one fused step's specialisation
   ProdMK k;
   int red = PGM_RED_SUM, XI = 1, unroll = 8;
   bool store = true, xcd = false, nt = false;
+  bool has_m = true;  // false: the product alone (pgm_product_n_bind), no marginal
   unsigned gx = 1;
   uint64_t total = 0;  // blocks
 };
@@ -2614,7 +2615,7 @@ static int pm_knob(const char *name, int dflt) {
 static std::string pm_body(const PMSpec &sp, const std::string &name) {
   const ProdMK &k = sp.k;
   const int red = sp.red, XI = sp.XI, unroll = sp.unroll;
-  const bool store = sp.store, xcd = sp.xcd, nt = sp.nt;
+  const bool store = sp.store, xcd = sp.xcd, nt = sp.nt, has_m = sp.has_m;
   const unsigned gx = sp.gx;
   const uint64_t total = sp.total;
   std::string o;
@@ -2659,7 +2660,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     }
   }
   const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
-  for (int u = 0; u < XI; ++u) appendf(o, "  pgm_d2 a%d = {%s, %s};\n", u, init, init);
+  for (int u = 0; u < XI && has_m; ++u) appendf(o, "  pgm_d2 a%d = {%s, %s};\n", u, init, init);
   // reduced dims as nested loops (dim 0 outermost: the generic kernel's entry order); the innermost
   // dims whose trip product stays within `unroll` are unrolled
   int first_unrolled = k.nr;
@@ -2729,7 +2730,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
         appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
     }
   }
-  for (int u = 0; u < XI; ++u) {
+  for (int u = 0; u < XI && has_m; ++u) {
     if (red == PGM_RED_MAX)
       appendf(o, "%sa%d.x = pgm_maxn(a%d.x, w%d.x); a%d.y = pgm_maxn(a%d.y, w%d.y);\n", ind.c_str(), u, u, u, u,
               u, u);
@@ -2740,7 +2741,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     ind.resize(ind.size() - 2);
     appendf(o, "%s}\n", ind.c_str());
   }
-  for (int u = 0; u < XI; ++u) {
+  for (int u = 0; u < XI && has_m; ++u) {
     const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
     appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
   }
@@ -3126,7 +3127,7 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
 }
 
 static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double *C, const int64_t *marg_s,
-                   int32_t reduce, double *M, void **bound, std::string *src_out) {
+                   int32_t reduce, double *M, void **bound, std::string *src_out, bool has_m = true) {
   *bound = nullptr;
   if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
     return fail(PGM_EINVAL, "product_n_marginal: reduce must be PGM_RED_SUM or PGM_RED_MAX");
@@ -3162,6 +3163,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.XI = XI;
   sp.unroll = unroll;
   sp.store = C != nullptr;
+  sp.has_m = has_m;
   sp.xcd = xcd_knob && total % 8 == 0;
   sp.nt = nt != 0;
   sp.gx = (unsigned)gx;
@@ -3192,6 +3194,21 @@ int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const 
   STALE_PROBE();
   if (!bound) return fail(PGM_EINVAL, "product_n_marginal_bind: null bound");
   return pm_bind(d, ops, C, marg_s, reduce, M, bound, nullptr);
+}
+
+int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, double *C, void **bound) {
+  STALE_PROBE();
+  if (!bound || !d || !C) return fail(PGM_EINVAL, "product_n_bind: null argument");
+  *bound = nullptr;
+  if (d->n_keep < 1 || d->n_keep > PGM_MAX_DIMS) return fail(PGM_EINVAL, "product_n_bind: n_keep out of range");
+  // the product as a fused step whose every dim is kept (no reduced entries) and no marginal stored
+  int64_t ms[PGM_MAX_DIMS];
+  for (int i = 0; i < d->n_keep; ++i) ms[i] = d->keep_sc[i] ? d->keep_sc[i] : 1;
+  ProdMK k;
+  dim3 g;
+  const int r = plan_product_marg(d, ops, C, ms, C, k, g);
+  if (r <= 0) return r < 0 ? r : PGM_OK;  // shape not handled: *bound NULL, the generic kernel runs
+  return pm_bind(d, ops, C, ms, PGM_RED_SUM, C, bound, nullptr, false);
 }
 
 int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,

@@ -346,7 +346,7 @@ def product_n(operands, out_labels, out=None, kinds=None):
     return out
 
 
-def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None, store=True):
+def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kinds=None, store=True, M=None):
     """(descriptor, operand pointers, C, marginal strides, M, fused?) for C = product_n(...) and
     M[marg_labels] = reduce of C over the other labels (pgm_product_n_marginal); marg_labels must
     be a subset of out_labels.  fused is False when the fused kernel does not apply.  store=False:
@@ -355,7 +355,8 @@ def prepare_product_n_marginal(operands, out_labels, marg_labels, out=None, kind
     out_labels, marg_labels = list(out_labels), list(marg_labels)
     if any(l not in out_labels for l in marg_labels):
         raise ValueError("marginal labels must be output labels")
-    M = empty([int(out.shape[out_labels.index(l)]) for l in marg_labels])
+    if M is None:
+        M = empty([int(out.shape[out_labels.index(l)]) for l in marg_labels])
     ms = (ctypes.c_int64 * len(out_labels))(*[int(M.stride(marg_labels.index(l))) if l in marg_labels else 0
                                                for l in out_labels])
     ok = bool(N.lib().pgm_product_n_marginal_ok(ctypes.byref(d), ptrs, N.ptr(out) if store else None, ms, N.ptr(M)))

@@ -204,9 +204,13 @@ class Program:
             job = None
             if w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
                 job = ("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)))
-            self._emit(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"),
-                       f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}",
-                       [A, B], [out, ws], job)
+            fn, pm = (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), None
+            if job is None and B is None and combine == "copy" and reduce in ("sum", "max"):
+                pm = self._bind_marginal(A, la, out_labels, out, reduce)
+                if pm is not None:
+                    fn = lambda s, b=pm: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
+            self._emit(fn, f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}",
+                       [A, B], [out, ws], job, pm=pm)
             return out
         w = _work(d) if self._batch is not None else 0
         if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
@@ -217,6 +221,26 @@ class Program:
         self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
         self.notes.append(f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}")
         return out
+
+    def _bind_marginal(self, A, la, out_labels, out, reduce):
+        """out = reduce of A onto out_labels as a specialised marginal-only step (one operand), or
+        None when the fused kernel does not take the shape (rows not innermost, too few blocks)."""
+        la, out_labels = list(la), list(out_labels)
+        if not out_labels or out_labels[-1] != la[-1] or any(l not in la for l in out_labels):
+            return None
+        d, ptrs, _, ms, _, ok = E.prepare_product_n_marginal([(A, la)], la, out_labels, out=A, store=False,
+                                                             M=out)
+        if not ok:
+            return None
+        L = N.lib()
+        bound = ctypes.c_void_p()
+        N.check(L.pgm_product_n_marginal_bind(ctypes.byref(d), ptrs, None, ms, E._REDUCE[reduce], N.ptr(out),
+                                              ctypes.byref(bound)), "product_n_marginal_bind")
+        if not bound.value:
+            return None
+        self._keep.extend([d, ptrs, ms])
+        self._pm_bound.append(bound)
+        return bound
 
     def product_n(self, operands, out_labels, out=None, kinds=None):
         ops = list(operands)
@@ -231,9 +255,15 @@ class Program:
         self._keep.extend([d, ptrs, out] + [t for t, _ in ops])
         args = (ctypes.byref(d), ptrs, N.ptr(out))
         job = ("product_n", args) if out.numel() <= PRODN_BATCH_MAX else None
-        self._emit(lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n"),
-                   f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
-                   f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job)
+        fn, pm = (lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n")), None
+        if job is None and self._levels and len(ops) <= 4:  # a specialised step, merged with its level's
+            bound = ctypes.c_void_p()
+            N.check(L.pgm_product_n_bind(*args, ctypes.byref(bound)), "product_n_bind")
+            if bound.value:
+                self._pm_bound.append(bound)
+                fn, pm = (lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), bound
+        self._emit(fn, f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
+                       f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job, pm=pm)
         return out
 
     def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum",

@@ -714,3 +714,49 @@ def test_specialised_kernel_disk_cache(gpu, tmp_path):
     assert a["bound"] > 0 and a["files"] >= a["bound"] // 2, a  # shapes may repeat across steps
     assert b["bound"] == a["bound"] and b["files"] == a["files"], (a, b)
     assert b["checksum"] == a["checksum"]
+
+
+@pytest.mark.parametrize("rows", [1000, 2100])
+def test_product_n_bound_matches_generic(gpu, rows):
+    """pgm_product_n_bind (the n-ary product as a specialised step, no marginal) and the same step
+    merged with a marginal-only step (pgm_pm_merge) give the generic kernels' outputs exactly."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    L = NN.lib()
+    rng = np.random.default_rng(rows + 1)
+    cl = list("abcdef")
+    card = dict(zip(cl, (8, 2, 3, 8, 5, 9)))
+    R = E.ROW
+    psi = E.to_device(rng.random([card[v] for v in cl]))
+    msg = E.to_device(rng.random([card["a"], card["c"], card["f"], rows]))
+    sig = E.to_device(rng.random([card["a"], card["d"], card["f"], rows]))
+    ops = [(psi, cl), (msg, ["a", "c", "f", R]), (sig, ["a", "d", "f", R])]
+    d0, p0, C0 = E.prepare_product_n(ops, cl + [R])
+    NN.check(L.pgm_product_n(ctypes.byref(d0), p0, NN.ptr(C0), NN.stream_handle()), "product_n")
+    d1, p1, C1 = E.prepare_product_n(ops, cl + [R])
+    b = ctypes.c_void_p()
+    NN.check(L.pgm_product_n_bind(ctypes.byref(d1), p1, NN.ptr(C1), ctypes.byref(b)), "bind")
+    assert b.value
+    # a marginal-only step of another product, merged with the product into one launch
+    d2, p2, C2, ms2, M2, ok = E.prepare_product_n_marginal(ops[:2], cl + [R], ["a", "d", "f", R], store=False)
+    assert ok
+    b2 = ctypes.c_void_p()
+    NN.check(L.pgm_product_n_marginal_bind(ctypes.byref(d2), p2, None, ms2, E._REDUCE["sum"], NN.ptr(M2),
+                                           ctypes.byref(b2)), "bind2")
+    assert b2.value
+    arr = (ctypes.c_void_p * 2)(b.value, b2.value)
+    m = ctypes.c_void_p()
+    NN.check(L.pgm_pm_merge(arr, 2, ctypes.byref(m)), "merge")
+    assert m.value
+    NN.check(L.pgm_pm_bound_run(m, NN.stream_handle()), "run merged")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(E.to_host(C1), E.to_host(C0))
+    full = E.to_host(psi)[..., None] * E.to_host(msg)[:, None, :, None, None, :, :]
+    np.testing.assert_allclose(E.to_host(M2), full.sum(axis=(1, 2, 4)), rtol=1e-13)
+    for h in (b, b2, m):
+        L.pgm_pm_bound_destroy(h)
