@@ -163,6 +163,10 @@ int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, dou
  * host-side tests. */
 int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
                                   const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len);
+/* Compile (hipRTC, distinct sources on parallel threads, code-object disk cache) and load the kernels
+ * of bound / merged steps that are not loaded yet; a bound step not prepared compiles at its first
+ * run.  Call before graph capture. */
+int pgm_pm_prepare(void *const *bounds, int32_t n);
 int pgm_pm_bound_run(void *bound, void *stream);
 /* Several bound steps with no dependence between them (one level of a batched-BP sweep) as ONE
  * launch: a kernel whose block ranges run the steps' bodies.  *merged = NULL (PGM_OK) when the merge

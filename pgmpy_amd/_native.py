@@ -162,6 +162,7 @@ _SIGS = {
     "pgm_product_n_bind": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_pm_bound_run": ([_P, _P], ctypes.c_int),
     "pgm_pm_merge": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_pm_prepare": ([ctypes.POINTER(_P), ctypes.c_int32], ctypes.c_int),
     "pgm_pm_bound_destroy": ([_P], ctypes.c_int),
     "pgm_gemm": ([ctypes.POINTER(GemmDesc), _P, _P, _P, _P], ctypes.c_int),
     "pgm_batch_create": ([ctypes.POINTER(_P)], ctypes.c_int),

@@ -16,6 +16,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -24,6 +25,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <sys/stat.h>
@@ -2533,7 +2535,11 @@ static void rtc_cache_store(const std::string &path, const std::string &src, con
 static bool rtc_code(const std::string &src, const char *what, std::vector<char> &code) {
   const std::string path = rtc_cache_path(src);
   if (rtc_cache_load(path, src, code)) return true;
-  std::lock_guard<std::mutex> lk(g_rtc_mu);
+  // hipRTC programs compile concurrently from several threads (pgm_pm_prepare); PGM_RTC_SERIAL=1
+  // serialises every compile
+  static const bool serial = getenv("PGM_RTC_SERIAL") && atoi(getenv("PGM_RTC_SERIAL")) != 0;
+  std::unique_lock<std::mutex> lk(g_rtc_mu, std::defer_lock);
+  if (serial) lk.lock();
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return false;
   const char *opts[] = {"--offload-arch=gfx950", "-O3"};
@@ -2600,7 +2606,8 @@ struct PMSpec {  // one fused step's specialisation
 // body i runs on blocks [start_i, start_i + total_i), starts padded to multiples of 8 so each body's
 // XCD grouping holds)
 struct PMBound {
-  hipFunction_t fn = nullptr;
+  hipFunction_t fn = nullptr;  // compiled lazily: pgm_pm_prepare (in parallel) or the first run
+  std::string src;
   unsigned blocks = 0;
   std::vector<PMSpec> specs;
   std::vector<const double *> ptrs;  // 6 per body: o0..o3, C, M
@@ -2788,12 +2795,13 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
 static std::mutex g_pm_mu;
 static std::vector<std::pair<std::string, hipFunction_t>> g_pm_cache;  // source -> kernel (process lifetime)
 
-static hipFunction_t pm_compile(const std::string &src) {
-  std::lock_guard<std::mutex> lk(g_pm_mu);
+static hipFunction_t pm_cached(const std::string &src) {  // caller holds g_pm_mu
   for (auto &e : g_pm_cache)
     if (e.first == src) return e.second;
-  std::vector<char> code;
-  if (!rtc_code(src, "specialised product+marginal kernel", code)) return nullptr;
+  return nullptr;
+}
+
+static hipFunction_t pm_load(const std::string &src, const std::vector<char> &code) {  // caller holds g_pm_mu
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
   if (hipModuleLoadData(&mod, code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "pgm_pm") != hipSuccess) {
@@ -2802,6 +2810,54 @@ static hipFunction_t pm_compile(const std::string &src) {
   }
   g_pm_cache.emplace_back(src, fn);
   return fn;
+}
+
+static hipFunction_t pm_compile(const std::string &src) {
+  std::lock_guard<std::mutex> lk(g_pm_mu);
+  if (hipFunction_t f = pm_cached(src)) return f;
+  std::vector<char> code;
+  if (!rtc_code(src, "specialised product+marginal kernel", code)) return nullptr;
+  return pm_load(src, code);
+}
+
+// compile every bound step's kernel that is not loaded yet: distinct sources on up to
+// PGM_RTC_THREADS (default 16) threads, then load the modules
+static int pm_prepare(PMBound *const *bs, int n) {
+  std::vector<std::string> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_pm_mu);
+    for (int i = 0; i < n; ++i) {
+      if (!bs[i] || bs[i]->fn) continue;
+      if (hipFunction_t f = pm_cached(bs[i]->src)) {
+        bs[i]->fn = f;
+        continue;
+      }
+      if (std::find(todo.begin(), todo.end(), bs[i]->src) == todo.end()) todo.push_back(bs[i]->src);
+    }
+  }
+  if (!todo.empty()) {
+    std::vector<std::vector<char>> codes(todo.size());
+    std::vector<char> ok(todo.size(), 0);
+    const char *te = getenv("PGM_RTC_THREADS");
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(todo.size(), te ? (size_t)atoi(te) : 16));
+    std::atomic<size_t> next(0);
+    auto work = [&] {
+      for (size_t i; (i = next.fetch_add(1)) < todo.size();)
+        ok[i] = rtc_code(todo[i], "specialised product+marginal kernel", codes[i]) ? 1 : 0;
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    std::lock_guard<std::mutex> lk(g_pm_mu);
+    for (size_t i = 0; i < todo.size(); ++i) {
+      if (!ok[i] || (!pm_cached(todo[i]) && !pm_load(todo[i], codes[i])))
+        return fail(PGM_EDEVICE, "specialised product+marginal kernel: compile / load failed");
+    }
+    for (int i = 0; i < n; ++i)
+      if (bs[i] && !bs[i]->fn) bs[i]->fn = pm_cached(bs[i]->src);
+  }
+  return PGM_OK;
 }
 
 // ============================================================================= C-ABI
@@ -3175,11 +3231,9 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
     *src_out = src;
     return PGM_OK;
   }
-  hipFunction_t fn = pm_compile(src);
-  if (!fn) return PGM_OK;
   PMBound *b = new (std::nothrow) PMBound;
   if (!b) return fail(PGM_ENOMEM, "product_n_marginal_bind: out of host memory");
-  b->fn = fn;
+  b->src = src;
   b->blocks = (unsigned)blocks;
   b->specs.push_back(sp);
   for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(k.ops[t]);
@@ -3229,6 +3283,10 @@ int pgm_pm_bound_run(void *bound, void *stream) {
   STALE_PROBE();
   PMBound *b = (PMBound *)bound;
   if (!b) return fail(PGM_EINVAL, "pm_bound_run: null bound");
+  if (!b->fn) {
+    const int r = pm_prepare(&b, 1);
+    if (r != PGM_OK) return r;
+  }
   size_t sz = b->ptrs.size() * sizeof(void *);
   void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)b->ptrs.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
@@ -3253,16 +3311,20 @@ int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
   uint64_t blocks = 0;
   const std::string src = pm_source(specs, starts, &blocks);
   if (blocks >= (1ull << 31)) return PGM_OK;  // too large for one grid: keep the separate launches
-  hipFunction_t fn = pm_compile(src);
-  if (!fn) return PGM_OK;
   PMBound *m = new (std::nothrow) PMBound;
   if (!m) return fail(PGM_ENOMEM, "pm_merge: out of host memory");
-  m->fn = fn;
+  m->src = src;
   m->blocks = (unsigned)blocks;
   m->specs = specs;
   m->ptrs = ptrs;
   *merged = m;
   return PGM_OK;
+}
+
+int pgm_pm_prepare(void *const *bounds, int32_t n) {
+  STALE_PROBE();
+  if (!bounds || n < 0) return fail(PGM_EINVAL, "pm_prepare: null bounds");
+  return pm_prepare((PMBound *const *)bounds, n);
 }
 
 int pgm_pm_bound_destroy(void *bound) {

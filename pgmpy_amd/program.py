@@ -18,6 +18,10 @@ BATCH_SPLIT_WORK = 1 << 16  # a step the planner would split (few outputs, long 
 # outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
 # their own row-mode launch (16-B two-rows-per-lane).  Tuning knob: PGM_PRODN_BATCH_MAX.
 PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
+# levelled programs: n-ary products / separator marginals at least this large (entries) become
+# specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
+# take or that are below the engine's own threshold, PGM_PM_JIT_MIN)
+PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 18))  # C4 1,000 rows: 745K -> 856K
 
 
 def _key(t):
@@ -64,6 +68,7 @@ class Program:
         self._handles = []
         self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
+        self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
@@ -112,11 +117,23 @@ class Program:
             self._steps.append(fn)
             self.notes.append(note)
 
+    def _ready(self):
+        """Lower, then compile every specialised kernel the steps launch (in parallel, before any
+        run or capture)."""
+        self._lower()
+        if self._pm_launch is None:
+            self._pm_launch = list(self._pm_bound)  # plain Program: every bound step is launched
+        if self._pm_launch:
+            arr = (ctypes.c_void_p * len(self._pm_launch))(*[h.value for h in self._pm_launch])
+            N.check(N.lib().pgm_pm_prepare(arr, len(self._pm_launch)), "pm_prepare")
+            self._pm_launch = []
+
     def _lower(self):
         """Levelled Program -> steps: per level, its unbatched launches then one batch launch."""
         if not self._levels or self._lowered:
             return
         self._lowered = True
+        self._pm_launch = []
         last_w, last_r = {}, {}
         n_lv = 0
         for r in self._recs:
@@ -144,6 +161,8 @@ class Program:
                 if r.job is None or len(small) == 1:
                     self._steps.append(r.fn)
                     self.notes.append(r.note)
+                    if r.pm is not None:
+                        self._pm_launch.append(r.pm)
             if len(small) < 2:
                 self.step_levels.extend([lv] * (len(self._steps) - n0))
                 continue
@@ -183,6 +202,7 @@ class Program:
             if not m.value:
                 continue
             self._pm_bound.append(m)
+            self._pm_launch.append(m)
             self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
             done.update(part)
@@ -205,10 +225,11 @@ class Program:
             if w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
                 job = ("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)))
             fn, pm = (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), None
-            if job is None and B is None and combine == "copy" and reduce in ("sum", "max"):
+            if (job is None or A.numel() >= PM_PREFER_MIN) and B is None and combine == "copy" and \
+                    reduce in ("sum", "max"):
                 pm = self._bind_marginal(A, la, out_labels, out, reduce)
                 if pm is not None:
-                    fn = lambda s, b=pm: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
+                    fn, job = (lambda s, b=pm: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), None
             self._emit(fn, f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}",
                        [A, B], [out, ws], job, pm=pm)
             return out
@@ -256,12 +277,13 @@ class Program:
         args = (ctypes.byref(d), ptrs, N.ptr(out))
         job = ("product_n", args) if out.numel() <= PRODN_BATCH_MAX else None
         fn, pm = (lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n")), None
-        if job is None and self._levels and len(ops) <= 4:  # a specialised step, merged with its level's
+        if (job is None or out.numel() >= PM_PREFER_MIN) and self._levels and len(ops) <= 4:
+            # a specialised step, merged with its level's
             bound = ctypes.c_void_p()
             N.check(L.pgm_product_n_bind(*args, ctypes.byref(bound)), "product_n_bind")
             if bound.value:
                 self._pm_bound.append(bound)
-                fn, pm = (lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), bound
+                fn, pm, job = (lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), bound, None
         self._emit(fn, f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
                        f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job, pm=pm)
         return out
@@ -354,7 +376,7 @@ class Program:
         """[(us, note)] per recorded step, each replayed alone (profiling aid; not graph-replayed)."""
         import ctypes as C
 
-        self._lower()
+        self._ready()
         L = N.lib()
         s = N.stream_handle()
         a, b = C.c_void_p(), C.c_void_p()
@@ -376,7 +398,7 @@ class Program:
 
     # ------------------------------------------------------------------ execution
     def run(self, stream=None):
-        self._lower()
+        self._ready()
         s = N.stream_handle(stream)
         if self._graph is not None:
             N.check(N.lib().pgm_graph_launch(self._graph, s), "graph_launch")
@@ -391,7 +413,7 @@ class Program:
 
         if self._graph is not None:
             return
-        self._lower()
+        self._ready()
         L = N.lib()
         self._stream = torch.cuda.Stream()
         torch.cuda.current_stream().synchronize()

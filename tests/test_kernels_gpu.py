@@ -711,7 +711,7 @@ def test_specialised_kernel_disk_cache(gpu, tmp_path):
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     a, b = runs
-    assert a["bound"] > 0 and a["files"] >= a["bound"] // 2, a  # shapes may repeat across steps
+    assert a["bound"] > 0 and a["files"] > 0, a  # merged steps compile as one kernel per level
     assert b["bound"] == a["bound"] and b["files"] == a["files"], (a, b)
     assert b["checksum"] == a["checksum"]
 
