@@ -27,6 +27,22 @@ __global__ void k_store(double *out, int64_t n, int64_t ld) {
   }
 }
 
+// write-through stores (relaxed agent-scope atomic store = global_store ... sc1), as the specialised
+// row kernel's default output form
+template <int NCOL, int RPL>
+__global__ void k_store_wt(double *out, int64_t n, int64_t ld) {
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    int64_t r = ((int64_t)blockIdx.x * RPL + k) * blockDim.x + threadIdx.x;
+    if (r < n) {
+#pragma unroll
+      for (int c = 0; c < NCOL; ++c)
+        __hip_atomic_store((__attribute__((address_space(1))) double *)(out + c * ld + r), (double)c,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int NCOL, int RPL>
 __global__ void k_store_plain(double *out, int64_t n, int64_t ld) {
 #pragma unroll
@@ -160,6 +176,8 @@ int main(int argc, char **argv) {
   timeit("empty 1x64", [&] { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, 0, nullptr); }, reps, 0);
   timeit("store nt wg64", [&] { hipLaunchKernelGGL((k_store<17, 1>), dim3(g64), dim3(64), 0, 0, out, n, n); }, reps, sb);
   timeit("store plain wg64", [&] { hipLaunchKernelGGL((k_store_plain<17, 1>), dim3(g64), dim3(64), 0, 0, out, n, n); }, reps, sb);
+  timeit("store wt wg256", [&] { hipLaunchKernelGGL((k_store_wt<17, 1>), dim3((n + 255) / 256), dim3(256), 0, 0, out, n, n); }, reps, sb);
+  timeit("store wt wg128", [&] { hipLaunchKernelGGL((k_store_wt<17, 1>), dim3((n + 127) / 128), dim3(128), 0, 0, out, n, n); }, reps, sb);
   timeit("store nt wg256", [&] { hipLaunchKernelGGL((k_store<17, 1>), dim3((n + 255) / 256), dim3(256), 0, 0, out, n, n); }, reps, sb);
   timeit("store plain wg256", [&] { hipLaunchKernelGGL((k_store_plain<17, 1>), dim3((n + 255) / 256), dim3(256), 0, 0, out, n, n); }, reps, sb);
   timeit("store nt wg256 rpl2", [&] { hipLaunchKernelGGL((k_store<17, 2>), dim3((n + 511) / 512), dim3(256), 0, 0, out, n, n); }, reps, sb);
