@@ -158,6 +158,15 @@ int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const 
  * kernel handles (rows innermost, even, >= 64) or is too small. */
 int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, double *C, void **bound);
 
+/* Two marginals of the same product in ONE pass (nothing else stored), as a bound specialised step
+ * (mergeable): M1 over the keep dims with marg_s1 != 0, M2 likewise with marg_s2 (rows last, stride 1
+ * in both).  A batched-BP parent's sigma' onto two child scopes from its operands
+ * (ExactInference.py:784-797: each sigma is a marginalize of the same belief).  *bound = NULL when
+ * the shapes are outside the pass's limits (<= 32 accumulators, <= 512 unrolled states); then run two
+ * marginal passes. */
+int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const *ops, const int64_t *marg_s1,
+                                 double *M1, const int64_t *marg_s2, double *M2, int32_t reduce, void **bound);
+
 /* The generated kernel source for the same arguments (no compile, no GPU): returns its length (0
  * when the generic kernel would run), copies at most len-1 bytes + NUL into buf.  Inspection and
  * host-side tests. */
@@ -167,6 +176,8 @@ int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *cons
  * of bound / merged steps that are not loaded yet; a bound step not prepared compiles at its first
  * run.  Call before graph capture. */
 int pgm_pm_prepare(void *const *bounds, int32_t n);
+/* The generated source of a bound / merged step (its length; at most len-1 bytes + NUL copied). */
+int pgm_pm_bound_source(void *bound, char *buf, size_t len);
 int pgm_pm_bound_run(void *bound, void *stream);
 /* Several bound steps with no dependence between them (one level of a batched-BP sweep) as ONE
  * launch: a kernel whose block ranges run the steps' bodies.  *merged = NULL (PGM_OK) when the merge

@@ -159,10 +159,14 @@ _SIGS = {
     "pgm_product_n_marginal_source": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P,
                                        ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, _P, ctypes.c_char_p,
                                        ctypes.c_size_t], ctypes.c_int),
+    "pgm_product_n_marginals_bind": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P),
+                                      ctypes.POINTER(ctypes.c_int64), _P, ctypes.POINTER(ctypes.c_int64), _P,
+                                      ctypes.c_int32, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_product_n_bind": ([ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_pm_bound_run": ([_P, _P], ctypes.c_int),
     "pgm_pm_merge": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_pm_prepare": ([ctypes.POINTER(_P), ctypes.c_int32], ctypes.c_int),
+    "pgm_pm_bound_source": ([_P, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
     "pgm_pm_bound_destroy": ([_P], ctypes.c_int),
     "pgm_gemm": ([ctypes.POINTER(GemmDesc), _P, _P, _P, _P], ctypes.c_int),
     "pgm_batch_create": ([ctypes.POINTER(_P)], ctypes.c_int),

@@ -2593,7 +2593,25 @@ static bool rows_jit_ready(RowsHandle *h) {
 // that lack the row axis read at wave-uniform addresses (scalar loads), one 1-D grid with an optional
 // XCD-grouped block order.  Compiled once per shape (hipRTC, cached by source), bound to its
 // pointers, launched by pgm_pm_bound_run (capturable in a HIP graph).
+// two marginals of one product in a single pass (no product stored): block = one state of the dims
+// both keep (K) x a row chunk; the dims only one of them keeps (U = R1 + R2) are unrolled at
+// generation time with one register accumulator per R1 / R2 state; dims neither keeps (Z) are runtime
+// inner loops.  Batched-BP distribute: a parent's sigma' for two child scopes from its operands.
+struct PMMulti {
+  int n_ops = 0;
+  int kind[MOPS] = {}, vec[MOPS] = {};
+  int nK = 0, nU = 0, nZ = 0;
+  unsigned kcard[KMAX] = {}, ucard[KMAX] = {}, zcard[KMAX] = {};
+  int64_t ks[MOPS][KMAX] = {}, k1[KMAX] = {}, k2[KMAX] = {};
+  int64_t us[MOPS][KMAX] = {}, u1[KMAX] = {}, u2[KMAX] = {};
+  int64_t zs[MOPS][KMAX] = {};
+  uint32_t n_outer = 0, NP = 0;
+  unsigned n1 = 1, n2 = 1;  // accumulators (R1 / R2 states)
+};
+
 struct PMSpec {  // one fused step's specialisation
+  int multi = 0;  // 1: PMMulti body (two marginals), else the ProdMK body
+  PMMulti mm;
   ProdMK k;
   int red = PGM_RED_SUM, XI = 1, unroll = 8;
   bool store = true, xcd = false, nt = false;
@@ -2756,6 +2774,143 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   return o;
 }
 
+static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
+  // the target with fewer states of its own dims (R_reg) keeps one register accumulator per state,
+  // its dims unrolled innermost; the other target's own dims (R_str) are runtime loops outermost, and
+  // its marginal is complete after each of their iterations (everything inside is summed), so it is
+  // stored there — registers stay bounded by the smaller target
+  const PMMulti &q = sp.mm;
+  const int red = sp.red;
+  const int treg = q.n1 <= q.n2 ? 0 : 1;  // 0: M1 (C slot) in registers, 1: M2 (M slot)
+  const int64_t *sreg = treg == 0 ? q.u1 : q.u2;
+  const int64_t *sstr = treg == 0 ? q.u2 : q.u1;
+  const char *preg = treg == 0 ? "C" : "M", *pstr = treg == 0 ? "M" : "C";
+  const char *mreg = treg == 0 ? "m1" : "m2", *mstr = treg == 0 ? "m2" : "m1";
+  const unsigned nreg = treg == 0 ? q.n1 : q.n2;
+  std::string o;
+  appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
+             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
+             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
+  o += "  (void)o1; (void)o2; (void)o3;\n";
+  if (sp.xcd) appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;\n", (unsigned long long)(sp.total / 8));
+  appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", sp.gx, sp.gx);
+  o += "  unsigned idx = ob;\n  long long m1 = 0, m2 = 0";
+  for (int i = 0; i < q.n_ops; ++i) appendf(o, ", f%d = 0", i);
+  o += ";\n  (void)idx;\n";
+  for (int d = q.nK - 1; d >= 0; --d) {
+    appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", q.kcard[d], q.kcard[d]);
+    if (q.k1[d]) appendf(o, " m1 += (long long)g * %lldLL;", (long long)q.k1[d]);
+    if (q.k2[d]) appendf(o, " m2 += (long long)g * %lldLL;", (long long)q.k2[d]);
+    for (int i = 0; i < q.n_ops; ++i)
+      if (q.ks[i][d]) appendf(o, " f%d += (long long)g * %lldLL;", i, (long long)q.ks[i][d]);
+    o += " }\n";
+  }
+  const bool tail = q.NP % 256u != 0;
+  o += "  const unsigned x = xb * 256u + threadIdx.x;\n";
+  if (tail) appendf(o, "  const unsigned c = x < %uu ? x : %uu;\n", q.NP, q.NP - 1);
+  else o += "  const unsigned c = x;\n";
+  const std::string guard = tail ? "if (x < " + std::to_string(q.NP) + "u) " : "";
+  const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
+  for (unsigned a = 0; a < nreg; ++a) appendf(o, "  pgm_d2 ar_%u = {%s, %s};\n", a, init, init);
+  // runtime loops: the streamed target's own dims (u), then the dims neither keeps (z)
+  std::string ind = "  ";
+  std::vector<int> ustr, ureg;
+  for (int d = 0; d < q.nU; ++d) (sstr[d] ? ustr : ureg).push_back(d);
+  for (int d : ustr) {
+    appendf(o, "%s#pragma unroll 1\n%sfor (int u%d = 0; u%d < %u; ++u%d) {\n", ind.c_str(), ind.c_str(), d, d,
+            q.ucard[d], d);
+    ind += "  ";
+  }
+  appendf(o, "%spgm_d2 as = {%s, %s};\n", ind.c_str(), init, init);
+  for (int z = 0; z < q.nZ; ++z) {
+    appendf(o, "%s#pragma unroll %s\n", ind.c_str(), z == q.nZ - 1 ? "2" : "1");
+    appendf(o, "%sfor (int z%d = 0; z%d < %u; ++z%d) {\n", ind.c_str(), z, z, q.zcard[z], z);
+    ind += "  ";
+  }
+  auto runtime_off = [&](const int64_t *zs, const int64_t (*us)[KMAX], int i) {
+    std::string e;
+    for (int z = 0; z < q.nZ; ++z)
+      if (zs[z]) e += " + (long long)z" + std::to_string(z) + " * " + std::to_string((long long)zs[z]) + "LL";
+    for (int d : ustr)
+      if (us[i][d]) e += " + (long long)u" + std::to_string(d) + " * " + std::to_string((long long)us[i][d]) + "LL";
+    return e;
+  };
+  uint64_t nr = 1;
+  for (int d : ureg) nr *= q.ucard[d];
+  for (uint64_t ra = 0; ra < nr; ++ra) {
+    unsigned dig[KMAX] = {};
+    uint64_t rem = ra;
+    for (int k = (int)ureg.size() - 1; k >= 0; --k) {
+      dig[ureg[k]] = (unsigned)(rem % q.ucard[ureg[k]]);
+      rem /= q.ucard[ureg[k]];
+    }
+    int64_t off[MOPS] = {};
+    for (int d : ureg)
+      for (int i = 0; i < q.n_ops; ++i) off[i] += (int64_t)dig[d] * q.us[i][d];
+    appendf(o, "%s{\n", ind.c_str());
+    for (int i = 0; i < q.n_ops; ++i) {
+      const std::string ro = runtime_off(q.zs[i], q.us, i);
+      if (q.vec[i])
+        appendf(o, "%s  const pgm_d2 v%d = ((const pgm_d2 *)(o%d + f%d + %lldLL%s))[c];\n", ind.c_str(), i, i, i,
+                (long long)off[i], ro.c_str());
+      else
+        appendf(o, "%s  const double s%d = o%d[f%d + %lldLL%s];\n", ind.c_str(), i, i, i, (long long)off[i],
+                ro.c_str());
+    }
+    for (int h = 0; h < 2; ++h) {
+      const char cx = h ? 'y' : 'x';
+      auto term = [&](int i) {
+        char buf[32];
+        if (q.vec[i]) snprintf(buf, sizeof buf, "v%d.%c", i, cx);
+        else snprintf(buf, sizeof buf, "s%d", i);
+        return std::string(buf);
+      };
+      std::string e = "1.0";
+      for (int i = 0; i < q.n_ops; ++i) {
+        if (q.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
+        else if (q.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
+          e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+      }
+      appendf(o, "%s  const double w%c = %s;\n", ind.c_str(), cx, e.c_str());
+    }
+    appendf(o, "%s  const pgm_d2 w = {wx, wy};\n", ind.c_str());
+    if (red == PGM_RED_MAX)
+      appendf(o, "%s  ar_%llu.x = pgm_maxn(ar_%llu.x, w.x); ar_%llu.y = pgm_maxn(ar_%llu.y, w.y); "
+                 "as.x = pgm_maxn(as.x, w.x); as.y = pgm_maxn(as.y, w.y);\n",
+              ind.c_str(), (unsigned long long)ra, (unsigned long long)ra, (unsigned long long)ra,
+              (unsigned long long)ra);
+    else
+      appendf(o, "%s  ar_%llu += w; as += w;\n", ind.c_str(), (unsigned long long)ra);
+    appendf(o, "%s}\n", ind.c_str());
+  }
+  for (int z = q.nZ - 1; z >= 0; --z) {
+    ind.resize(ind.size() - 2);
+    appendf(o, "%s}\n", ind.c_str());
+  }
+  {  // the streamed target's marginal for this iteration is complete
+    std::string e;
+    for (int d : ustr)
+      e += " + (long long)u" + std::to_string(d) + " * " + std::to_string((long long)sstr[d]) + "LL";
+    appendf(o, "%s%s((pgm_d2 *)(%s + %s%s))[x] = as;\n", ind.c_str(), guard.c_str(), pstr, mstr, e.c_str());
+  }
+  for (size_t k = 0; k < ustr.size(); ++k) {
+    ind.resize(ind.size() - 2);
+    appendf(o, "%s}\n", ind.c_str());
+  }
+  for (uint64_t ra = 0; ra < nr; ++ra) {  // register target: accumulator ra at its digits' offset
+    uint64_t rem = ra;
+    int64_t off = 0;
+    for (int k = (int)ureg.size() - 1; k >= 0; --k) {
+      off += (int64_t)(rem % q.ucard[ureg[k]]) * sreg[ureg[k]];
+      rem /= q.ucard[ureg[k]];
+    }
+    appendf(o, "  %s((pgm_d2 *)(%s + %s + %lldLL))[x] = ar_%llu;\n", guard.c_str(), preg, mreg, (long long)off,
+            (unsigned long long)ra);
+  }
+  o += "}\n";
+  return o;
+}
+
 // kernel pgm_pm over the bodies (kernel argument: 6 pointers per body); starts[i] = first block of
 // body i, returns the grid size through *blocks
 static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint64_t> &starts, uint64_t *blocks) {
@@ -2772,7 +2927,7 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
     at = (at + 7) / 8 * 8;
     starts[i] = at;
     at += specs[i].total;
-    o += pm_body(specs[i], "pm" + std::to_string(i));
+    o += specs[i].multi ? pm_multi_body(specs[i], "pm" + std::to_string(i)) : pm_body(specs[i], "pm" + std::to_string(i));
   }
   *blocks = at;
   appendf(o, "struct pgm_pm_args { const double *p[%zu][6]; };\n", n);
@@ -3265,6 +3420,103 @@ int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, dou
   return pm_bind(d, ops, C, ms, PGM_RED_SUM, C, bound, nullptr, false);
 }
 
+// plan of the two-marginal pass; 1 = supported (q filled), 0 = not (caller runs two passes)
+static int plan_two_marginals(const pgm_productn_desc *d, const double *const *ops, const int64_t *s1,
+                              const int64_t *s2, const double *M1, const double *M2, PMMulti &q) {
+  if (!d || !ops || !s1 || !s2 || !M1 || !M2) return fail(PGM_EINVAL, "product_n_marginals: null argument");
+  if (d->n_ops < 1 || d->n_ops > MOPS || d->n_keep < 2 || d->n_keep > PGM_MAX_DIMS) return 0;
+  const int last = d->n_keep - 1;
+  const int64_t NX = d->keep_card[last];
+  if (NX < 64 || NX % 2 || d->keep_sc[last] != 1 || s1[last] != 1 || s2[last] != 1) return 0;
+  if (((uintptr_t)M1 & 15) || ((uintptr_t)M2 & 15)) return 0;
+  q = PMMulti();
+  q.n_ops = d->n_ops;
+  for (int t = 0; t < d->n_ops; ++t) {
+    if (!ops[t] || d->op_kind[t] < 0 || d->op_kind[t] > 2) return fail(PGM_EINVAL, "product_n_marginals: operand %d", t);
+    const int64_t sx = d->keep_s[t][last];
+    if (sx != 0 && sx != 1) return 0;
+    if (sx == 1 && ((uintptr_t)ops[t] & 15)) return 0;
+    q.vec[t] = sx == 1;
+    q.kind[t] = d->op_kind[t];
+  }
+  uint64_t nk = 1, nu = 1;
+  for (int i = 0; i < last; ++i) {
+    const int64_t c = d->keep_card[i];
+    if (c <= 0) return fail(PGM_EINVAL, "product_n_marginals: keep_card[%d] <= 0", i);
+    if (c == 1) continue;
+    if ((s1[i] && s1[i] % 2) || (s2[i] && s2[i] % 2)) return 0;
+    for (int t = 0; t < d->n_ops; ++t)
+      if (q.vec[t] && d->keep_s[t][i] % 2) return 0;
+    if (s1[i] && s2[i]) {
+      if (q.nK >= KMAX) return 0;
+      q.kcard[q.nK] = (unsigned)c;
+      q.k1[q.nK] = s1[i];
+      q.k2[q.nK] = s2[i];
+      for (int t = 0; t < d->n_ops; ++t) q.ks[t][q.nK] = d->keep_s[t][i];
+      ++q.nK;
+      nk *= (uint64_t)c;
+    } else if (s1[i] || s2[i]) {
+      if (q.nU >= KMAX) return 0;
+      q.ucard[q.nU] = (unsigned)c;
+      q.u1[q.nU] = s1[i];
+      q.u2[q.nU] = s2[i];
+      for (int t = 0; t < d->n_ops; ++t) q.us[t][q.nU] = d->keep_s[t][i];
+      ++q.nU;
+      nu *= (uint64_t)c;
+      if (s1[i]) q.n1 *= (unsigned)c;
+      else q.n2 *= (unsigned)c;
+    } else {
+      if (q.nZ >= KMAX) return 0;
+      q.zcard[q.nZ] = (unsigned)c;
+      for (int t = 0; t < d->n_ops; ++t) q.zs[t][q.nZ] = d->keep_s[t][i];
+      ++q.nZ;
+    }
+  }
+  // register accumulators: the smaller target's own states, unrolled (knob PGM_PM2_MAX_ACC, default 16)
+  static const unsigned max_acc = getenv("PGM_PM2_MAX_ACC") ? (unsigned)atoi(getenv("PGM_PM2_MAX_ACC")) : 16u;
+  (void)nu;
+  if (std::min(q.n1, q.n2) > max_acc || nk >= (1ull << 31)) return 0;
+  q.n_outer = (uint32_t)nk;
+  q.NP = (uint32_t)(NX / 2);
+  const uint64_t gx = (q.NP + 255) / 256;
+  if (gx * nk < 256) return 0;  // fewer blocks than CUs: two single-marginal passes fill the chip better
+  return 1;
+}
+
+int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const *ops, const int64_t *marg_s1,
+                                 double *M1, const int64_t *marg_s2, double *M2, int32_t reduce, void **bound) {
+  STALE_PROBE();
+  if (!bound) return fail(PGM_EINVAL, "product_n_marginals_bind: null bound");
+  *bound = nullptr;
+  if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
+    return fail(PGM_EINVAL, "product_n_marginals: reduce must be PGM_RED_SUM or PGM_RED_MAX");
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr || pm_knob("PGM_PM_JIT", 1) == 0 ||
+                             pm_knob("PGM_PM2", 1) == 0;
+  if (no_jit) return PGM_OK;
+  PMSpec sp;
+  const int r = plan_two_marginals(d, ops, marg_s1, marg_s2, M1, M2, sp.mm);
+  if (r <= 0) return r;
+  sp.multi = 1;
+  sp.red = reduce;
+  sp.store = false;
+  sp.gx = (sp.mm.NP + 255) / 256;
+  sp.total = (uint64_t)sp.gx * sp.mm.n_outer;
+  sp.xcd = pm_knob("PGM_PM_XCD", 1) && sp.total % 8 == 0;
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source({sp}, starts, &blocks);
+  PMBound *b = new (std::nothrow) PMBound;
+  if (!b) return fail(PGM_ENOMEM, "product_n_marginals_bind: out of host memory");
+  b->src = src;
+  b->blocks = (unsigned)blocks;
+  b->specs.push_back(sp);
+  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(t < d->n_ops ? ops[t] : ops[0]);
+  b->ptrs.push_back(M1);  // the C slot
+  b->ptrs.push_back(M2);  // the M slot
+  *bound = b;
+  return PGM_OK;
+}
+
 int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
                                   const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len) {
   STALE_PROBE();
@@ -3319,6 +3571,16 @@ int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
   m->ptrs = ptrs;
   *merged = m;
   return PGM_OK;
+}
+
+int pgm_pm_bound_source(void *bound, char *buf, size_t len) {
+  STALE_PROBE();
+  const PMBound *b = (const PMBound *)bound;
+  if (!b || !buf || len == 0) return fail(PGM_EINVAL, "pm_bound_source: null argument");
+  const size_t n = std::min(len - 1, b->src.size());
+  memcpy(buf, b->src.data(), n);
+  buf[n] = 0;
+  return (int)b->src.size();
 }
 
 int pgm_pm_prepare(void *const *bounds, int32_t n) {

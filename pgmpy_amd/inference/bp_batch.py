@@ -177,7 +177,8 @@ class BPSchedule:
             if p in premarg:
                 sc0, m0 = premarg[p]
                 have[tuple(sc0)] = m0
-            for sc in sorted(scopes, key=lambda x: -scope_size(x)):
+            ordered = sorted(scopes, key=lambda x: -scope_size(x))
+            for si, sc in enumerate(ordered):
                 if sc in have:
                     sigma = have[sc]
                 else:
@@ -185,11 +186,21 @@ class BPSchedule:
                     sigma = None
                     if src == tuple(lp):  # not from the belief (a clique-sized read): from its operands,
                         fops, fk = final[p]  # marginal only (the fused kernel writes nothing but sigma')
-                        d_, p_, o_, ms_, M_, ok = E.prepare_product_n_marginal(fops, lp + [R], list(sc) + [R], tp,
-                                                                               fk, store=False)
-                        if ok:
-                            _, sigma, _ = prog.product_n_marginal(fops, lp + [R], list(sc) + [R], out=tp, kinds=fk,
-                                                                  reduce=red, store=False)
+                        # a second scope that would also come from the operands: both in one pass
+                        partner = next((s2 for s2 in ordered[si + 1:] if s2 not in have and not set(s2) <= set(sc)
+                                        and all(not set(s2) <= set(h) for h in have if h != tuple(lp))), None)
+                        two = None
+                        if partner is not None:
+                            two = prog.product_n_marginals(fops, lp + [R], list(sc) + [R], list(partner) + [R],
+                                                           out=tp, kinds=fk, reduce=red)
+                        if two is not None:
+                            sigma, have[partner] = two
+                        else:
+                            d_, p_, o_, ms_, M_, ok = E.prepare_product_n_marginal(fops, lp + [R], list(sc) + [R],
+                                                                                   tp, fk, store=False)
+                            if ok:
+                                _, sigma, _ = prog.product_n_marginal(fops, lp + [R], list(sc) + [R], out=tp,
+                                                                      kinds=fk, reduce=red, store=False)
                     if sigma is None:
                         sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
                                               combine="copy")

@@ -320,6 +320,35 @@ class Program:
         M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")
         return C, M, True
 
+    def product_n_marginals(self, operands, out_labels, marg1, marg2, out=None, kinds=None, reduce="sum"):
+        """(M1, M2): two marginals of the product of operands onto marg1 / marg2 in ONE specialised
+        pass that stores nothing else (pgm_product_n_marginals_bind), or None when the pass does not
+        take the shapes.  `out` (not written) only describes the product's index space."""
+        ops = list(operands)
+        if len(ops) > 4 or not self._levels:
+            return None
+        L = N.lib()
+        d, ptrs, C = E.prepare_product_n(ops, out_labels, out, kinds)
+        shape = {l: int(C.shape[i]) for i, l in enumerate(out_labels)}
+        Ms, strides = [], []
+        for marg in (marg1, marg2):
+            M = E.empty([shape[l] for l in marg])
+            Ms.append(M)
+            strides.append((ctypes.c_int64 * len(out_labels))(*[int(M.stride(list(marg).index(l))) if l in marg else 0
+                                                                 for l in out_labels]))
+        bound = ctypes.c_void_p()
+        N.check(L.pgm_product_n_marginals_bind(ctypes.byref(d), ptrs, strides[0], N.ptr(Ms[0]), strides[1],
+                                               N.ptr(Ms[1]), E._REDUCE[reduce], ctypes.byref(bound)),
+                "product_n_marginals_bind")
+        if not bound.value:
+            return None
+        self._keep.extend([d, ptrs, C] + strides + Ms + [t for t, _ in ops])
+        self._pm_bound.append(bound)
+        self._emit(lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"),
+                   f"product_n_marginals {[(list(ls), tuple(t.shape)) for t, ls in ops]} -> {list(marg1)} + "
+                   f"{list(marg2)}", [t for t, _ in ops], Ms, pm=bound)
+        return Ms[0], Ms[1]
+
     def indicator(self, codes_col, card, n_rows, err=None):
         out = E.empty([card, n_rows])
         L = N.lib()

@@ -760,3 +760,55 @@ def test_product_n_bound_matches_generic(gpu, rows):
     np.testing.assert_allclose(E.to_host(M2), full.sum(axis=(1, 2, 4)), rtol=1e-13)
     for h in (b, b2, m):
         L.pgm_pm_bound_destroy(h)
+
+
+@pytest.mark.parametrize("rows,red,ratio", [(1000, "sum", False), (2100, "max", False), (1000, "sum", True)])
+def test_two_marginals_one_pass(gpu, rows, red, ratio):
+    """pgm_product_n_marginals_bind: two marginals of one product (dims kept by both, by one only,
+    by neither) in one specialised pass equal numpy's sums / maxima of the full product, including a
+    sigma/mu ratio pair (0/0 -> 0) and a row tail."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    L = NN.lib()
+    rng = np.random.default_rng(rows + 7)
+    cl = list("abcdef")
+    card = dict(zip(cl, (4, 2, 3, 2, 5, 33)))  # 165 states kept by both marginals: enough blocks
+    R = E.ROW
+    psi = rng.random([card[v] for v in cl])
+    A = rng.random([card["a"], card["b"], card["f"], rows])
+    B = rng.random([card["c"], card["d"], card["f"], rows])
+    ops = [(E.to_device(psi), cl), (E.to_device(A), ["a", "b", "f", R]), (E.to_device(B), ["c", "d", "f", R])]
+    full = psi[..., None] * A[:, :, None, None, None, :, :] * B[None, None, :, :, None, :, :]
+    kinds = None
+    if ratio:
+        mu = rng.random([card["a"], card["b"], card["f"], rows])
+        A[0, 0, 0, :3] = 0.0
+        mu[0, 0, 0, :3] = 0.0
+        ops = [ops[0], (E.to_device(A), ["a", "b", "f", R]), (E.to_device(mu), ["a", "b", "f", R]), ops[2]]
+        kinds = [NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN, NN.PRODN_MUL]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            q = A / mu
+        q[np.isnan(q)] = 0.0
+        full = psi[..., None] * q[:, :, None, None, None, :, :] * B[None, None, :, :, None, :, :]
+    m1, m2 = ["a", "b", "e", "f", R], ["c", "d", "e", "f", R]  # e, f: by both; a,b / c,d: by one each
+    d, ptrs, C = E.prepare_product_n(ops, cl + [R], None, kinds)
+    Ms, st = [], []
+    for mg in (m1, m2):
+        M = E.empty([int(C.shape[(cl + [R]).index(l)]) for l in mg])
+        Ms.append(M)
+        st.append((ctypes.c_int64 * 7)(*[int(M.stride(mg.index(l))) if l in mg else 0 for l in cl + [R]]))
+    b = ctypes.c_void_p()
+    NN.check(L.pgm_product_n_marginals_bind(ctypes.byref(d), ptrs, st[0], NN.ptr(Ms[0]), st[1], NN.ptr(Ms[1]),
+                                            E._REDUCE[red], ctypes.byref(b)), "bind")
+    assert b.value
+    NN.check(L.pgm_pm_bound_run(b, NN.stream_handle()), "run")
+    torch.cuda.synchronize()
+    L.pgm_pm_bound_destroy(b)
+    f = np.sum if red == "sum" else np.max
+    np.testing.assert_allclose(E.to_host(Ms[0]), f(full, axis=(2, 3)), rtol=1e-13)
+    np.testing.assert_allclose(E.to_host(Ms[1]), f(full, axis=(0, 1)), rtol=1e-13)
