@@ -1,7 +1,9 @@
-// pgm_internal.h — private interface between pgmhip.hip (kernels, C-ABI) and pgmdq.cpp (direct AQL
-// dispatch).  Not part of the C-ABI of include/pgmhip.h.
+// pgm_internal.h — private interface between pgmhip.hip (kernels, C-ABI), pgmdq.cpp (direct AQL
+// dispatch) and pgmpm.cpp (plan-specialised batched-BP steps).  Not part of the C-ABI of
+// include/pgmhip.h.
 #pragma once
 #include <cstddef>
+#include <cstdint>
 
 extern "C" {
 
@@ -19,4 +21,44 @@ typedef struct {
 
 int pgmi_rows_bound_jit(void *bound, pgmi_jit_launch *out);
 int pgmi_fail(int code, const char *msg);  // set pgm_last_error, return code
+int pgmi_failf(int code, const char *fmt, ...);  // printf-style pgmi_fail
 }
+
+#ifdef __cplusplus
+#include <string>
+#include <vector>
+
+#include "pgmhip.h"
+
+#define KMAX 12  // dims of a contraction / fused-step index space (incl. the row dim)
+#define MOPS 4   // operands of a fused product + marginal step
+
+// n / d for n < 2^31 with one mul-hi and one shift (Granlund-Montgomery round-up method)
+struct FDiv {
+  uint32_t d, m, s;
+};
+
+// the fused product + marginal step's plan (pgmhip.hip plans it and runs the generic kernels;
+// pgmpm.cpp compiles it into specialised kernels)
+struct ProdMK {
+  int32_t n_ops, nk, nr, n_red;  // nk: kept outer dims + the row dim (last); nr: reduced dims
+  int32_t kind[MOPS];
+  int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
+  int32_t jvar[MOPS];            // operand varies over the reduced entries (else loaded once per outer)
+  uint32_t n_outer, NP;          // kept outer index space; row pairs
+  FDiv kdiv[KMAX];
+  int64_t ksc[KMAX], ksm[KMAX], ks[MOPS][KMAX];
+  FDiv rdiv[KMAX];
+  int64_t rsc[KMAX], rs[MOPS][KMAX];
+  const double *ops[MOPS];
+};
+
+struct dim3;
+int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops, const double *C,
+                           const int64_t *marg_s, const double *M, ProdMK &k, dim3 &grid);
+void pgmi_appendf(std::string &o, const char *fmt, ...);  // printf into a growing source string
+void pgmi_stale_probe(const char *fn);                   // PGM_STALE_PROBE=1 debugging aid
+// gfx950 code object of a generated kernel source: the on-disk cache, else hipRTC (then cached)
+bool pgmi_rtc_code(const std::string &src, const char *what, std::vector<char> &code);
+#define STALE_PROBE() pgmi_stale_probe(__func__)
+#endif

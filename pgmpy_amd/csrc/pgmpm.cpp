@@ -1,0 +1,823 @@
+// pgmpm.cpp — plan-specialised batched-BP steps (host code; the kernels it generates are compiled for
+// gfx950 with hipRTC at run time): the fused product + marginal, n-ary products, separator marginals
+// and two-marginal passes of a batched calibration (pgmpy ExactInference.py:770-805), merged per
+// dependency level into one launch, plus the on-disk code-object cache shared with the specialised
+// row kernels of pgmhip.hip.  C-ABI: include/pgmhip.h (pgm_product_n_marginal_bind, pgm_pm_*).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pgm_internal.h"
+#include "pgmhip.h"
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) {                                                                   \
+      (void)hipGetLastError();                                                                \
+      return pgmi_failf(e_ == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "%s: %s", #expr, \
+                        hipGetErrorString(e_));                                               \
+    }                                                                                         \
+  } while (0)
+
+static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+static std::mutex g_rtc_mu;  // PGM_RTC_SERIAL=1: one hipRTC compile at a time
+
+// ----------------------------------------------------------------------------- code-object cache
+// On-disk cache of specialised code objects: directory PGM_KERNEL_CACHE (default
+// $XDG_CACHE_HOME/pgmpy_amd or ~/.cache/pgmpy_amd; "0" disables), one file per source hash holding
+// the full source (compared on load, so a hash collision only misses) and the gfx950 code object.
+static std::string rtc_cache_dir() {
+  static const std::string dir = [] {
+    const char *e = getenv("PGM_KERNEL_CACHE");
+    if (e) return std::string(strcmp(e, "0") == 0 ? "" : e);
+    const char *x = getenv("XDG_CACHE_HOME");
+    if (x && *x) return std::string(x) + "/pgmpy_amd";
+    const char *h = getenv("HOME");
+    return h && *h ? std::string(h) + "/.cache/pgmpy_amd" : std::string();
+  }();
+  return dir;
+}
+
+static std::string rtc_cache_path(const std::string &src) {
+  const std::string dir = rtc_cache_dir();
+  if (dir.empty()) return dir;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the source and the ABI version
+  for (unsigned char c : src) h = (h ^ c) * 1099511628211ull;
+  h = (h ^ (uint64_t)pgm_version()) * 1099511628211ull;
+  char name[64];
+  snprintf(name, sizeof name, "/k%016llx.co", (unsigned long long)h);
+  return dir + name;
+}
+
+static bool rtc_cache_load(const std::string &path, const std::string &src, std::vector<char> &code) {
+  if (path.empty()) return false;
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint64_t n = 0, m = 0;
+  bool ok = fread(&n, 8, 1, f) == 1 && n == src.size();
+  std::string s2;
+  if (ok) {
+    s2.resize(n);
+    ok = fread(&s2[0], 1, n, f) == n && s2 == src && fread(&m, 8, 1, f) == 1 && m > 0 && m < (1ull << 30);
+  }
+  if (ok) {
+    code.resize(m);
+    ok = fread(code.data(), 1, m, f) == m;
+  }
+  fclose(f);
+  return ok;
+}
+
+static void rtc_cache_store(const std::string &path, const std::string &src, const std::vector<char> &code) {
+  if (path.empty()) return;
+  const std::string dir = path.substr(0, path.rfind('/'));
+  // mkdir -p: create each component
+  for (size_t i = 1; i <= dir.size(); ++i)
+    if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+  const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
+  FILE *f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const uint64_t n = src.size(), m = code.size();
+  const bool ok = fwrite(&n, 8, 1, f) == 1 && fwrite(src.data(), 1, n, f) == n && fwrite(&m, 8, 1, f) == 1 &&
+                  fwrite(code.data(), 1, m, f) == m;
+  if (fclose(f) == 0 && ok) (void)rename(tmp.c_str(), path.c_str());
+  else (void)remove(tmp.c_str());
+}
+
+// gfx950 code object of a specialised kernel source: the disk cache, else hipRTC (then cached)
+bool pgmi_rtc_code(const std::string &src, const char *what, std::vector<char> &code) {
+  const std::string path = rtc_cache_path(src);
+  if (rtc_cache_load(path, src, code)) return true;
+  // hipRTC programs compile concurrently from several threads (pgm_pm_prepare); PGM_RTC_SERIAL=1
+  // serialises every compile
+  static const bool serial = getenv("PGM_RTC_SERIAL") && atoi(getenv("PGM_RTC_SERIAL")) != 0;
+  std::unique_lock<std::mutex> lk(g_rtc_mu, std::defer_lock);
+  if (serial) lk.lock();
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return false;
+  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    fprintf(stderr, "pgmhip: %s did not compile (generic kernel used):\n%s\n", what, log.c_str());
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t sz = 0;
+  hiprtcGetCodeSize(prog, &sz);
+  code.resize(sz);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  rtc_cache_store(path, src, code);
+  return true;
+}
+
+
+// ----------------------------------------------------------------------------- specialised product+marginal
+// The fused batched-BP step (k_productn_marg_jx) with its plan baked in as literals: outer digits
+// decoded with constant divisors, the reduced entries walked as nested loops with literal bounds and
+// strides (inner ones unrolled, so several entries' operand loads are in flight together), operands
+// that lack the row axis read at wave-uniform addresses (scalar loads), one 1-D grid with an optional
+// XCD-grouped block order.  Compiled once per shape (hipRTC, cached by source), bound to its
+// pointers, launched by pgm_pm_bound_run (capturable in a HIP graph).
+// two marginals of one product in a single pass (no product stored): block = one state of the dims
+// both keep (K) x a row chunk; the dims only one of them keeps (U = R1 + R2) are unrolled at
+// generation time with one register accumulator per R1 / R2 state; dims neither keeps (Z) are runtime
+// inner loops.  Batched-BP distribute: a parent's sigma' for two child scopes from its operands.
+struct PMMulti {
+  int n_ops = 0;
+  int kind[MOPS] = {}, vec[MOPS] = {};
+  int nK = 0, nU = 0, nZ = 0;
+  unsigned kcard[KMAX] = {}, ucard[KMAX] = {}, zcard[KMAX] = {};
+  int64_t ks[MOPS][KMAX] = {}, k1[KMAX] = {}, k2[KMAX] = {};
+  int64_t us[MOPS][KMAX] = {}, u1[KMAX] = {}, u2[KMAX] = {};
+  int64_t zs[MOPS][KMAX] = {};
+  uint32_t n_outer = 0, NP = 0;
+  unsigned n1 = 1, n2 = 1;  // accumulators (R1 / R2 states)
+};
+
+struct PMSpec {  // one fused step's specialisation
+  int multi = 0;  // 1: PMMulti body (two marginals), else the ProdMK body
+  PMMulti mm;
+  ProdMK k;
+  int red = PGM_RED_SUM, XI = 1, unroll = 8;
+  bool store = true, xcd = false, nt = false;
+  bool has_m = true;  // false: the product alone (pgm_product_n_bind), no marginal
+  unsigned gx = 1;
+  uint64_t total = 0;  // blocks
+};
+
+// a bound launch: one step, or several independent steps merged into one kernel (pgm_pm_merge:
+// body i runs on blocks [start_i, start_i + total_i), starts padded to multiples of 8 so each body's
+// XCD grouping holds)
+struct PMBound {
+  hipFunction_t fn = nullptr;  // compiled lazily: pgm_pm_prepare (in parallel) or the first run
+  std::string src;
+  unsigned blocks = 0;
+  std::vector<PMSpec> specs;
+  std::vector<const double *> ptrs;  // 6 per body: o0..o3, C, M
+};
+
+static int pm_knob(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// body `name` of one step: a device function of its block index within the step
+static std::string pm_body(const PMSpec &sp, const std::string &name) {
+  const ProdMK &k = sp.k;
+  const int red = sp.red, XI = sp.XI, unroll = sp.unroll;
+  const bool store = sp.store, xcd = sp.xcd, nt = sp.nt, has_m = sp.has_m;
+  const unsigned gx = sp.gx;
+  const uint64_t total = sp.total;
+  std::string o;
+  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
+             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
+             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
+  o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
+  if (xcd) pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n",
+                   (unsigned long long)(total / 8));
+  pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
+  o += "  unsigned idx = ob;\n  long long oc = 0, om = 0";
+  for (int i = 0; i < k.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
+  o += ";\n  (void)oc; (void)idx;\n";
+  const int kx = k.nk - 1;  // kept outer dims 0..kx-1 (kx-1 fastest), the row dim last
+  for (int q = kx - 1; q >= 0; --q) {
+    const unsigned dq = k.kdiv[q].d;
+    pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", dq, dq);
+    if (k.ksc[q]) pgmi_appendf(o, " oc += (long long)g * %lldLL;", (long long)k.ksc[q]);
+    if (k.ksm[q]) pgmi_appendf(o, " om += (long long)g * %lldLL;", (long long)k.ksm[q]);
+    for (int i = 0; i < k.n_ops; ++i)
+      if (k.ks[i][q]) pgmi_appendf(o, " f%d += (long long)g * %lldLL;", i, (long long)k.ks[i][q]);
+    o += " }\n";
+  }
+  const uint32_t NP = k.NP;
+  const bool tail = NP % (256u * XI) != 0;
+  pgmi_appendf(o, "  const unsigned xbase = xb * %uu + threadIdx.x;\n", 256u * XI);
+  for (int u = 0; u < XI; ++u) {
+    pgmi_appendf(o, "  const unsigned x%d = xbase + %uu;\n", u, 256u * u);
+    if (tail)
+      pgmi_appendf(o, "  const unsigned c%d = x%d < %uu ? x%d : %uu;\n", u, u, NP, u, NP - 1);
+    else
+      pgmi_appendf(o, "  const unsigned c%d = x%d;\n", u, u);
+  }
+  // operands constant over the reduced entries: once per block
+  for (int i = 0; i < k.n_ops; ++i) {
+    if (k.jvar[i]) continue;
+    if (k.vec[i]) {
+      for (int u = 0; u < XI; ++u)
+        pgmi_appendf(o, "  const pgm_d2 h%d_%d = ((const pgm_d2 *)(o%d + f%d))[c%d];\n", i, u, i, i, u);
+    } else {
+      pgmi_appendf(o, "  const double h%d = o%d[f%d];\n", i, i, i);
+    }
+  }
+  const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
+  for (int u = 0; u < XI && has_m; ++u) pgmi_appendf(o, "  pgm_d2 a%d = {%s, %s};\n", u, init, init);
+  // reduced dims as nested loops (dim 0 outermost: the generic kernel's entry order); the innermost
+  // dims whose trip product stays within `unroll` are unrolled
+  int first_unrolled = k.nr;
+  {
+    uint64_t prod = 1;
+    for (int r = k.nr - 1; r >= 0; --r) {
+      prod *= k.rdiv[r].d;
+      if (prod > (uint64_t)unroll) break;
+      first_unrolled = r;
+    }
+  }
+  std::string ind = "  ";
+  for (int r = 0; r < k.nr; ++r) {
+    if (r >= first_unrolled)
+      pgmi_appendf(o, "%s#pragma unroll\n", ind.c_str());
+    else if (r == k.nr - 1)  // an innermost loop too long to unroll fully: `unroll` entries at a time
+      pgmi_appendf(o, "%s#pragma unroll %d\n", ind.c_str(), std::max(1, unroll));
+    else
+      pgmi_appendf(o, "%s#pragma unroll 1\n", ind.c_str());
+    pgmi_appendf(o, "%sfor (int r%d = 0; r%d < %u; ++r%d) {\n", ind.c_str(), r, r, k.rdiv[r].d, r);
+    ind += "  ";
+  }
+  auto lin = [&](const int64_t *s) {  // literal offset of the current reduced entry
+    std::string e = "0LL";
+    for (int r = 0; r < k.nr; ++r)
+      if (s[r]) e += " + (long long)r" + std::to_string(r) + " * " + std::to_string((long long)s[r]) + "LL";
+    return e;
+  };
+  for (int i = 0; i < k.n_ops; ++i) {
+    if (!k.jvar[i]) continue;
+    const std::string J = lin(k.rs[i]);
+    if (k.vec[i]) {
+      pgmi_appendf(o, "%sconst pgm_d2 *p%d = (const pgm_d2 *)(o%d + f%d + %s);\n", ind.c_str(), i, i, i, J.c_str());
+      for (int u = 0; u < XI; ++u) pgmi_appendf(o, "%sconst pgm_d2 v%d_%d = p%d[c%d];\n", ind.c_str(), i, u, i, u);
+    } else {
+      pgmi_appendf(o, "%sconst double s%d = o%d[f%d + %s];\n", ind.c_str(), i, i, i, J.c_str());
+    }
+  }
+  for (int u = 0; u < XI; ++u) {
+    for (int h = 0; h < 2; ++h) {
+      const char cx = h ? 'y' : 'x';
+      auto term = [&](int i) {
+        char buf[64];
+        if (k.jvar[i] && k.vec[i]) snprintf(buf, sizeof buf, "v%d_%d.%c", i, u, cx);
+        else if (k.jvar[i]) snprintf(buf, sizeof buf, "s%d", i);
+        else if (k.vec[i]) snprintf(buf, sizeof buf, "h%d_%d.%c", i, u, cx);
+        else snprintf(buf, sizeof buf, "h%d", i);
+        return std::string(buf);
+      };
+      std::string e = "1.0";
+      for (int i = 0; i < k.n_ops; ++i) {
+        if (k.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
+        else if (k.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
+          e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+      }
+      pgmi_appendf(o, "%sconst double w%d%c = %s;\n", ind.c_str(), u, cx, e.c_str());
+    }
+    pgmi_appendf(o, "%sconst pgm_d2 w%d = {w%dx, w%dy};\n", ind.c_str(), u, u, u);
+  }
+  if (store) {
+    pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
+    for (int u = 0; u < XI; ++u) {
+      const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
+      if (nt)
+        pgmi_appendf(o, "%s%s__builtin_nontemporal_store(w%d, cj + x%d);\n", ind.c_str(), guard.c_str(), u, u);
+      else
+        pgmi_appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
+    }
+  }
+  for (int u = 0; u < XI && has_m; ++u) {
+    if (red == PGM_RED_MAX)
+      pgmi_appendf(o, "%sa%d.x = pgm_maxn(a%d.x, w%d.x); a%d.y = pgm_maxn(a%d.y, w%d.y);\n", ind.c_str(), u, u, u, u,
+              u, u);
+    else
+      pgmi_appendf(o, "%sa%d += w%d;\n", ind.c_str(), u, u);
+  }
+  for (int r = k.nr - 1; r >= 0; --r) {
+    ind.resize(ind.size() - 2);
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+  }
+  for (int u = 0; u < XI && has_m; ++u) {
+    const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
+    pgmi_appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
+  }
+  o += "}\n";
+  return o;
+}
+
+static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
+  // the target with fewer states of its own dims (R_reg) keeps one register accumulator per state,
+  // its dims unrolled innermost; the other target's own dims (R_str) are runtime loops outermost, and
+  // its marginal is complete after each of their iterations (everything inside is summed), so it is
+  // stored there — registers stay bounded by the smaller target
+  const PMMulti &q = sp.mm;
+  const int red = sp.red;
+  const int treg = q.n1 <= q.n2 ? 0 : 1;  // 0: M1 (C slot) in registers, 1: M2 (M slot)
+  const int64_t *sreg = treg == 0 ? q.u1 : q.u2;
+  const int64_t *sstr = treg == 0 ? q.u2 : q.u1;
+  const char *preg = treg == 0 ? "C" : "M", *pstr = treg == 0 ? "M" : "C";
+  const char *mreg = treg == 0 ? "m1" : "m2", *mstr = treg == 0 ? "m2" : "m1";
+  const unsigned nreg = treg == 0 ? q.n1 : q.n2;
+  std::string o;
+  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
+             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
+             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
+  o += "  (void)o1; (void)o2; (void)o3;\n";
+  if (sp.xcd) pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;\n", (unsigned long long)(sp.total / 8));
+  pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", sp.gx, sp.gx);
+  o += "  unsigned idx = ob;\n  long long m1 = 0, m2 = 0";
+  for (int i = 0; i < q.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
+  o += ";\n  (void)idx;\n";
+  for (int d = q.nK - 1; d >= 0; --d) {
+    pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", q.kcard[d], q.kcard[d]);
+    if (q.k1[d]) pgmi_appendf(o, " m1 += (long long)g * %lldLL;", (long long)q.k1[d]);
+    if (q.k2[d]) pgmi_appendf(o, " m2 += (long long)g * %lldLL;", (long long)q.k2[d]);
+    for (int i = 0; i < q.n_ops; ++i)
+      if (q.ks[i][d]) pgmi_appendf(o, " f%d += (long long)g * %lldLL;", i, (long long)q.ks[i][d]);
+    o += " }\n";
+  }
+  const bool tail = q.NP % 256u != 0;
+  o += "  const unsigned x = xb * 256u + threadIdx.x;\n";
+  if (tail) pgmi_appendf(o, "  const unsigned c = x < %uu ? x : %uu;\n", q.NP, q.NP - 1);
+  else o += "  const unsigned c = x;\n";
+  const std::string guard = tail ? "if (x < " + std::to_string(q.NP) + "u) " : "";
+  const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
+  for (unsigned a = 0; a < nreg; ++a) pgmi_appendf(o, "  pgm_d2 ar_%u = {%s, %s};\n", a, init, init);
+  // runtime loops: the streamed target's own dims (u), then the dims neither keeps (z)
+  std::string ind = "  ";
+  std::vector<int> ustr, ureg;
+  for (int d = 0; d < q.nU; ++d) (sstr[d] ? ustr : ureg).push_back(d);
+  for (int d : ustr) {
+    pgmi_appendf(o, "%s#pragma unroll 1\n%sfor (int u%d = 0; u%d < %u; ++u%d) {\n", ind.c_str(), ind.c_str(), d, d,
+            q.ucard[d], d);
+    ind += "  ";
+  }
+  pgmi_appendf(o, "%spgm_d2 as = {%s, %s};\n", ind.c_str(), init, init);
+  for (int z = 0; z < q.nZ; ++z) {
+    pgmi_appendf(o, "%s#pragma unroll %s\n", ind.c_str(), z == q.nZ - 1 ? "2" : "1");
+    pgmi_appendf(o, "%sfor (int z%d = 0; z%d < %u; ++z%d) {\n", ind.c_str(), z, z, q.zcard[z], z);
+    ind += "  ";
+  }
+  auto runtime_off = [&](const int64_t *zs, const int64_t (*us)[KMAX], int i) {
+    std::string e;
+    for (int z = 0; z < q.nZ; ++z)
+      if (zs[z]) e += " + (long long)z" + std::to_string(z) + " * " + std::to_string((long long)zs[z]) + "LL";
+    for (int d : ustr)
+      if (us[i][d]) e += " + (long long)u" + std::to_string(d) + " * " + std::to_string((long long)us[i][d]) + "LL";
+    return e;
+  };
+  uint64_t nr = 1;
+  for (int d : ureg) nr *= q.ucard[d];
+  for (uint64_t ra = 0; ra < nr; ++ra) {
+    unsigned dig[KMAX] = {};
+    uint64_t rem = ra;
+    for (int k = (int)ureg.size() - 1; k >= 0; --k) {
+      dig[ureg[k]] = (unsigned)(rem % q.ucard[ureg[k]]);
+      rem /= q.ucard[ureg[k]];
+    }
+    int64_t off[MOPS] = {};
+    for (int d : ureg)
+      for (int i = 0; i < q.n_ops; ++i) off[i] += (int64_t)dig[d] * q.us[i][d];
+    pgmi_appendf(o, "%s{\n", ind.c_str());
+    for (int i = 0; i < q.n_ops; ++i) {
+      const std::string ro = runtime_off(q.zs[i], q.us, i);
+      if (q.vec[i])
+        pgmi_appendf(o, "%s  const pgm_d2 v%d = ((const pgm_d2 *)(o%d + f%d + %lldLL%s))[c];\n", ind.c_str(), i, i, i,
+                (long long)off[i], ro.c_str());
+      else
+        pgmi_appendf(o, "%s  const double s%d = o%d[f%d + %lldLL%s];\n", ind.c_str(), i, i, i, (long long)off[i],
+                ro.c_str());
+    }
+    for (int h = 0; h < 2; ++h) {
+      const char cx = h ? 'y' : 'x';
+      auto term = [&](int i) {
+        char buf[32];
+        if (q.vec[i]) snprintf(buf, sizeof buf, "v%d.%c", i, cx);
+        else snprintf(buf, sizeof buf, "s%d", i);
+        return std::string(buf);
+      };
+      std::string e = "1.0";
+      for (int i = 0; i < q.n_ops; ++i) {
+        if (q.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
+        else if (q.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
+          e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+      }
+      pgmi_appendf(o, "%s  const double w%c = %s;\n", ind.c_str(), cx, e.c_str());
+    }
+    pgmi_appendf(o, "%s  const pgm_d2 w = {wx, wy};\n", ind.c_str());
+    if (red == PGM_RED_MAX)
+      pgmi_appendf(o, "%s  ar_%llu.x = pgm_maxn(ar_%llu.x, w.x); ar_%llu.y = pgm_maxn(ar_%llu.y, w.y); "
+                 "as.x = pgm_maxn(as.x, w.x); as.y = pgm_maxn(as.y, w.y);\n",
+              ind.c_str(), (unsigned long long)ra, (unsigned long long)ra, (unsigned long long)ra,
+              (unsigned long long)ra);
+    else
+      pgmi_appendf(o, "%s  ar_%llu += w; as += w;\n", ind.c_str(), (unsigned long long)ra);
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+  }
+  for (int z = q.nZ - 1; z >= 0; --z) {
+    ind.resize(ind.size() - 2);
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+  }
+  {  // the streamed target's marginal for this iteration is complete
+    std::string e;
+    for (int d : ustr)
+      e += " + (long long)u" + std::to_string(d) + " * " + std::to_string((long long)sstr[d]) + "LL";
+    pgmi_appendf(o, "%s%s((pgm_d2 *)(%s + %s%s))[x] = as;\n", ind.c_str(), guard.c_str(), pstr, mstr, e.c_str());
+  }
+  for (size_t k = 0; k < ustr.size(); ++k) {
+    ind.resize(ind.size() - 2);
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+  }
+  for (uint64_t ra = 0; ra < nr; ++ra) {  // register target: accumulator ra at its digits' offset
+    uint64_t rem = ra;
+    int64_t off = 0;
+    for (int k = (int)ureg.size() - 1; k >= 0; --k) {
+      off += (int64_t)(rem % q.ucard[ureg[k]]) * sreg[ureg[k]];
+      rem /= q.ucard[ureg[k]];
+    }
+    pgmi_appendf(o, "  %s((pgm_d2 *)(%s + %s + %lldLL))[x] = ar_%llu;\n", guard.c_str(), preg, mreg, (long long)off,
+            (unsigned long long)ra);
+  }
+  o += "}\n";
+  return o;
+}
+
+// kernel pgm_pm over the bodies (kernel argument: 6 pointers per body); starts[i] = first block of
+// body i, returns the grid size through *blocks
+static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint64_t> &starts, uint64_t *blocks) {
+  std::string o =
+      "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
+      "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
+      "__device__ __forceinline__ double pgm_ratio(double a, double b) { const double r = a / b; "
+      "return r != r ? 0.0 : r; }\n"
+      "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
+  const size_t n = specs.size();
+  starts.assign(n, 0);
+  uint64_t at = 0;
+  for (size_t i = 0; i < n; ++i) {
+    at = (at + 7) / 8 * 8;
+    starts[i] = at;
+    at += specs[i].total;
+    o += specs[i].multi ? pm_multi_body(specs[i], "pm" + std::to_string(i)) : pm_body(specs[i], "pm" + std::to_string(i));
+  }
+  *blocks = at;
+  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%zu][6]; };\n", n);
+  o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const pgm_pm_args a) {\n"
+       "  const unsigned b = blockIdx.x;\n";
+  for (size_t i = 0; i < n; ++i) {
+    if (n == 1) {
+      o += "  pm0(b, a.p[0][0], a.p[0][1], a.p[0][2], a.p[0][3], (double *)a.p[0][4], (double *)a.p[0][5]);\n";
+      break;
+    }
+    pgmi_appendf(o, "  if (b >= %lluu && b < %lluu) { pm%zu(b - %lluu, a.p[%zu][0], a.p[%zu][1], a.p[%zu][2], "
+               "a.p[%zu][3], (double *)a.p[%zu][4], (double *)a.p[%zu][5]); return; }\n",
+            (unsigned long long)starts[i], (unsigned long long)(starts[i] + specs[i].total), i,
+            (unsigned long long)starts[i], i, i, i, i, i, i);
+  }
+  o += "}\n";
+  return o;
+}
+
+static std::mutex g_pm_mu;
+static std::vector<std::pair<std::string, hipFunction_t>> g_pm_cache;  // source -> kernel (process lifetime)
+
+static hipFunction_t pm_cached(const std::string &src) {  // caller holds g_pm_mu
+  for (auto &e : g_pm_cache)
+    if (e.first == src) return e.second;
+  return nullptr;
+}
+
+static hipFunction_t pm_load(const std::string &src, const std::vector<char> &code) {  // caller holds g_pm_mu
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "pgm_pm") != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  g_pm_cache.emplace_back(src, fn);
+  return fn;
+}
+
+static hipFunction_t pm_compile(const std::string &src) {
+  std::lock_guard<std::mutex> lk(g_pm_mu);
+  if (hipFunction_t f = pm_cached(src)) return f;
+  std::vector<char> code;
+  if (!pgmi_rtc_code(src, "specialised product+marginal kernel", code)) return nullptr;
+  return pm_load(src, code);
+}
+
+// compile every bound step's kernel that is not loaded yet: distinct sources on up to
+// PGM_RTC_THREADS (default 16) threads, then load the modules
+static int pm_prepare(PMBound *const *bs, int n) {
+  std::vector<std::string> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_pm_mu);
+    for (int i = 0; i < n; ++i) {
+      if (!bs[i] || bs[i]->fn) continue;
+      if (hipFunction_t f = pm_cached(bs[i]->src)) {
+        bs[i]->fn = f;
+        continue;
+      }
+      if (std::find(todo.begin(), todo.end(), bs[i]->src) == todo.end()) todo.push_back(bs[i]->src);
+    }
+  }
+  if (!todo.empty()) {
+    std::vector<std::vector<char>> codes(todo.size());
+    std::vector<char> ok(todo.size(), 0);
+    const char *te = getenv("PGM_RTC_THREADS");
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(todo.size(), te ? (size_t)atoi(te) : 16));
+    std::atomic<size_t> next(0);
+    auto work = [&] {
+      for (size_t i; (i = next.fetch_add(1)) < todo.size();)
+        ok[i] = pgmi_rtc_code(todo[i], "specialised product+marginal kernel", codes[i]) ? 1 : 0;
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    std::lock_guard<std::mutex> lk(g_pm_mu);
+    for (size_t i = 0; i < todo.size(); ++i) {
+      if (!ok[i] || (!pm_cached(todo[i]) && !pm_load(todo[i], codes[i])))
+        return pgmi_failf(PGM_EDEVICE, "specialised product+marginal kernel: compile / load failed");
+    }
+    for (int i = 0; i < n; ++i)
+      if (bs[i] && !bs[i]->fn) bs[i]->fn = pm_cached(bs[i]->src);
+  }
+  return PGM_OK;
+}
+
+
+// ============================================================================= C-ABI
+extern "C" {
+
+static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double *C, const int64_t *marg_s,
+                   int32_t reduce, double *M, void **bound, std::string *src_out, bool has_m = true) {
+  *bound = nullptr;
+  if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
+    return pgmi_failf(PGM_EINVAL, "product_n_marginal: reduce must be PGM_RED_SUM or PGM_RED_MAX");
+  ProdMK k;
+  dim3 g;
+  const int r = pgmi_plan_product_marg(d, ops, C, marg_s, M, k, g);
+  if (r < 0) return r;
+  if (r == 0)
+    return pgmi_failf(PGM_EINVAL, "product_n_marginal: shape not supported by the fused kernel "
+                            "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
+  // knobs: PGM_PM_JIT=0 keeps the generic kernel; PGM_PM_JIT_MIN = smallest clique (entries incl.
+  // rows) specialised; PGM_PM_XI row pairs per lane; PGM_PM_UNROLL entries unrolled; PGM_PM_XCD
+  // block order grouped by XCD; PGM_PM_NT nontemporal belief stores
+  static const int on = pm_knob("PGM_PM_JIT", 1);
+  // defaults measured on MI355X, pathfinder C4 (4,000 / 1,000 rows: generic 781K / 515K calibrations/s;
+  // specialised above 2M entries 911K / 601K; + one row pair per lane, nontemporal belief stores and
+  // XCD-grouped blocks 933K; threshold 256K entries 648K at 1,000 rows)
+  static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 18);
+  static const int xi_knob = pm_knob("PGM_PM_XI", 1);
+  static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
+  static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
+  static const int nt = pm_knob("PGM_PM_NT", 1);
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
+  const uint64_t entries = (uint64_t)k.n_outer * (uint64_t)k.n_red * 2ull * k.NP;
+  if (!on || no_jit || entries < (uint64_t)min_entries) return PGM_OK;  // *bound NULL: generic kernel
+  const int XI = xi_knob == 2 || xi_knob == 4 ? xi_knob : 1;
+  const uint64_t gx = (k.NP + 256ull * XI - 1) / (256ull * XI);
+  const uint64_t total = gx * (uint64_t)k.n_outer;
+  if (total >= (1ull << 31)) return PGM_OK;
+  PMSpec sp;
+  sp.k = k;
+  sp.red = reduce;
+  sp.XI = XI;
+  sp.unroll = unroll;
+  sp.store = C != nullptr;
+  sp.has_m = has_m;
+  sp.xcd = xcd_knob && total % 8 == 0;
+  sp.nt = nt != 0;
+  sp.gx = (unsigned)gx;
+  sp.total = total;
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source({sp}, starts, &blocks);
+  if (src_out) {
+    *src_out = src;
+    return PGM_OK;
+  }
+  PMBound *b = new (std::nothrow) PMBound;
+  if (!b) return pgmi_failf(PGM_ENOMEM, "product_n_marginal_bind: out of host memory");
+  b->src = src;
+  b->blocks = (unsigned)blocks;
+  b->specs.push_back(sp);
+  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(k.ops[t]);
+  b->ptrs.push_back(C);
+  b->ptrs.push_back(M);
+  *bound = b;
+  return PGM_OK;
+}
+
+int pgm_product_n_marginal_bind(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                const int64_t *marg_s, int32_t reduce, double *M, void **bound) {
+  STALE_PROBE();
+  if (!bound) return pgmi_failf(PGM_EINVAL, "product_n_marginal_bind: null bound");
+  return pm_bind(d, ops, C, marg_s, reduce, M, bound, nullptr);
+}
+
+int pgm_product_n_bind(const pgm_productn_desc *d, const double *const *ops, double *C, void **bound) {
+  STALE_PROBE();
+  if (!bound || !d || !C) return pgmi_failf(PGM_EINVAL, "product_n_bind: null argument");
+  *bound = nullptr;
+  if (d->n_keep < 1 || d->n_keep > PGM_MAX_DIMS) return pgmi_failf(PGM_EINVAL, "product_n_bind: n_keep out of range");
+  // the product as a fused step whose every dim is kept (no reduced entries) and no marginal stored
+  int64_t ms[PGM_MAX_DIMS];
+  for (int i = 0; i < d->n_keep; ++i) ms[i] = d->keep_sc[i] ? d->keep_sc[i] : 1;
+  ProdMK k;
+  dim3 g;
+  const int r = pgmi_plan_product_marg(d, ops, C, ms, C, k, g);
+  if (r <= 0) return r < 0 ? r : PGM_OK;  // shape not handled: *bound NULL, the generic kernel runs
+  return pm_bind(d, ops, C, ms, PGM_RED_SUM, C, bound, nullptr, false);
+}
+
+// plan of the two-marginal pass; 1 = supported (q filled), 0 = not (caller runs two passes)
+static int plan_two_marginals(const pgm_productn_desc *d, const double *const *ops, const int64_t *s1,
+                              const int64_t *s2, const double *M1, const double *M2, PMMulti &q) {
+  if (!d || !ops || !s1 || !s2 || !M1 || !M2) return pgmi_failf(PGM_EINVAL, "product_n_marginals: null argument");
+  if (d->n_ops < 1 || d->n_ops > MOPS || d->n_keep < 2 || d->n_keep > PGM_MAX_DIMS) return 0;
+  const int last = d->n_keep - 1;
+  const int64_t NX = d->keep_card[last];
+  if (NX < 64 || NX % 2 || d->keep_sc[last] != 1 || s1[last] != 1 || s2[last] != 1) return 0;
+  if (((uintptr_t)M1 & 15) || ((uintptr_t)M2 & 15)) return 0;
+  q = PMMulti();
+  q.n_ops = d->n_ops;
+  for (int t = 0; t < d->n_ops; ++t) {
+    if (!ops[t] || d->op_kind[t] < 0 || d->op_kind[t] > 2) return pgmi_failf(PGM_EINVAL, "product_n_marginals: operand %d", t);
+    const int64_t sx = d->keep_s[t][last];
+    if (sx != 0 && sx != 1) return 0;
+    if (sx == 1 && ((uintptr_t)ops[t] & 15)) return 0;
+    q.vec[t] = sx == 1;
+    q.kind[t] = d->op_kind[t];
+  }
+  uint64_t nk = 1, nu = 1;
+  for (int i = 0; i < last; ++i) {
+    const int64_t c = d->keep_card[i];
+    if (c <= 0) return pgmi_failf(PGM_EINVAL, "product_n_marginals: keep_card[%d] <= 0", i);
+    if (c == 1) continue;
+    if ((s1[i] && s1[i] % 2) || (s2[i] && s2[i] % 2)) return 0;
+    for (int t = 0; t < d->n_ops; ++t)
+      if (q.vec[t] && d->keep_s[t][i] % 2) return 0;
+    if (s1[i] && s2[i]) {
+      if (q.nK >= KMAX) return 0;
+      q.kcard[q.nK] = (unsigned)c;
+      q.k1[q.nK] = s1[i];
+      q.k2[q.nK] = s2[i];
+      for (int t = 0; t < d->n_ops; ++t) q.ks[t][q.nK] = d->keep_s[t][i];
+      ++q.nK;
+      nk *= (uint64_t)c;
+    } else if (s1[i] || s2[i]) {
+      if (q.nU >= KMAX) return 0;
+      q.ucard[q.nU] = (unsigned)c;
+      q.u1[q.nU] = s1[i];
+      q.u2[q.nU] = s2[i];
+      for (int t = 0; t < d->n_ops; ++t) q.us[t][q.nU] = d->keep_s[t][i];
+      ++q.nU;
+      nu *= (uint64_t)c;
+      if (s1[i]) q.n1 *= (unsigned)c;
+      else q.n2 *= (unsigned)c;
+    } else {
+      if (q.nZ >= KMAX) return 0;
+      q.zcard[q.nZ] = (unsigned)c;
+      for (int t = 0; t < d->n_ops; ++t) q.zs[t][q.nZ] = d->keep_s[t][i];
+      ++q.nZ;
+    }
+  }
+  // register accumulators: the smaller target's own states, unrolled (knob PGM_PM2_MAX_ACC, default 16)
+  static const unsigned max_acc = getenv("PGM_PM2_MAX_ACC") ? (unsigned)atoi(getenv("PGM_PM2_MAX_ACC")) : 16u;
+  (void)nu;
+  if (std::min(q.n1, q.n2) > max_acc || nk >= (1ull << 31)) return 0;
+  q.n_outer = (uint32_t)nk;
+  q.NP = (uint32_t)(NX / 2);
+  const uint64_t gx = (q.NP + 255) / 256;
+  if (gx * nk < 256) return 0;  // fewer blocks than CUs: two single-marginal passes fill the chip better
+  return 1;
+}
+
+int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const *ops, const int64_t *marg_s1,
+                                 double *M1, const int64_t *marg_s2, double *M2, int32_t reduce, void **bound) {
+  STALE_PROBE();
+  if (!bound) return pgmi_failf(PGM_EINVAL, "product_n_marginals_bind: null bound");
+  *bound = nullptr;
+  if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
+    return pgmi_failf(PGM_EINVAL, "product_n_marginals: reduce must be PGM_RED_SUM or PGM_RED_MAX");
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr || pm_knob("PGM_PM_JIT", 1) == 0 ||
+                             pm_knob("PGM_PM2", 1) == 0;
+  if (no_jit) return PGM_OK;
+  PMSpec sp;
+  const int r = plan_two_marginals(d, ops, marg_s1, marg_s2, M1, M2, sp.mm);
+  if (r <= 0) return r;
+  sp.multi = 1;
+  sp.red = reduce;
+  sp.store = false;
+  sp.gx = (sp.mm.NP + 255) / 256;
+  sp.total = (uint64_t)sp.gx * sp.mm.n_outer;
+  sp.xcd = pm_knob("PGM_PM_XCD", 1) && sp.total % 8 == 0;
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source({sp}, starts, &blocks);
+  PMBound *b = new (std::nothrow) PMBound;
+  if (!b) return pgmi_failf(PGM_ENOMEM, "product_n_marginals_bind: out of host memory");
+  b->src = src;
+  b->blocks = (unsigned)blocks;
+  b->specs.push_back(sp);
+  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(t < d->n_ops ? ops[t] : ops[0]);
+  b->ptrs.push_back(M1);  // the C slot
+  b->ptrs.push_back(M2);  // the M slot
+  *bound = b;
+  return PGM_OK;
+}
+
+int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
+                                  const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len) {
+  STALE_PROBE();
+  if (!buf || len == 0) return pgmi_failf(PGM_EINVAL, "product_n_marginal_source: null buffer");
+  void *unused = nullptr;
+  std::string src;
+  const int r = pm_bind(d, ops, C, marg_s, reduce, M, &unused, &src);
+  if (r < 0) return r;
+  const size_t n = std::min(len - 1, src.size());
+  memcpy(buf, src.data(), n);
+  buf[n] = 0;
+  return (int)src.size();
+}
+
+int pgm_pm_bound_run(void *bound, void *stream) {
+  STALE_PROBE();
+  PMBound *b = (PMBound *)bound;
+  if (!b) return pgmi_failf(PGM_EINVAL, "pm_bound_run: null bound");
+  if (!b->fn) {
+    const int r = pm_prepare(&b, 1);
+    if (r != PGM_OK) return r;
+  }
+  size_t sz = b->ptrs.size() * sizeof(void *);
+  void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)b->ptrs.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+  HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(stream), nullptr, extra));
+  return PGM_OK;
+}
+
+int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
+  STALE_PROBE();
+  if (!bounds || !merged || n < 1 || n > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: 1..64 bound steps");
+  *merged = nullptr;
+  std::vector<PMSpec> specs;
+  std::vector<const double *> ptrs;
+  for (int i = 0; i < n; ++i) {
+    const PMBound *b = (const PMBound *)bounds[i];
+    if (!b) return pgmi_failf(PGM_EINVAL, "pm_merge: null bound %d", i);
+    specs.insert(specs.end(), b->specs.begin(), b->specs.end());
+    ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
+  }
+  if (specs.size() > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: more than 64 bodies");
+  std::vector<uint64_t> starts;
+  uint64_t blocks = 0;
+  const std::string src = pm_source(specs, starts, &blocks);
+  if (blocks >= (1ull << 31)) return PGM_OK;  // too large for one grid: keep the separate launches
+  PMBound *m = new (std::nothrow) PMBound;
+  if (!m) return pgmi_failf(PGM_ENOMEM, "pm_merge: out of host memory");
+  m->src = src;
+  m->blocks = (unsigned)blocks;
+  m->specs = specs;
+  m->ptrs = ptrs;
+  *merged = m;
+  return PGM_OK;
+}
+
+int pgm_pm_bound_source(void *bound, char *buf, size_t len) {
+  STALE_PROBE();
+  const PMBound *b = (const PMBound *)bound;
+  if (!b || !buf || len == 0) return pgmi_failf(PGM_EINVAL, "pm_bound_source: null argument");
+  const size_t n = std::min(len - 1, b->src.size());
+  memcpy(buf, b->src.data(), n);
+  buf[n] = 0;
+  return (int)b->src.size();
+}
+
+int pgm_pm_prepare(void *const *bounds, int32_t n) {
+  STALE_PROBE();
+  if (!bounds || n < 0) return pgmi_failf(PGM_EINVAL, "pm_prepare: null bounds");
+  return pm_prepare((PMBound *const *)bounds, n);
+}
+
+int pgm_pm_bound_destroy(void *bound) {
+  STALE_PROBE();
+  delete (PMBound *)bound;
+  return PGM_OK;
+}
+
+}  // extern "C"
