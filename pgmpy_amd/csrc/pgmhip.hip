@@ -2282,7 +2282,10 @@ static int jit_store() {
 // R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
 static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
-  const bool lds = NV * 8 <= 48 * 1024;
+  // CPT values staged in LDS (default) or gathered straight from global memory (knob
+  // PGM_ROWS_JIT_LDS=0: no staging barrier; the values come from L1/L2)
+  static const bool lds_knob = !(getenv("PGM_ROWS_JIT_LDS") && atoi(getenv("PGM_ROWS_JIT_LDS")) == 0);
+  const bool lds = lds_knob && NV * 8 <= 48 * 1024;
   const int WG = jit_wg();
   pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_jit%s(const double *__restrict__ V, "
              "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
