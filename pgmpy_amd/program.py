@@ -33,13 +33,14 @@ class _Rec:
     """One recorded launch of a levelled Program: plain launch, optional batch job, buffers it
     reads / writes (storage keys)."""
 
-    __slots__ = ("fn", "note", "job", "reads", "writes", "level", "pm")
+    __slots__ = ("fn", "note", "job", "reads", "writes", "level", "pm", "nbytes")
 
-    def __init__(self, fn, note, job, reads, writes, pm=None):
+    def __init__(self, fn, note, job, reads, writes, pm=None, nbytes=0):
         self.fn, self.note, self.job = fn, note, job
         self.reads, self.writes = reads, writes
         self.level = 0
         self.pm = pm  # bound specialised product+marginal step (mergeable with its level's others)
+        self.nbytes = nbytes  # algorithmic bytes: every distinct tensor read or written once
 
 
 class _Batch:
@@ -68,6 +69,7 @@ class Program:
         self._handles = []
         self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
+        self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
@@ -112,7 +114,12 @@ class Program:
                 raise RuntimeError("levelled Program: no recording after the first run / capture")
             rk = [k for k in (_key(t) for t in reads if t is not None) if k]
             wk = [k for k in (_key(t) for t in writes if t is not None) if k]
-            self._recs.append(_Rec(fn, note, job, rk, wk, pm))
+            seen, nb = set(), 0
+            for t in list(reads) + list(writes):
+                if t is not None and hasattr(t, "numel") and id(t) not in seen:
+                    seen.add(id(t))
+                    nb += t.numel() * t.element_size()
+            self._recs.append(_Rec(fn, note, job, rk, wk, pm, nb))
         else:
             self._steps.append(fn)
             self.notes.append(note)
@@ -161,6 +168,7 @@ class Program:
                 if r.job is None or len(small) == 1:
                     self._steps.append(r.fn)
                     self.notes.append(r.note)
+                    self.step_bytes.append(r.nbytes)
                     if r.pm is not None:
                         self._pm_launch.append(r.pm)
             if len(small) < 2:
@@ -183,6 +191,7 @@ class Program:
             N.check(L.pgm_batch_finalize(h), "batch_finalize")
             self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
             self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
+            self.step_bytes.append(sum(r.nbytes for r in small))
             self.step_levels.extend([lv] * (len(self._steps) - n0))
 
     def _merge_pm(self, recs):
@@ -205,6 +214,7 @@ class Program:
             self._pm_launch.append(m)
             self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
+            self.step_bytes.append(sum(r.nbytes for r in part))
             done.update(part)
         return done
 

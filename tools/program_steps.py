@@ -74,11 +74,19 @@ def main():
               [big[lv] for lv in range(prog.n_levels)], " batched jobs per level:",
               [small[lv] for lv in range(prog.n_levels)])
     if os.environ.get("LEVELS") and prog._recs:
+        tot_b = 0
         for lv in range(prog.n_levels):
-            mine = [res[i] for i, l in enumerate(prog.step_levels) if l == lv]
-            print(f"-- level {lv}: {len(mine)} launches, {sum(us for us, _ in mine):.1f} us")
-            for us, note in mine:
-                print(f"   {us:8.1f} us  {note[:150]}")
+            idx = [i for i, l in enumerate(prog.step_levels) if l == lv]
+            us_l = sum(res[i][0] for i in idx)
+            b_l = sum(prog.step_bytes[i] for i in idx)
+            tot_b += b_l
+            print(f"-- level {lv}: {len(idx)} launches, {us_l:.1f} us, {b_l / 1e6:.1f} MB, "
+                  f"{b_l / max(us_l, 1e-9) / 1e3:.0f} GB/s")
+            for i in idx:
+                us, note = res[i]
+                print(f"   {us:8.1f} us {prog.step_bytes[i] / 1e6:9.1f} MB {prog.step_bytes[i] / max(us, 1e-9) / 1e3:6.0f} GB/s"
+                      f"  {note[:120]}")
+        print(f"total algorithmic bytes of the steps: {tot_b / 1e6:.1f} MB")
     top = int(os.environ.get("TOP", "25"))
     for us, note in sorted(res, key=lambda r: -r[0])[:top]:
         print(f"{us:9.1f} us  {note[:220] if len(sys.argv) < 4 else note}")
