@@ -658,13 +658,19 @@ def bench_c4(args):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     bpc = bjt.bytes_per_calibration()
+    sch = bjt.schedule(n, ev_vars, "marginalize", False)
+    step_bytes = sum(sch.prog.step_bytes) / n if sch.prog.step_bytes else None
     return {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
             "rows_per_step": n, "ms_per_step": dt * 1e3, "bytes_per_calibration": bpc,
             "achieved_GBps": bpc * n / dt / 1e9, "frac_of_8TBps": bpc * n / dt / 1e9 / HBM_PEAK_GBS,
+            "executed_step_bytes_per_calibration": step_bytes,
+            "executed_step_GBps": step_bytes * n / dt / 1e9 if step_bytes else None,
             "reference_schedule_bytes_per_calibration": bjt.reference_bytes_per_calibration(),
             "note": "bytes_per_calibration: every belief written once + separator messages / sigma' written and "
-                    "read once (this schedule); the reference schedule's figure reads and writes every belief "
-                    "in both passes (SURVEY §8(d) C4)",
+                    "read once (this schedule's floor); executed_step_bytes: the sum over the launched steps of "
+                    "every tensor each reads or writes (operands re-read by the collect and distribute passes, "
+                    "aggregates); the reference schedule's figure reads and writes every belief in both passes "
+                    "(SURVEY §8(d) C4)",
             "cliques": len(bjt.cliques)}
 
 
