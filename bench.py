@@ -430,17 +430,22 @@ def bench_c5(args, dist, rank, world):
     assert plan.kind == "fused", plan.describe()
     d_codes = upload_codes(codes_ev)
     dev = d_codes.device
-    send = torch.zeros((plan.n_acc, block), dtype=torch.float64, device=dev)  # ld = block (padded)
-    out = {"marg": send[:, :rows] if rows else send[:, :1]}
+    want_map = getattr(args, "c5_output", "marginals") == "map"
+    if want_map:  # predict(): the MAP assignment per row, as the plan's int32 flat index
+        send = torch.zeros((1, block), dtype=torch.int32, device=dev)
+        out = {"map": send[0, :rows] if rows else send[0, :1]}
+    else:  # predict_probability(): the [17, rows] marginals, ld = block (padded)
+        send = torch.zeros((plan.n_acc, block), dtype=torch.float64, device=dev)
+        out = {"marg": send[:, :rows] if rows else send[:, :1]}
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
     launcher = Launcher(bound, args.launch)
     nccl = dist is not None and _BACKEND == "nccl"
     recv = None
     if dist is not None and rank == 0:
-        recv = [torch.empty((plan.n_acc, block), dtype=torch.float64, device=dev if nccl else "cpu")
+        recv = [torch.empty(tuple(send.shape), dtype=send.dtype, device=dev if nccl else "cpu")
                 for _ in range(world)]
-    host_send = None if nccl or dist is None else torch.empty((plan.n_acc, block), dtype=torch.float64)
+    host_send = None if nccl or dist is None else torch.empty(tuple(send.shape), dtype=send.dtype)
 
     def gather():
         if dist is None:
@@ -484,7 +489,7 @@ def bench_c5(args, dist, rank, world):
         gather()
     torch.cuda.synchronize()
     gather_ms = max_over_ranks(dist, (time.perf_counter() - g0) * 1e3 / args.steps)
-    bpr = plan.algorithmic_bytes_per_row(marginals=True)
+    bpr = plan.algorithmic_bytes_per_row(marginals=not want_map, map_=want_map)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
     parity = None
     if rank == 0:
@@ -494,13 +499,25 @@ def bench_c5(args, dist, rank, world):
 
         net = load_network("munin")
         got = download(send[:, :min(rows, 16)].contiguous())
-        worst = 0.0
+        worst, wrong, checked = 0.0, 0, 0
         for r in range(got.shape[1]):
             ev = {v: net.states[v][codes_ev[j, r]] for j, v in enumerate(observed)}
-            m = OVE.query(net, variables, ev, joint_out=False)
-            exp = np.concatenate([m[v] for v in plan.variables])
-            worst = max(worst, float(np.max(np.abs(got[:, r] - exp) / np.maximum(np.abs(exp), 1e-300))))
-        parity = {"rows_checked": int(got.shape[1]), "max_rel_err": worst, "ok": worst <= 1e-6}
+            if want_map:
+                mp, gap = OVE.map_query(net, list(plan.variables), ev)
+                if gap <= 1e-9:
+                    continue  # a near-tie may break either way
+                flat = 0
+                for v in plan.variables:
+                    flat = flat * len(net.states[v]) + net.states[v].index(mp[v])
+                wrong += int(got[0, r] != flat)
+                checked += 1
+            else:
+                m = OVE.query(net, variables, ev, joint_out=False)
+                exp = np.concatenate([m[v] for v in plan.variables])
+                worst = max(worst, float(np.max(np.abs(got[:, r] - exp) / np.maximum(np.abs(exp), 1e-300))))
+                checked += 1
+        parity = ({"rows_checked": checked, "map_mismatches": wrong, "ok": wrong == 0} if want_map else
+                  {"rows_checked": checked, "max_rel_err": worst, "ok": worst <= 1e-6})
     return {
         "metric": METRIC,
         "value": total * args.steps / elapsed,
@@ -514,8 +531,10 @@ def bench_c5(args, dist, rank, world):
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))",
-        "config": {"workload": "C5 munin predict_probability template, 1M rows per step sharded over the ranks "
-                               "+ gather of the marginals to rank 0",
+        "config": {"workload": ("C5 munin predict (MAP) template, 1M rows per step sharded over the ranks + gather "
+                                "of the int32 MAP indices to rank 0") if want_map else
+                               ("C5 munin predict_probability template, 1M rows per step sharded over the ranks "
+                                "+ gather of the marginals to rank 0"),
                    "network": "munin", "missing": variables, "global_rows_per_step": total,
                    "launch": args.launch,
                    "rows_per_gpu_per_step": rows, "parallelism": f"rows sharded over {world} rank(s), "
@@ -682,6 +701,8 @@ def main():
     ap.add_argument("--rows", type=int, default=None,
                     help="c3: rows per GPU per step (100,000); c5: rows per step over all GPUs (1,000,000)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c5", "c1", "c2", "c4"])
+    ap.add_argument("--c5-output", default="marginals", choices=["marginals", "map"],
+                    help="c5: gather the fp64 marginals (predict_probability) or the MAP indices (predict)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
