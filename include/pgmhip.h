@@ -172,7 +172,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
  * host-side tests. */
 int pgm_product_n_marginal_source(const pgm_productn_desc *d, const double *const *ops, double *C,
                                   const int64_t *marg_s, int32_t reduce, double *M, char *buf, size_t len);
-/* Compile (hipRTC, distinct sources on parallel threads, code-object disk cache) and load the kernels
+/* Compile (hipRTC, distinct sources, optionally on parallel threads, code-object disk cache) and load the kernels
  * of bound / merged steps that are not loaded yet; a bound step not prepared compiles at its first
  * run.  Call before graph capture. */
 int pgm_pm_prepare(void *const *bounds, int32_t n);

@@ -519,7 +519,8 @@ static hipFunction_t pm_compile(const std::string &src) {
 }
 
 // compile every bound step's kernel that is not loaded yet: distinct sources on up to
-// PGM_RTC_THREADS (default 16) threads, then load the modules
+// PGM_RTC_THREADS threads (default 1: hipRTC serialises compiles internally — pathfinder's 20 kernels
+// take 2.5 s on 1 thread and 2.6 s on 16), then load the modules
 static int pm_prepare(PMBound *const *bs, int n) {
   std::vector<std::string> todo;
   {
@@ -537,7 +538,7 @@ static int pm_prepare(PMBound *const *bs, int n) {
     std::vector<std::vector<char>> codes(todo.size());
     std::vector<char> ok(todo.size(), 0);
     const char *te = getenv("PGM_RTC_THREADS");
-    const size_t nt = std::max<size_t>(1, std::min<size_t>(todo.size(), te ? (size_t)atoi(te) : 16));
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(todo.size(), te ? (size_t)atoi(te) : 1));
     std::atomic<size_t> next(0);
     auto work = [&] {
       for (size_t i; (i = next.fetch_add(1)) < todo.size();)
