@@ -179,6 +179,25 @@ class Launcher:
         return self.q.timer_stop_ms() if self.kind == "direct" else self.timer.stop_ms()
 
 
+def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
+    """Average GPU span per launch of the plan's dispatch floor (PatternPlan.bind(floor=True)) over
+    args.steps launches, launched and timed as the measured kernel; outside the timed region, into
+    its own output buffer.  None when the specialised kernel is not in use."""
+    if plan.kernel_name() != "pgm_rows_jit":
+        return None
+    out = plan.alloc_outputs(rows, marginals=True)
+    fl = launcher_cls(plan.bind(d_codes, rows, 0, rows, out, floor=True), args.launch)
+    for _ in range(max(args.warmup, 1)):
+        fl.run()
+    fl.sync()
+    fl.timer_start()
+    for _ in range(args.steps):
+        fl.run()
+    ms = fl.timer_stop_ms()
+    fl.sync()
+    return ms / args.steps if ms > 0 else None
+
+
 def load_traffic(kernel):
     """HBM bytes/launch from a committed rocprofv3 PMC summary (profiles/pmc_<kernel>.json), if present."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
@@ -336,6 +355,7 @@ def bench_c3(args, dist, rank, world):
         kern_ms = (t_end - t_start) * 1e3 / args.steps
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
+    floor_ms = dispatch_floor_ms(plan, d_codes, rows, args, Launcher)
     kname = plan.kernel_name()
     traffic, traffic_rows = load_traffic(kname)
     if traffic is not None and traffic_rows:
@@ -374,6 +394,11 @@ def bench_c3(args, dist, rank, world):
             "traffic": traffic,
             "kernel": kname,
             "kernel_ms": kern_ms,
+            # the same dispatch with the CPT staging and arithmetic removed (pgm_rows_floor: same grid,
+            # same code loads, same write-through output stores), timed the same way after the timed
+            # region: what one launch of this shape costs before any inference work
+            "dispatch_floor_ms": floor_ms,
+            "kernel_over_floor": (kern_ms / floor_ms) if floor_ms else None,
             "algorithmic_bytes_per_row": bpr,
             "bytes_per_launch": bpr * rows,
         },

@@ -343,7 +343,10 @@ enum pgm_rows_mode {
   PGM_ROWS_VALUES_GLOBAL = 16, /* tuning: read CPT values through L1/L2 instead of staging them in LDS */
   PGM_ROWS_ONE_GROUP = 32,     /* tuning: one 64-row group per workgroup (no staging amortisation) */
   PGM_ROWS_GENERIC = 64,       /* tuning: table-driven kernel even for all-affine plans (testing)  */
-  PGM_ROWS_NO_JIT = 128        /* testing: skip the plan-specialised (hipRTC) kernel, run the AOT ones */
+  PGM_ROWS_NO_JIT = 128,       /* testing: skip the plan-specialised (hipRTC) kernel, run the AOT ones */
+  PGM_ROWS_FLOOR = 256         /* measurement (pgm_rows_plan_bind only): the plan's dispatch floor — same grid,
+                                  same evidence-column loads and output stores as the specialised kernel, no
+                                  CPT staging or arithmetic; the outputs are NOT results */
 };
 
 typedef struct {

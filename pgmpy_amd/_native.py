@@ -35,7 +35,7 @@ ROWS_MAX_EV = 48
 ROWS_MAX_COMP = 12
 ROWS_MAX_MARG = 192
 ROWS_MARGINALS, ROWS_JOINT, ROWS_MAP, ROWS_MAPGAP, ROWS_VALUES_GLOBAL = 1, 2, 4, 8, 16
-ROWS_ONE_GROUP, ROWS_GENERIC, ROWS_NO_JIT = 32, 64, 128
+ROWS_ONE_GROUP, ROWS_GENERIC, ROWS_NO_JIT, ROWS_FLOOR = 32, 64, 128, 256
 
 
 class NativeUnavailable(RuntimeError):

@@ -1715,6 +1715,7 @@ struct RowsHandle {
   hipModule_t jit_mod = nullptr;
   hipFunction_t jit_fn = nullptr;
   hipFunction_t jit_fn2 = nullptr;  // two rows per thread
+  hipFunction_t jit_fn_floor = nullptr;  // PGM_ROWS_FLOOR: the same dispatch's loads + stores only
   std::vector<char> jit_code;         // the compiled code object (the direct AQL path loads it again)
   bool jit_write_through = false;     // its output stores are write-through (jit_store() == 2)
 };
@@ -2417,6 +2418,40 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   }
 }
 
+// the dispatch floor of a plan (PGM_ROWS_FLOOR, measurement only): the one-row kernel's grid, its
+// evidence-column byte loads and its output stores (same addresses, same cache policy), with the CPT
+// staging, gathers and arithmetic replaced by one conversion of the loaded codes
+static void emit_rows_floor(std::string &o, const pgm_rows_plan *pl) {
+  const int WG = jit_wg();
+  pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_floor(const double *__restrict__ V, "
+             "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
+             "double *__restrict__ M, long long ldo, int *__restrict__ MP, double *__restrict__ G, "
+             "int *__restrict__ E, int mode) {\n", WG);
+  pgmi_appendf(o, "  const long long r = (long long)blockIdx.x * %d + threadIdx.x;\n  if (r >= n) return;\n", WG);
+  std::vector<int> cols;
+  for (int j = 0; j < pl->n_ev; ++j)
+    if (std::find(cols.begin(), cols.end(), pl->ev_col[j]) == cols.end()) cols.push_back(pl->ev_col[j]);
+  o += "  unsigned x = 0u;\n";
+  if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + r;\n";
+  for (size_t i = 0; i < cols.size(); ++i) pgmi_appendf(o, "  x += cr[%dLL * ldc];\n", cols[i]);
+  o += "  const double v = (double)x;\n  if (mode & 1) {\n";
+  const bool wt = jit_store() == 2;
+  for (int c = 0; c < pl->n_comp; ++c) {
+    const int lb = pl->comp_loop_begin[c];
+    if (pl->comp_n_query[c] != 1) continue;
+    for (int q = 0; q < pl->loop_card[lb]; ++q) {
+      const int mo = pl->loop_marg_off[lb] + q;
+      if (wt) pgmi_appendf(o, "    PGM_WT8(double, &M[%dLL * ldo + r], v);\n", mo);
+      else pgmi_appendf(o, "    M[%dLL * ldo + r] = v;\n", mo);
+    }
+  }
+  o += "  }\n  if (mode & 12) {\n";
+  if (wt)
+    o += "    if (MP) PGM_WT4(int, &MP[r], (int)x);\n    if ((mode & 8) && G) PGM_WT8(double, &G[r], v);\n  }\n}\n";
+  else
+    o += "    if (MP) MP[r] = (int)x;\n    if ((mode & 8) && G) G[r] = v;\n  }\n}\n";
+}
+
 static std::string rows_jit_source(const pgm_rows_plan *pl) {
   // write-through stores: 4/8 B as relaxed agent-scope atomic stores (global_store ... sc1), 16 B as
   // a buffer store with the sc1 cache bit (element offset into the resource's base, bytes < 2 GiB)
@@ -2431,6 +2466,8 @@ static std::string rows_jit_source(const pgm_rows_plan *pl) {
   emit_rows_kernel(o, pl, 1);
   o += "\n";
   emit_rows_kernel(o, pl, 2);
+  o += "\n";
+  emit_rows_floor(o, pl);
   return o;
 }
 
@@ -2470,7 +2507,8 @@ static bool rows_jit_ready(RowsHandle *h) {
     return false;
   }
   if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess ||
-      hipModuleGetFunction(&h->jit_fn2, h->jit_mod, "pgm_rows_jit2") != hipSuccess) {
+      hipModuleGetFunction(&h->jit_fn2, h->jit_mod, "pgm_rows_jit2") != hipSuccess ||
+      hipModuleGetFunction(&h->jit_fn_floor, h->jit_mod, "pgm_rows_floor") != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -3575,6 +3613,10 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
   STALE_PROBE();
   if (!bound) return fail(PGM_EINVAL, "rows_plan_bind: null output pointer");
   *bound = nullptr;
+  const bool floor = (mode & PGM_ROWS_FLOOR) != 0;
+  mode &= ~PGM_ROWS_FLOOR;
+  if (floor && (mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP)))
+    return fail(PGM_EINVAL, "rows_plan_bind: the floor kernel exists for the specialised kernel's modes only");
   const int st = rows_plan_run(handle, mode, codes, ld_codes, row0, n_rows, marg, joint, ld_out, map, gap, err_flag,
                                stream, true);
   if (st != PGM_OK) return st;
@@ -3598,10 +3640,13 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
   if (n_rows > 0 && h->jit_state > 0 &&
       !(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP))) {
     const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, h->k.n_marg);
-    b->fn = two ? h->jit_fn2 : h->jit_fn;
+    b->fn = floor ? h->jit_fn_floor : two ? h->jit_fn2 : h->jit_fn;
     b->args = RowsJitArgs{h->d_values, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, err_flag, mode, 0};
-    const uint64_t rpb = (uint64_t)jit_wg() * (two ? 2 : 1);
+    const uint64_t rpb = (uint64_t)jit_wg() * (two && !floor ? 2 : 1);
     b->blocks = (unsigned)(((uint64_t)n_rows + rpb - 1) / rpb);
+  } else if (floor) {
+    delete b;
+    return fail(PGM_EINVAL, "rows_plan_bind: the floor kernel needs the plan-specialised (hipRTC) kernel");
   }
   *bound = b;
   return PGM_OK;
@@ -3637,7 +3682,7 @@ int pgmi_rows_bound_jit(void *bound, pgmi_jit_launch *out) {
   if (h->jit_code.empty()) return fail(PGM_EINVAL, "direct launch: no code object kept for this plan");
   out->code = h->jit_code.data();
   out->code_size = h->jit_code.size();
-  out->kernel = b->fn == h->jit_fn2 ? "pgm_rows_jit2" : "pgm_rows_jit";
+  out->kernel = b->fn == h->jit_fn2 ? "pgm_rows_jit2" : b->fn == h->jit_fn_floor ? "pgm_rows_floor" : "pgm_rows_jit";
   out->args = &b->args;
   out->args_size = b->args_size;
   out->blocks = b->blocks;

@@ -335,13 +335,15 @@ class PatternPlan:
                                     N.stream_handle()), "rows_plan_run")
         return out
 
-    def bind(self, codes, ld, row0, n_rows, out, err=None, stream=None):
+    def bind(self, codes, ld, row0, n_rows, out, err=None, stream=None, floor=False):
         """A prepared launch of run() on fixed buffers (pgm_rows_plan_bind): `.run()` re-runs the same
-        pass with one argument-free C call.  Fused plans with marginal / MAP outputs only."""
+        pass with one argument-free C call.  Fused plans with marginal / MAP outputs only.
+        floor=True binds the plan's dispatch floor instead (PGM_ROWS_FLOOR: the same grid, code loads and
+        output stores without the CPT arithmetic) — a measurement, its outputs are not results."""
         if self.kind != "fused" or "joint" in out:
             raise ValueError("bind(): fused plans without a joint output only")
         self._build_fused()
-        return BoundRows(self, codes, ld, row0, n_rows, out, err, stream)
+        return BoundRows(self, codes, ld, row0, n_rows, out, err, stream, floor=floor)
 
     def _dev_factors(self):
         if not hasattr(self, "_dev_cache"):
@@ -541,12 +543,12 @@ class BoundRows:
     """Prepared fused row-plan launch (pgm_rows_plan_bind / pgm_rows_bound_run).  Keeps the plan and
     every buffer alive for as long as the bound handle exists."""
 
-    def __init__(self, plan, codes, ld, row0, n_rows, out, err, stream):
+    def __init__(self, plan, codes, ld, row0, n_rows, out, err, stream, floor=False):
         import ctypes
 
         L = N.lib()
         self._keep = (plan, codes, out, err)
-        mode = plan._mode(out)
+        mode = plan._mode(out) | (N.ROWS_FLOOR if floor else 0)
         ld_out = int(out["marg"].stride(0)) if "marg" in out else int(n_rows)
         h = ctypes.c_void_p()
         N.check(L.pgm_rows_plan_bind(plan._handle, mode, N.ptr(codes), int(ld), int(row0), int(n_rows),

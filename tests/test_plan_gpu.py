@@ -191,6 +191,46 @@ def test_direct_queue_launch_matches_bound(gpu, rows):
     assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
 
 
+def test_dispatch_floor_kernel(gpu):
+    """PGM_ROWS_FLOOR (bench.py's dispatch floor): the floor kernel writes every marginal row with the
+    sum of the plan's distinct evidence codes of that row (the loads and stores the specialised kernel
+    makes, no CPT arithmetic), over both launchers; plans without the specialised kernel refuse it."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import DirectQueue, PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    rows = 5000
+    codes, nodes = forward_sample_codes(m, rows, seed=13)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    cols = [plan.col_of[v] for v in plan.ev_used]
+    expect = ev[cols].astype(np.float64).sum(axis=0)
+    for direct in (False, True):
+        out = plan.alloc_outputs(rows, marginals=True)
+        b = plan.bind(d, rows, 0, rows, out, floor=True)
+        if direct:
+            q = DirectQueue()
+            r = b.direct(q)
+            r.run()
+            q.sync()
+        else:
+            b.run()
+        torch.cuda.synchronize()
+        got = out["marg"].cpu().numpy()
+        for k in range(plan.n_acc):
+            np.testing.assert_array_equal(got[k], expect)
+
+
 def test_direct_queue_needs_specialised_kernel(gpu):
     """A bound launch that runs an AOT kernel (no hipRTC code object) cannot be re-bound to the
     direct queue: ValueError, nothing dispatched."""
