@@ -150,17 +150,53 @@ class Launcher:
     """The timed launch of a bound fused row plan.  "direct" (default): one AQL dispatch packet per
     step on a user-mode HSA queue (pgm_dq_launch; kernel time = the queue's dispatch timestamps
     from the first to the last timed dispatch).  "hip": hipModuleLaunchKernel per step
-    (pgm_rows_bound_run; kernel time = HIP events on the launch stream)."""
+    (pgm_rows_bound_run; kernel time = HIP events on the launch stream).
 
-    def __init__(self, bound, kind):
+    Several bounds (distinct row batches, distinct outputs): step i runs batch i % len(bounds);
+    with group > 1 (direct only) consecutive steps are dispatched `group` at a time as one
+    pgm_dq_launch_group (first packet waits for all earlier work, the others may overlap it)."""
+
+    def __init__(self, bound, kind, group=1):
+        bounds = list(bound) if isinstance(bound, (list, tuple)) else [bound]
         self.kind = kind
+        self.group = max(1, int(group))
+        if self.group > 1 and kind != "direct":
+            raise ValueError("grouped dispatch needs --launch direct")
+        if self.group > len(bounds):
+            raise ValueError(f"group of {self.group} needs as many distinct batches ({len(bounds)} bound)")
         if kind == "direct":
-            self.r = bound.direct()
-            self.q = self.r.queue
+            self.rs = [b.direct() for b in bounds]
+            self.q = self.rs[0].queue
         else:
-            self.r = bound
+            self.rs = bounds
             self.timer = HipTimer()
-        self.run = self.r.run
+        self.r = self.rs[0]
+        self._groups = {}
+        self._next = 0
+
+    def run(self):
+        """One step: the next batch."""
+        self.rs[self._next].run()
+        self._next = (self._next + 1) % len(self.rs)
+
+    def steps(self, k):
+        """k steps, `group` launches per dispatch call when grouped."""
+        if self.group == 1:
+            for _ in range(k):
+                self.run()
+            return
+        from pgmpy_amd.inference.plan import DirectGroup
+
+        n = len(self.rs)
+        while k > 0:
+            g = min(self.group, k)
+            key = (self._next, g)
+            grp = self._groups.get(key)
+            if grp is None:
+                grp = self._groups[key] = DirectGroup([self.rs[(self._next + j) % n] for j in range(g)])
+            grp.run()
+            self._next = (self._next + g) % n
+            k -= g
 
     def sync(self):
         import torch
@@ -187,12 +223,10 @@ def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
         return None
     out = plan.alloc_outputs(rows, marginals=True)
     fl = launcher_cls(plan.bind(d_codes, rows, 0, rows, out, floor=True), args.launch)
-    for _ in range(max(args.warmup, 1)):
-        fl.run()
+    fl.steps(max(args.warmup, 1))
     fl.sync()
     fl.timer_start()
-    for _ in range(args.steps):
-        fl.run()
+    fl.steps(args.steps)
     ms = fl.timer_stop_ms()
     fl.sync()
     return ms / args.steps if ms > 0 else None
@@ -242,7 +276,7 @@ def _cpu_worker(job):
     t0 = time.perf_counter()
     n = 0
     for r in range(w, codes_host.shape[1], W):
-        ev = {v: net.states[v][codes_host[pos[v], r]] for v in obs}
+        ev = {v: net.states[v][codes_host[pos[v], r0 + r]] for v in obs}
         OVE.query(net, list(missing), ev, joint_out=False)
         n += 1
         if time.perf_counter() - t0 > seconds:
@@ -277,8 +311,9 @@ def cpu_baselines_c3(args):
     return single, allcore
 
 
-def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64):
-    """First rows of the device output against the oracle (1e-6 relative, BASELINE.json)."""
+def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64, r0=0):
+    """First rows of the device output (evidence columns r0.. of codes_host) against the oracle
+    (1e-6 relative, BASELINE.json)."""
     from oracle import ve as OVE
     from oracle.network import load_network
     from pgmpy_amd.inference.batch import download
@@ -289,7 +324,7 @@ def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64):
     marg = download(out["marg"])
     worst = 0.0
     for r in range(n_check):
-        ev = {v: net.states[v][codes_host[pos[v], r]] for v in obs}
+        ev = {v: net.states[v][codes_host[pos[v], r0 + r]] for v in obs}
         m = OVE.query(net, list(plan.variables), ev, joint_out=False)
         exp = np.concatenate([m[v] for v in plan.variables])
         got = marg[:, r]
@@ -315,24 +350,26 @@ def bench_c3(args, dist, rank, world):
     missing = set(model.nodes()) - (set(model.nodes()) - set(missing_list))
     variables = list(missing)  # the reference's predict_probability column order (set iteration)
     rows = args.rows
+    nb = max(1, args.batches)  # distinct resident batches, stepped round robin
     t0 = time.perf_counter()
-    codes_all, nodes = forward_sample_codes(model, rows, seed=42 + rank)
+    codes_all, nodes = forward_sample_codes(model, rows * nb, seed=42 + rank)
     observed = [v for v in nodes if v not in missing]
     pos = {v: i for i, v in enumerate(nodes)}
-    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])  # [1038, rows]
+    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])  # [1038, rows * nb]
     col_of = {v: i for i, v in enumerate(observed)}
-    log(f"[rank {rank}] sampled {rows} rows in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] sampled {rows * nb} rows in {time.perf_counter() - t0:.1f}s")
     plan = PatternPlan(model, variables, observed, col_of)
     assert plan.kind == "fused", plan.describe()
     d_codes = upload_codes(codes_ev)
-    out = plan.alloc_outputs(rows, marginals=True)
+    outs = [plan.alloc_outputs(rows, marginals=True) for _ in range(nb)]
+    out = outs[0]
     err = torch.zeros(1, dtype=torch.int32, device=d_codes.device)
-    # one step = one pass of the fused row plan over the resident batch, launched through the
-    # prepared (bound) C-ABI entry: validated and marshalled once, one argument-free call per step
-    bound = plan.bind(d_codes, rows, 0, rows, out, err=err)
-    launcher = Launcher(bound, args.launch)
-    for _ in range(args.warmup):
-        launcher.run()
+    # one step = one pass of the fused row plan over one resident batch (batch i = evidence columns
+    # [i*rows, (i+1)*rows), its own output), launched through the prepared (bound) C-ABI entry:
+    # validated and marshalled once, one argument-free call per step
+    bounds = [plan.bind(d_codes, rows * nb, i * rows, rows, outs[i], err=err) for i in range(nb)]
+    launcher = Launcher(bounds, args.launch, group=args.group)
+    launcher.steps(max(args.warmup, nb))
     launcher.sync()
     barrier(dist)
     # GPU span of the timed dispatches (queue timestamps or HIP events on the launch stream):
@@ -340,8 +377,7 @@ def bench_c3(args, dist, rank, world):
     # kernel time omits
     launcher.timer_start()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        launcher.run()
+    launcher.steps(args.steps)
     kern_ms_total = launcher.timer_stop_ms()
     torch.cuda.synchronize()
     t_end = time.perf_counter()
@@ -382,6 +418,8 @@ def bench_c3(args, dist, rank, world):
             "missing": variables,
             "rows_per_gpu_per_step": rows,
             "global_rows_per_step": rows * world,
+            "batches": nb,
+            "dispatch_group": args.group,
             "parallelism": f"rows sharded over {world} GPU(s), no data-path collective",
             "plan": plan.describe(),
         },
@@ -404,7 +442,13 @@ def bench_c3(args, dist, rank, world):
         },
     }
     if rank == 0:
-        result["parity"] = parity_spot_check(model, missing, plan, out, codes_all, nodes)
+        n_chk = max(16, 64 // nb)
+        checks = [parity_spot_check(model, missing, plan, outs[i], codes_all, nodes, n_check=n_chk, r0=i * rows)
+                  for i in range(nb)]
+        result["parity"] = {"rows_checked": sum(c["rows_checked"] for c in checks),
+                            "batches_checked": nb,
+                            "max_rel_err": max(c["max_rel_err"] for c in checks),
+                            "ok": all(c["ok"] for c in checks)}
         if world == 1 and args.cpu_pre is not None:
             result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
@@ -732,6 +776,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    ap.add_argument("--batches", type=int, default=1,
+                    help="c3: distinct resident row batches (each its own evidence columns and output), "
+                         "stepped round robin")
+    ap.add_argument("--group", type=int, default=1,
+                    help="c3 direct launch: dispatch this many consecutive steps (distinct batches) as one "
+                         "pgm_dq_launch_group (<= --batches)")
     ap.add_argument("--launch", default="direct", choices=["direct", "hip"],
                     help="c3/c5: AQL packets on a user-mode HSA queue (direct) or hipModuleLaunchKernel (hip)")
     args = ap.parse_args()

@@ -412,6 +412,10 @@ int pgm_dq_create(int hip_device, void **dq);
 int pgm_dq_destroy(void *dq);
 int pgm_dq_bind_rows(void *dq, void *bound, void **dbound);
 int pgm_dq_launch(void *dbound);
+/* a group of bound launches on one queue whose outputs are pairwise distinct (independent batches):
+ * the first waits for everything before it (barrier bit), the others may overlap it and each other;
+ * the next launch or sync waits for the whole group.  At most 128 launches, no launch repeated. */
+int pgm_dq_launch_group(void *const *dbounds, int32_t n);
 int pgm_dq_sync(void *dq);
 int pgm_dq_timer_start(void *dq);
 int pgm_dq_timer_stop_ms(void *dq, float *ms);

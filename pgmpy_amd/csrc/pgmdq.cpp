@@ -10,7 +10,11 @@
 //
 // Ordering contract (include/pgmhip.h, pgm_dq_*): pgm_dq_bind_rows drains the device (HIP work that
 // produced the inputs is complete); packets on the queue run in order (barrier bit set: each
-// dispatch waits for the previous one, as kernels on one HIP stream do); inputs may change only
+// dispatch waits for the previous one, as kernels on one HIP stream do) — except inside a group
+// (pgm_dq_launch_group: launches with pairwise distinct outputs, e.g. independent row batches):
+// its first packet carries the barrier bit, the others do not, so the CP starts each member's
+// workgroups while the previous member drains (the per-dispatch launch and drain latency of a
+// 100k-row batch is longer than its HBM time); inputs may change only
 // between pgm_dq_sync and the next launch (the first dispatch after a sync acquires at system
 // scope); pgm_dq_sync issues a system-scope release barrier and waits for it, after which HIP
 // streams may consume the outputs.  Every packet completes an interrupt-free signal from a ring,
@@ -58,6 +62,7 @@ struct DirectQueue {
   bool fresh = true;          // next dispatch is the first since bind/sync
   bool need_release = false;  // dispatches since the last system-scope release
   uint64_t last_kernel = 0;   // index of the last kernel dispatch (timer end)
+  uint64_t group_first = 0;   // first dispatch of the last group (its members may finish in any order)
   std::mutex mu;
   std::atomic<int> queue_error{0};
   // timer: the GPU span from the first dispatch after pgm_dq_timer_start to the last one issued
@@ -283,8 +288,8 @@ static int next_slot(DirectQueue *dq, hsa_signal_t *sig, void **slot, uint64_t *
   return PGM_OK;
 }
 
-static uint32_t header_word(uint16_t type, uint16_t acq, uint16_t rel, uint16_t setup) {
-  const uint16_t h = (uint16_t)((type << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
+static uint32_t header_word(uint16_t type, uint16_t acq, uint16_t rel, uint16_t setup, bool barrier = true) {
+  const uint16_t h = (uint16_t)((type << HSA_PACKET_HEADER_TYPE) | ((barrier ? 1u : 0u) << HSA_PACKET_HEADER_BARRIER) |
                                 (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                 (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   return (uint32_t)h | ((uint32_t)setup << 16);
@@ -294,6 +299,17 @@ static void publish(DirectQueue *dq, void *slot, uint32_t header, uint64_t idx) 
   __atomic_store_n((uint32_t *)slot, header, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(dq->q->doorbell_signal, (hsa_signal_value_t)idx);
   dq->issued += 1;
+}
+
+// wait for every dispatch from the last group's first member on (members without the barrier bit
+// may complete out of order; everything before the group completed before it started)
+static int wait_tail(DirectQueue *dq) {
+  const uint64_t from = std::max(dq->group_first, dq->issued >= kRing ? dq->issued - kRing : 0);
+  for (uint64_t i = from; i < dq->issued; ++i) {
+    const int rc = wait_zero(dq, dq->ring[i % kRing]);
+    if (rc != PGM_OK) return rc;
+  }
+  return PGM_OK;
 }
 
 extern "C" int pgm_dq_sync(void *handle) {
@@ -317,7 +333,7 @@ extern "C" int pgm_dq_sync(void *handle) {
     dq->need_release = false;
   }
   dq->fresh = true;
-  return wait_zero(dq, dq->ring[(dq->issued - 1) % kRing]);
+  return wait_tail(dq);
 }
 
 int pgm_dq_destroy(void *handle) {
@@ -394,11 +410,9 @@ int pgm_dq_bind_rows(void *handle, void *bound, void **out) {
   return PGM_OK;
 }
 
-int pgm_dq_launch(void *dbound) {
-  DirectBound *db = (DirectBound *)dbound;
-  if (!db) return fail(PGM_EINVAL, "dq_launch: null handle");
+// one kernel-dispatch packet of a bound launch (caller holds dq->mu)
+static int dispatch(DirectBound *db, bool barrier) {
   DirectQueue *dq = db->dq;
-  std::lock_guard<std::mutex> lk(dq->mu);
   hsa_signal_t sig;
   void *slot;
   uint64_t idx;
@@ -422,8 +436,36 @@ int pgm_dq_launch(void *dbound) {
   dq->fresh = false;
   dq->need_release = dq->need_release || db->rel_scope != HSA_FENCE_SCOPE_SYSTEM;
   dq->last_kernel = dq->issued;
+  if (barrier) dq->group_first = dq->issued;
   publish(dq, slot, header_word(HSA_PACKET_TYPE_KERNEL_DISPATCH, acq, db->rel_scope,
-                                (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS)), idx);
+                                (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS), barrier), idx);
+  return PGM_OK;
+}
+
+int pgm_dq_launch(void *dbound) {
+  DirectBound *db = (DirectBound *)dbound;
+  if (!db) return fail(PGM_EINVAL, "dq_launch: null handle");
+  std::lock_guard<std::mutex> lk(db->dq->mu);
+  return dispatch(db, true);
+}
+
+int pgm_dq_launch_group(void *const *dbounds, int32_t n) {
+  if (!dbounds || n <= 0) return fail(PGM_EINVAL, "dq_launch_group: empty group");
+  if (n > (int32_t)(kRing / 2)) return fail(PGM_EINVAL, "dq_launch_group: %d launches > %d per group", n, (int)(kRing / 2));
+  DirectQueue *dq = nullptr;
+  for (int32_t i = 0; i < n; ++i) {
+    const DirectBound *db = (const DirectBound *)dbounds[i];
+    if (!db) return fail(PGM_EINVAL, "dq_launch_group: null handle at %d", i);
+    if (dq && db->dq != dq) return fail(PGM_EINVAL, "dq_launch_group: launches bound to different queues");
+    dq = db->dq;
+    for (int32_t j = 0; j < i; ++j)
+      if (dbounds[j] == dbounds[i]) return fail(PGM_EINVAL, "dq_launch_group: launch %d repeats launch %d", i, j);
+  }
+  std::lock_guard<std::mutex> lk(dq->mu);
+  for (int32_t i = 0; i < n; ++i) {
+    const int rc = dispatch((DirectBound *)dbounds[i], i == 0);
+    if (rc != PGM_OK) return rc;
+  }
   return PGM_OK;
 }
 
@@ -445,17 +487,22 @@ int pgm_dq_timer_stop_ms(void *handle, float *ms) {
   if (!dq->timing) return fail(PGM_EINVAL, "dq_timer_stop: timer not started");
   dq->timing = false;
   if (dq->issued == dq->t_first) return PGM_OK;  // nothing dispatched in the span
-  int rc = wait_zero(dq, dq->ring[(dq->issued - 1) % kRing]);
+  int rc = wait_tail(dq);
   if (rc != PGM_OK || !dq->profiling) return rc;
-  const hsa_signal_t last = dq->ring[dq->last_kernel % kRing];
-  hsa_amd_profiling_dispatch_time_t te;
-  HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, last, &te));
+  // the span ends with the latest end among the last group's members (up to the last kernel)
+  hsa_amd_profiling_dispatch_time_t te{};
+  const uint64_t from = std::max(std::max(dq->group_first, dq->t_first), dq->issued >= kRing ? dq->issued - kRing + 1 : 0);
+  for (uint64_t i = from; i <= dq->last_kernel; ++i) {
+    hsa_amd_profiling_dispatch_time_t t;
+    HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
+    te.end = std::max(te.end, t.end);
+  }
   if (!dq->have_start) {
     hsa_amd_profiling_dispatch_time_t ts;
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[dq->t_first % kRing], &ts));
     dq->start_ticks = ts.start;
   }
-  *ms = (float)((double)(te.end - dq->start_ticks) * 1e3 / (double)dq->freq);
+  *ms = te.end > dq->start_ticks ? (float)((double)(te.end - dq->start_ticks) * 1e3 / (double)dq->freq) : 0.f;
   return PGM_OK;
 }
 

@@ -627,6 +627,38 @@ class DirectQueue:
                 pass
 
 
+class DirectGroup:
+    """Bound launches on one DirectQueue whose outputs are pairwise distinct (independent row
+    batches), dispatched together by pgm_dq_launch_group: the first packet waits for all earlier
+    work, the others may overlap it, so one batch's workgroups start while the previous drains."""
+
+    def __init__(self, members):
+        import ctypes
+
+        members = list(members)
+        if not members:
+            raise ValueError("DirectGroup: no launches")
+        q = members[0].queue
+        if any(m.queue is not q for m in members):
+            raise ValueError("DirectGroup: launches bound to different queues")
+        outs = [t.data_ptr() for m in members for t in m.out.values()]
+        if len(set(outs)) != len(outs):
+            raise ValueError("DirectGroup: launches share an output buffer")
+        self._keep = members
+        self.queue = q
+        self._arr = (ctypes.c_void_p * len(members))(*[m._h.value for m in members])
+        self._n = len(members)
+        self._launch = N.lib().pgm_dq_launch_group
+
+    def run(self):
+        st = self._launch(self._arr, self._n)
+        if st != 0:
+            N.check(st, "dq_launch_group")
+
+    def sync(self):
+        self.queue.sync()
+
+
 class DirectRows:
     """A bound row-plan launch re-bound to a DirectQueue (pgm_dq_bind_rows / pgm_dq_launch)."""
 

@@ -225,8 +225,11 @@ def test_specialised_row_kernel_source_compiles_for_gfx950():
     plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
     assert plan.kernel_name() == "pgm_rows_jit"
     src = plan.specialised_source()
-    assert src.count("M[") == plan.n_acc == 17
-    assert src.count("cr[") == 7  # the template's 7 evidence columns
+    one_row = src[:src.index("pgm_rows_jit2(")]
+    assert one_row.count("M[") == plan.n_acc == 17
+    assert one_row.count("cr[") == 7  # the template's 7 evidence columns
+    floor = src[src.index("pgm_rows_floor("):]  # the dispatch floor: same loads and stores, no CPT math
+    assert floor.count("M[") == 17 and floor.count("cr[") == 7 and "S[" not in floor
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")

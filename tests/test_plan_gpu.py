@@ -191,6 +191,62 @@ def test_direct_queue_launch_matches_bound(gpu, rows):
     assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
 
 
+def test_direct_group_launch_matches_bound(gpu):
+    """pgm_dq_launch_group (independent row batches dispatched with only the first packet carrying
+    the barrier bit): after many groups every batch's output equals its own HIP-launched bound run
+    bit for bit, the timer spans the group, sync waits for all members; a group that repeats a
+    launch or shares an output buffer is refused."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import DirectGroup, DirectQueue, PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    rows, nb = 100_000, 4
+    codes, nodes = forward_sample_codes(m, rows * nb, seed=21)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    refs, outs, bounds = [], [], []
+    for i in range(nb):
+        ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+        plan.bind(d, rows * nb, i * rows, rows, ref).run()
+        refs.append(ref)
+        out = plan.alloc_outputs(rows, marginals=True, map_=True)
+        outs.append(out)
+        bounds.append(plan.bind(d, rows * nb, i * rows, rows, out))
+    torch.cuda.synchronize()
+    q = DirectQueue()
+    rs = [b.direct(q) for b in bounds]
+    grp = DirectGroup(rs)
+    q.timer_start()
+    for _ in range(100):  # 400 dispatches: the signal ring wraps mid-group
+        grp.run()
+    ms = q.timer_stop_ms()
+    q.sync()
+    assert ms > 0.0
+    for out, ref in zip(outs, refs):
+        assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    for o in outs:
+        o["marg"].zero_()
+    torch.cuda.synchronize()
+    grp.run()
+    q.sync()
+    for out, ref in zip(outs, refs):
+        assert torch.equal(out["marg"], ref["marg"])
+    with pytest.raises(ValueError):
+        DirectGroup([rs[0], rs[0]])
+    with pytest.raises(ValueError):
+        DirectGroup([rs[0], plan.bind(d, rows * nb, rows, rows, outs[0]).direct(q)])
+
+
 def test_dispatch_floor_kernel(gpu):
     """PGM_ROWS_FLOOR (bench.py's dispatch floor): the floor kernel writes every marginal row with the
     sum of the plan's distinct evidence codes of that row (the loads and stores the specialised kernel
