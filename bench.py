@@ -156,17 +156,25 @@ class Launcher:
     with group > 1 (direct only) consecutive steps are dispatched `group` at a time as one
     pgm_dq_launch_group (first packet waits for all earlier work, the others may overlap it)."""
 
-    def __init__(self, bound, kind, group=1):
+    def __init__(self, bound, kind, group=1, queues=1):
         bounds = list(bound) if isinstance(bound, (list, tuple)) else [bound]
         self.kind = kind
         self.group = max(1, int(group))
-        if self.group > 1 and kind != "direct":
-            raise ValueError("grouped dispatch needs --launch direct")
-        if self.group > len(bounds):
-            raise ValueError(f"group of {self.group} needs as many distinct batches ({len(bounds)} bound)")
+        queues = max(1, int(queues))
+        if (self.group > 1 or queues > 1) and kind != "direct":
+            raise ValueError("grouped / multi-queue dispatch needs --launch direct")
+        if self.group > 1 and queues > 1:
+            raise ValueError("--group and --queues are separate experiments")
+        if max(self.group, queues) > len(bounds):
+            raise ValueError(f"group / queues of {max(self.group, queues)} need as many distinct batches "
+                             f"({len(bounds)} bound)")
         if kind == "direct":
-            self.rs = [b.direct() for b in bounds]
-            self.q = self.rs[0].queue
+            from pgmpy_amd.inference.plan import DirectQueue
+
+            # batch i on queue i % queues (queue 0: the process's default queue)
+            self.qs = [DirectQueue.default()] + [DirectQueue() for _ in range(queues - 1)]
+            self.rs = [b.direct(self.qs[i % queues]) for i, b in enumerate(bounds)]
+            self.q = self.qs[0]
         else:
             self.rs = bounds
             self.timer = HipTimer()
@@ -202,17 +210,27 @@ class Launcher:
         import torch
 
         if self.kind == "direct":
-            self.q.sync()
+            for q in self.qs:
+                q.sync()
         torch.cuda.synchronize()
 
     def timer_start(self):
         if self.kind == "direct":
-            self.q.timer_start()
+            for q in self.qs:
+                q.timer_start()
         else:
             self.timer.start()
 
     def timer_stop_ms(self):
-        return self.q.timer_stop_ms() if self.kind == "direct" else self.timer.stop_ms()
+        if self.kind != "direct":
+            return self.timer.stop_ms()
+        if len(self.qs) == 1:
+            return self.q.timer_stop_ms()
+        spans = [q.timer_stop_ticks() for q in self.qs]  # one HSA system clock for every queue
+        spans = [(a, b, f) for a, b, f in spans if b > a]
+        if not spans:
+            return 0.0
+        return (max(b for _, b, _ in spans) - min(a for a, _, _ in spans)) * 1e3 / spans[0][2]
 
 
 def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
@@ -230,6 +248,33 @@ def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
     ms = fl.timer_stop_ms()
     fl.sync()
     return ms / args.steps if ms > 0 else None
+
+
+def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, n_out=24, steps=200):
+    """The C3 launch streamed over n_out distinct output buffers (n_out x 13.6 MB > the 256 MiB MALL, so
+    the outputs of a step are evicted to HBM before the buffer comes round again) on args.queues
+    queues; inputs cycle over the nb resident batches (0.7 MB read per launch).  Average GPU span per
+    launch over `steps` launches, outside the timed region; the bytes / span are an HBM rate."""
+    import torch
+
+    outs = [plan.alloc_outputs(rows, marginals=True) for _ in range(n_out)]
+    bounds = [plan.bind(d_codes, rows * nb, (i % nb) * rows, rows, outs[i], err=err) for i in range(n_out)]
+    q = max(1, args.queues)
+    ln = Launcher(bounds, "direct", queues=min(q, n_out))
+    ln.steps(n_out)
+    ln.sync()
+    ln.timer_start()
+    ln.steps(steps)
+    ms = ln.timer_stop_ms()
+    ln.sync()
+    same = all(torch.equal(outs[i]["marg"], outs[i % nb]["marg"]) for i in range(nb, n_out, 5))
+    bpl = plan.algorithmic_bytes_per_row(marginals=True) * rows
+    kms = ms / steps
+    ach = bpl / (kms * 1e-3) / 1e9 if kms > 0 else None
+    del ln, bounds, outs
+    return {"output_buffers": n_out, "queues": min(q, n_out), "steps": steps,
+            "working_set_bytes": bpl * n_out, "kernel_ms": kms, "achieved": ach,
+            "frac": ach / HBM_PEAK_GBS if ach else None, "outputs_match_resident_batches": same}
 
 
 def load_traffic(kernel):
@@ -276,7 +321,7 @@ def _cpu_worker(job):
     t0 = time.perf_counter()
     n = 0
     for r in range(w, codes_host.shape[1], W):
-        ev = {v: net.states[v][codes_host[pos[v], r0 + r]] for v in obs}
+        ev = {v: net.states[v][codes_host[pos[v], r]] for v in obs}
         OVE.query(net, list(missing), ev, joint_out=False)
         n += 1
         if time.perf_counter() - t0 > seconds:
@@ -352,12 +397,18 @@ def bench_c3(args, dist, rank, world):
     rows = args.rows
     nb = max(1, args.batches)  # distinct resident batches, stepped round robin
     t0 = time.perf_counter()
-    codes_all, nodes = forward_sample_codes(model, rows * nb, seed=42 + rank)
+    codes_all, nodes = forward_sample_codes(model, rows, seed=42 + rank)
     observed = [v for v in nodes if v not in missing]
     pos = {v: i for i, v in enumerate(nodes)}
-    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])  # [1038, rows * nb]
+    codes_one = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])  # [1038, rows]
+    # batch 0 = the sampled rows; batch i > 0 = a seeded row permutation of them (distinct inputs and
+    # outputs per batch without re-running the sampler)
+    prng = np.random.default_rng(1000 + rank)
+    perms = [np.arange(rows)] + [prng.permutation(rows) for _ in range(nb - 1)]
+    codes_ev = np.concatenate([codes_one[:, p] for p in perms], axis=1) if nb > 1 else codes_one  # [1038, rows * nb]
+    del codes_one
     col_of = {v: i for i, v in enumerate(observed)}
-    log(f"[rank {rank}] sampled {rows * nb} rows in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] sampled {rows} rows, {nb} batch(es), in {time.perf_counter() - t0:.1f}s")
     plan = PatternPlan(model, variables, observed, col_of)
     assert plan.kind == "fused", plan.describe()
     d_codes = upload_codes(codes_ev)
@@ -368,7 +419,8 @@ def bench_c3(args, dist, rank, world):
     # [i*rows, (i+1)*rows), its own output), launched through the prepared (bound) C-ABI entry:
     # validated and marshalled once, one argument-free call per step
     bounds = [plan.bind(d_codes, rows * nb, i * rows, rows, outs[i], err=err) for i in range(nb)]
-    launcher = Launcher(bounds, args.launch, group=args.group)
+    nq = args.queues if args.launch == "direct" else 1
+    launcher = Launcher(bounds, args.launch, group=args.group, queues=nq)
     launcher.steps(max(args.warmup, nb))
     launcher.sync()
     barrier(dist)
@@ -392,6 +444,7 @@ def bench_c3(args, dist, rank, world):
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
     floor_ms = dispatch_floor_ms(plan, d_codes, rows, args, Launcher)
+    stream = hbm_stream_roofline(plan, d_codes, rows, nb, args, err) if args.launch == "direct" else None
     kname = plan.kernel_name()
     traffic, traffic_rows = load_traffic(kname)
     if traffic is not None and traffic_rows:
@@ -411,8 +464,9 @@ def bench_c3(args, dist, rank, world):
         "data": "synthetic (forward-sampled munin evidence rows, seed 42+rank)",
         "config": {
             "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, "
-                        "fused row plan (pgm_rows_plan_bind; one launch per step)",
-            "launch": {"direct": "AQL packet on a user-mode HSA queue (pgm_dq_launch)",
+                        "fused row plan (pgm_rows_plan_bind; one launch per step: one 100k-row batch, "
+                        "batches resident in HBM and stepped round robin over the queues)",
+            "launch": {"direct": "AQL packet on user-mode HSA queues (pgm_dq_launch; batch i on queue i % queues)",
                        "hip": "hipModuleLaunchKernel (pgm_rows_bound_run)"}[args.launch],
             "network": "munin",
             "missing": variables,
@@ -420,6 +474,7 @@ def bench_c3(args, dist, rank, world):
             "global_rows_per_step": rows * world,
             "batches": nb,
             "dispatch_group": args.group,
+            "queues": nq,
             "parallelism": f"rows sharded over {world} GPU(s), no data-path collective",
             "plan": plan.describe(),
         },
@@ -439,12 +494,21 @@ def bench_c3(args, dist, rank, world):
             "kernel_over_floor": (kern_ms / floor_ms) if floor_ms else None,
             "algorithmic_bytes_per_row": bpr,
             "bytes_per_launch": bpr * rows,
+            # kernel_ms is the GPU span per step; with Q queues up to Q launches run at once, so the
+            # achieved rate is the launches' aggregate bytes over the span (a single dispatch's own
+            # duration, rocprofv3's per-kernel time, is longer by up to the overlap)
+            "concurrent_queues": nq,
+            # the batches' outputs + inputs (algorithmic bytes): <= 256 MiB stays in the MI355X
+            # Infinity Cache (MALL) between the steps that rewrite it; hbm_stream repeats the
+            # measurement over a batch set larger than the MALL (every output line goes to HBM)
+            "working_set_bytes": bpr * rows * nb,
+            "hbm_stream": stream,
         },
     }
     if rank == 0:
         n_chk = max(16, 64 // nb)
-        checks = [parity_spot_check(model, missing, plan, outs[i], codes_all, nodes, n_check=n_chk, r0=i * rows)
-                  for i in range(nb)]
+        checks = [parity_spot_check(model, missing, plan, outs[i], codes_all[:, perms[i][:n_chk]], nodes,
+                                    n_check=n_chk) for i in range(nb)]
         result["parity"] = {"rows_checked": sum(c["rows_checked"] for c in checks),
                             "batches_checked": nb,
                             "max_rel_err": max(c["max_rel_err"] for c in checks),
@@ -776,12 +840,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
-    ap.add_argument("--batches", type=int, default=1,
+    ap.add_argument("--batches", type=int, default=4,
                     help="c3: distinct resident row batches (each its own evidence columns and output), "
                          "stepped round robin")
     ap.add_argument("--group", type=int, default=1,
                     help="c3 direct launch: dispatch this many consecutive steps (distinct batches) as one "
                          "pgm_dq_launch_group (<= --batches)")
+    ap.add_argument("--queues", type=int, default=4,
+                    help="c3 direct launch: spread the batches over this many user-mode HSA queues "
+                         "(batch i on queue i %% Q; <= --batches)")
     ap.add_argument("--launch", default="direct", choices=["direct", "hip"],
                     help="c3/c5: AQL packets on a user-mode HSA queue (direct) or hipModuleLaunchKernel (hip)")
     args = ap.parse_args()

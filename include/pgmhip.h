@@ -419,6 +419,9 @@ int pgm_dq_launch_group(void *const *dbounds, int32_t n);
 int pgm_dq_sync(void *dq);
 int pgm_dq_timer_start(void *dq);
 int pgm_dq_timer_stop_ms(void *dq, float *ms);
+/* the same span as raw HSA system timestamps (start of the first timed dispatch, latest end) and their
+ * frequency, so spans of several queues can be joined */
+int pgm_dq_timer_stop_ticks(void *dq, uint64_t *start, uint64_t *end, uint64_t *freq);
 int pgm_dq_bound_destroy(void *dbound);
 
 #ifdef __cplusplus

@@ -480,9 +480,19 @@ int pgm_dq_timer_start(void *handle) {
 }
 
 int pgm_dq_timer_stop_ms(void *handle, float *ms) {
-  DirectQueue *dq = (DirectQueue *)handle;
-  if (!dq || !ms) return fail(PGM_EINVAL, "dq_timer_stop: null argument");
+  if (!ms) return fail(PGM_EINVAL, "dq_timer_stop: null argument");
   *ms = 0.f;
+  uint64_t t0 = 0, t1 = 0, f = 1;
+  const int rc = pgm_dq_timer_stop_ticks(handle, &t0, &t1, &f);
+  if (rc == PGM_OK && t1 > t0) *ms = (float)((double)(t1 - t0) * 1e3 / (double)f);
+  return rc;
+}
+
+int pgm_dq_timer_stop_ticks(void *handle, uint64_t *start, uint64_t *end, uint64_t *freq) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq || !start || !end || !freq) return fail(PGM_EINVAL, "dq_timer_stop: null argument");
+  *start = *end = 0;
+  *freq = dq->freq;
   std::lock_guard<std::mutex> lk(dq->mu);
   if (!dq->timing) return fail(PGM_EINVAL, "dq_timer_stop: timer not started");
   dq->timing = false;
@@ -502,7 +512,8 @@ int pgm_dq_timer_stop_ms(void *handle, float *ms) {
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[dq->t_first % kRing], &ts));
     dq->start_ticks = ts.start;
   }
-  *ms = te.end > dq->start_ticks ? (float)((double)(te.end - dq->start_ticks) * 1e3 / (double)dq->freq) : 0.f;
+  *start = dq->start_ticks;
+  *end = te.end > dq->start_ticks ? te.end : dq->start_ticks;
   return PGM_OK;
 }
 

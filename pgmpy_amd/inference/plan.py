@@ -618,6 +618,15 @@ class DirectQueue:
         N.check(N.lib().pgm_dq_timer_stop_ms(self._h, ctypes.byref(ms)), "dq_timer_stop")
         return float(ms.value)
 
+    def timer_stop_ticks(self):
+        """(start, end, ticks per second) of the timed span (pgm_dq_timer_stop_ticks)."""
+        import ctypes
+
+        a, b, f = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().pgm_dq_timer_stop_ticks(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(f)),
+                "dq_timer_stop")
+        return a.value, b.value, f.value
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 11
+    assert lib.pgm_version() == 12
 
 
 def test_struct_layouts_match_header():
@@ -348,3 +348,17 @@ def test_product_marginal_specialised_source_compiles(tmp_path, red, store, rati
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-c", str(f), "-o",
                         str(tmp_path / "pm.o")], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_bench_cpu_baselines_run():
+    """bench.py's cpu_baseline legs (numpy oracle, 1 core and the worker pool) run on a small sample
+    and report positive rates (the bench line carries them; no GPU involved)."""
+    import argparse
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    one, allcore = bench.cpu_baselines_c3(argparse.Namespace(rows=300, cpu_seconds=0.5))
+    assert one["value"] > 0 and one["cores"] == 1 and one["kind"] == "port"
+    assert allcore["value"] > 0 and allcore["cores"] >= 1

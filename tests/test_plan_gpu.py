@@ -247,6 +247,51 @@ def test_direct_group_launch_matches_bound(gpu):
         DirectGroup([rs[0], plan.bind(d, rows * nb, rows, rows, outs[0]).direct(q)])
 
 
+def test_direct_queues_in_parallel(gpu):
+    """Independent row batches on separate user-mode queues (bench.py --queues): every batch's
+    output equals its HIP-launched bound run after interleaved dispatches; the joined tick spans of
+    the queues are ordered and share one clock."""
+    import random
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import DirectQueue, PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    rows, nq = 50_000, 3
+    codes, nodes = forward_sample_codes(m, rows * nq, seed=23)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    plan = PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)})
+    d = upload_codes(ev)
+    qs = [DirectQueue() for _ in range(nq)]
+    refs, outs, rs = [], [], []
+    for i in range(nq):
+        ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+        plan.bind(d, rows * nq, i * rows, rows, ref).run()
+        refs.append(ref)
+        out = plan.alloc_outputs(rows, marginals=True, map_=True)
+        outs.append(out)
+        rs.append(plan.bind(d, rows * nq, i * rows, rows, out).direct(qs[i]))
+    torch.cuda.synchronize()
+    for q in qs:
+        q.timer_start()
+    for _ in range(50):
+        for r in rs:
+            r.run()
+    spans = [q.timer_stop_ticks() for q in qs]
+    for q in qs:
+        q.sync()
+    assert all(b > a > 0 for a, b, _ in spans) and len({f for _, _, f in spans}) == 1
+    for out, ref in zip(outs, refs):
+        assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+
+
 def test_dispatch_floor_kernel(gpu):
     """PGM_ROWS_FLOOR (bench.py's dispatch floor): the floor kernel writes every marginal row with the
     sum of the plan's distinct evidence codes of that row (the loads and stores the specialised kernel
