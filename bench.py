@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache (memory-side last-level cache)
 METRIC = "evidence-batched marginal queries/sec on munin; achieved HBM GB/s vs peak"
 
 
@@ -156,7 +157,7 @@ class Launcher:
     with group > 1 (direct only) consecutive steps are dispatched `group` at a time as one
     pgm_dq_launch_group (first packet waits for all earlier work, the others may overlap it)."""
 
-    def __init__(self, bound, kind, group=1, queues=1):
+    def __init__(self, bound, kind, group=1, queues=1, qs=None):
         bounds = list(bound) if isinstance(bound, (list, tuple)) else [bound]
         self.kind = kind
         self.group = max(1, int(group))
@@ -171,8 +172,13 @@ class Launcher:
         if kind == "direct":
             from pgmpy_amd.inference.plan import DirectQueue
 
-            # batch i on queue i % queues (queue 0: the process's default queue)
-            self.qs = [DirectQueue.default()] + [DirectQueue() for _ in range(queues - 1)]
+            # batch i on queue i % queues (queue 0: the process's default queue); reuse `qs` when given:
+            # every extra user-mode queue costs a hardware queue slot, and past the slots the GPU
+            # scheduler time-slices the queues (8 queues: 2x slower than 4, profiles/r02bd_*)
+            if qs is not None:
+                self.qs = list(qs)[:queues]
+            else:
+                self.qs = [DirectQueue.default()] + [DirectQueue() for _ in range(queues - 1)]
             self.rs = [b.direct(self.qs[i % queues]) for i, b in enumerate(bounds)]
             self.q = self.qs[0]
         else:
@@ -214,6 +220,18 @@ class Launcher:
                 q.sync()
         torch.cuda.synchronize()
 
+    def wait(self):
+        """End of a timed region: every launch issued so far has completed (direct queues: their
+        completion signals; HIP: the device)."""
+        import torch
+
+        if self.kind == "direct":
+            for q in self.qs:
+                q.wait()
+        else:  # the end event goes on the stream right after the last launch
+            self._hip_ms = self.timer.stop_ms()
+        torch.cuda.synchronize()
+
     def timer_start(self):
         if self.kind == "direct":
             for q in self.qs:
@@ -223,7 +241,8 @@ class Launcher:
 
     def timer_stop_ms(self):
         if self.kind != "direct":
-            return self.timer.stop_ms()
+            ms, self._hip_ms = getattr(self, "_hip_ms", None), None
+            return ms if ms is not None else self.timer.stop_ms()
         if len(self.qs) == 1:
             return self.q.timer_stop_ms()
         spans = [q.timer_stop_ticks() for q in self.qs]  # one HSA system clock for every queue
@@ -250,7 +269,7 @@ def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
     return ms / args.steps if ms > 0 else None
 
 
-def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, n_out=24, steps=200):
+def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, qs, n_out=24, steps=200):
     """The C3 launch streamed over n_out distinct output buffers (n_out x 13.6 MB > the 256 MiB MALL, so
     the outputs of a step are evicted to HBM before the buffer comes round again) on args.queues
     queues; inputs cycle over the nb resident batches (0.7 MB read per launch).  Average GPU span per
@@ -260,7 +279,7 @@ def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, n_out=24, steps=200)
     outs = [plan.alloc_outputs(rows, marginals=True) for _ in range(n_out)]
     bounds = [plan.bind(d_codes, rows * nb, (i % nb) * rows, rows, outs[i], err=err) for i in range(n_out)]
     q = max(1, args.queues)
-    ln = Launcher(bounds, "direct", queues=min(q, n_out))
+    ln = Launcher(bounds, "direct", queues=min(q, n_out), qs=qs)
     ln.steps(n_out)
     ln.sync()
     ln.timer_start()
@@ -430,9 +449,10 @@ def bench_c3(args, dist, rank, world):
     launcher.timer_start()
     t_start = time.perf_counter()
     launcher.steps(args.steps)
-    kern_ms_total = launcher.timer_stop_ms()
-    torch.cuda.synchronize()
+    launcher.wait()  # every step's dispatch complete (+ torch.cuda.synchronize)
     t_end = time.perf_counter()
+    kern_ms_total = launcher.timer_stop_ms()  # dispatch timestamps, read after the timed region
+    launcher.sync()
     barrier(dist)
     elapsed = max_over_ranks(dist, t_end - t_start)
     assert int(err.item()) == 0
@@ -444,7 +464,10 @@ def bench_c3(args, dist, rank, world):
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
     floor_ms = dispatch_floor_ms(plan, d_codes, rows, args, Launcher)
-    stream = hbm_stream_roofline(plan, d_codes, rows, nb, args, err) if args.launch == "direct" else None
+    working_set = bpr * rows * nb
+    stream = None
+    if args.launch == "direct" and working_set <= MALL_BYTES:
+        stream = hbm_stream_roofline(plan, d_codes, rows, nb, args, err, launcher.qs)
     kname = plan.kernel_name()
     traffic, traffic_rows = load_traffic(kname)
     if traffic is not None and traffic_rows:
@@ -498,10 +521,12 @@ def bench_c3(args, dist, rank, world):
             # achieved rate is the launches' aggregate bytes over the span (a single dispatch's own
             # duration, rocprofv3's per-kernel time, is longer by up to the overlap)
             "concurrent_queues": nq,
-            # the batches' outputs + inputs (algorithmic bytes): <= 256 MiB stays in the MI355X
-            # Infinity Cache (MALL) between the steps that rewrite it; hbm_stream repeats the
-            # measurement over a batch set larger than the MALL (every output line goes to HBM)
-            "working_set_bytes": bpr * rows * nb,
+            # the batches' outputs + inputs (algorithmic bytes): the default 24 batches (343 MB) exceed
+            # the MI355X's 256 MiB Infinity Cache (MALL), so a step's output lines are evicted to HBM
+            # before its buffer comes round again and the achieved rate is an HBM rate; with a set
+            # that fits (--batches <= 17) hbm_stream repeats the measurement over 24 output buffers
+            "working_set_bytes": working_set,
+            "working_set_exceeds_mall": working_set > MALL_BYTES,
             "hbm_stream": stream,
         },
     }
@@ -840,7 +865,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
-    ap.add_argument("--batches", type=int, default=4,
+    ap.add_argument("--batches", type=int, default=24,
                     help="c3: distinct resident row batches (each its own evidence columns and output), "
                          "stepped round robin")
     ap.add_argument("--group", type=int, default=1,

@@ -417,6 +417,9 @@ int pgm_dq_launch(void *dbound);
  * the next launch or sync waits for the whole group.  At most 128 launches, no launch repeated. */
 int pgm_dq_launch_group(void *const *dbounds, int32_t n);
 int pgm_dq_sync(void *dq);
+/* wait until every dispatch issued on the queue has completed (no release barrier: call pgm_dq_sync
+ * before HIP work reads the outputs) */
+int pgm_dq_wait(void *dq);
 int pgm_dq_timer_start(void *dq);
 int pgm_dq_timer_stop_ms(void *dq, float *ms);
 /* the same span as raw HSA system timestamps (start of the first timed dispatch, latest end) and their

@@ -336,6 +336,13 @@ extern "C" int pgm_dq_sync(void *handle) {
   return wait_tail(dq);
 }
 
+int pgm_dq_wait(void *handle) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq) return fail(PGM_EINVAL, "dq_wait: null handle");
+  std::lock_guard<std::mutex> lk(dq->mu);
+  return dq->issued ? wait_tail(dq) : PGM_OK;
+}
+
 int pgm_dq_destroy(void *handle) {
   DirectQueue *dq = (DirectQueue *)handle;
   if (!dq) return PGM_OK;

@@ -608,6 +608,10 @@ class DirectQueue:
     def sync(self):
         N.check(N.lib().pgm_dq_sync(self._h), "dq_sync")
 
+    def wait(self):
+        """Every dispatch issued so far has completed (no release: sync() before HIP reads)."""
+        N.check(N.lib().pgm_dq_wait(self._h), "dq_wait")
+
     def timer_start(self):
         N.check(N.lib().pgm_dq_timer_start(self._h), "dq_timer_start")
 
