@@ -309,9 +309,15 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     ind.resize(ind.size() - 2);
     pgmi_appendf(o, "%s}\n", ind.c_str());
   }
+  // marginal stores: plain (write-back L2), or nontemporal when the step stores no product (a
+  // marginal-only pass writes nothing else; knob PGM_PM_MNT=0 keeps them plain)
+  static const int mnt = pm_knob("PGM_PM_MNT", 1);
   for (int u = 0; u < XI && has_m; ++u) {
     const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
-    pgmi_appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
+    if (mnt && !store)
+      pgmi_appendf(o, "  %s__builtin_nontemporal_store(a%d, (pgm_d2 *)(M + om) + x%d);\n", guard.c_str(), u, u);
+    else
+      pgmi_appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
   }
   o += "}\n";
   return o;
@@ -583,14 +589,30 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // specialised above 2M entries 911K / 601K; + one row pair per lane, nontemporal belief stores and
   // XCD-grouped blocks 933K; threshold 256K entries 648K at 1,000 rows)
   static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 18);
-  static const int xi_knob = pm_knob("PGM_PM_XI", 1);
+  static const int xi_knob = pm_knob("PGM_PM_XI", 0);  // 0: per step (below); 1 / 2 / 4 / 8: forced
   static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
   static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
   static const int nt = pm_knob("PGM_PM_NT", 1);
   static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
   const uint64_t entries = (uint64_t)k.n_outer * (uint64_t)k.n_red * 2ull * k.NP;
   if (!on || no_jit || entries < (uint64_t)min_entries) return PGM_OK;  // *bound NULL: generic kernel
-  const int XI = xi_knob == 2 || xi_knob == 4 ? xi_knob : 1;
+  // row pairs per lane: a block of a step with few reduced entries (separator messages from small
+  // operands, products without a reduction) does little work per lane — one 16-B store and a few
+  // loads — so its lifetime, not HBM, bounds the step; XI pairs per lane give each lane ~8 entries of
+  // work while keeping >= 2,048 blocks (8 per CU) in the step
+  int XI = 1;
+  if (xi_knob == 1 || xi_knob == 2 || xi_knob == 4 || xi_knob == 8) {
+    XI = xi_knob;
+  } else {
+    const uint64_t red = std::max<uint64_t>(1, (uint64_t)k.n_red);
+    while (XI < 8 && red * (uint64_t)XI < 8) {
+      const int nx = XI * 2;
+      const uint64_t gx2 = (k.NP + 256ull * nx - 1) / (256ull * nx);
+      const uint64_t pad = gx2 * 256ull * nx - k.NP;  // idle lanes in the last block of a row range
+      if (gx2 * (uint64_t)k.n_outer < 2048 || pad * 4 > k.NP) break;
+      XI = nx;
+    }
+  }
   const uint64_t gx = (k.NP + 256ull * XI - 1) / (256ull * XI);
   const uint64_t total = gx * (uint64_t)k.n_outer;
   if (total >= (1ull << 31)) return PGM_OK;

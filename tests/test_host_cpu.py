@@ -308,8 +308,9 @@ def _pm_desc(N, shapes_labels, out_labels, card, kinds=None):
     return d
 
 
-@pytest.mark.parametrize("red,store,ratio", [(1, True, False), (2, True, True), (1, False, True)])
-def test_product_marginal_specialised_source_compiles(tmp_path, red, store, ratio):
+@pytest.mark.parametrize("red,store,ratio,short", [(1, True, False, False), (2, True, True, False),
+                                                   (1, False, True, False), (1, False, False, True)])
+def test_product_marginal_specialised_source_compiles(tmp_path, red, store, ratio, short):
     """The specialised product+marginal kernel the bind entry point would compile (hipRTC on the
     GPU box) is generated on the host and compiles for gfx950 with hipcc: literal outer decode,
     nested reduced loops, ratio operands, marginal-only form."""
@@ -324,7 +325,7 @@ def test_product_marginal_specialised_source_compiles(tmp_path, red, store, rati
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     L = N.load_library()
     R = "__row__"
-    card = dict(zip(list("abcdef") + [R], (8, 2, 3, 8, 5, 9, 2100)))
+    card = dict(zip(list("abcdef") + [R], (8, 2, 3, 8, 5, 9, 4000 if short else 2100)))
     cl = list("abcdef") + [R]
     ops = [list("abcdef"), ["a", "c", "f", R]]
     kinds = None
@@ -332,7 +333,9 @@ def test_product_marginal_specialised_source_compiles(tmp_path, red, store, rati
         ops = [cl, ["a", "d", "f", R], ["a", "d", "f", R]]
         kinds = [N.PRODN_MUL, N.PRODN_RATIO, N.PRODN_DEN]
     d = _pm_desc(N, ops, cl, card, kinds)
-    marg = ["a", "d", "e", R]
+    # short: a marginal over one 2-state dim (a separator message from a small operand) — too little
+    # work per lane for one row pair, so the generator gives each lane 4 (x0..x3)
+    marg = ["a", "c", "d", "e", "f", R] if short else ["a", "d", "e", R]
     m_st = [s // 8 for s in np.empty([card[x] for x in marg]).strides]
     ms = (ctypes.c_int64 * len(cl))(*[m_st[marg.index(l)] if l in marg else 0 for l in cl])
     fake = [0x10000000 * (i + 1) for i in range(len(ops))]  # 16-B aligned, never dereferenced
@@ -342,7 +345,8 @@ def test_product_marginal_specialised_source_compiles(tmp_path, red, store, rati
                                         red, ctypes.c_void_p(0x60000000), buf, len(buf))
     assert n > 0, "shape should specialise"
     src = buf.value.decode()
-    assert "pgm_pm" in src and ("* pgm_ratio(" in src) == ratio and ("cj[" in src or "nontemporal" in src) == store
+    assert "pgm_pm" in src and ("* pgm_ratio(" in src) == ratio and ("cj[" in src or "nontemporal_store(w" in src) == store
+    assert ("const unsigned x3 = " in src) == short
     f = tmp_path / "pm.hip"
     f.write_text("#include <hip/hip_runtime.h>\n" + src)
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-c", str(f), "-o",
