@@ -1439,8 +1439,11 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
   constexpr int FM = BM / 16 / WY, FN = BN / 16 / WX;
   constexpr int NA = BM * BK / 256, NB = BN * BK / 256;  // tile elements per thread per k tile
   static_assert(FM >= 1 && FN >= 1 && NA >= 1 && NB >= 1, "tile shape");
-  __shared__ double As[BK][BM + 2];
-  __shared__ double Bs[BK][BN + 2];
+#ifndef PGM_GEMM_PAD
+#define PGM_GEMM_PAD 1
+#endif
+  __shared__ double As[BK][BM + PGM_GEMM_PAD];  // +1: the k-fast tile stores (16 lanes down a column) hit 32 distinct banks
+  __shared__ double Bs[BK][BN + PGM_GEMM_PAD];
   typedef double d4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wy = wave / WX, wx = wave % WX;
@@ -1482,32 +1485,76 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const GemmK p, const double *_
     bcol[i] = bok[i] ? goff<TB>(p.s_bn, p.b_n, gn) : 0;
   }
   double ra[NA], rb[NB];
-  // k offsets (table reads for table groups) are fetched one k tile ahead of the loads that use
-  // them, so a table lookup never sits in series with its data load
+  // k offsets.  SR (64 x 64 tiles): strided groups keep a running offset advanced by BK strides per
+  // tile (one 64-bit add instead of a multiply and a clamp per element and tile: the plain 64 x 64
+  // kernel was VALU-bound on that address arithmetic, 4096^2 x 512: 35 -> 40 TF/s); tiles wholly
+  // inside K take unguarded loads, the last tile guards each k.  The 128 x 64 and 16 x 128 tiles keep
+  // the clamped per-tile form (the running form costs them registers: 500 x (100 x 576 x 125)
+  // 307 -> 400 us, profiles/r02bo_gemm_ab.txt).  Table groups read their entries one k tile ahead of
+  // the loads that use them, so a table lookup never sits in series with its data load.
+  constexpr bool SR = BM == 64 && BN == 64;
   int64_t oa[NA], ob[NB];
+  const int64_t dka = (int64_t)BK * p.s_ak, dkb = (int64_t)BK * p.s_bk;
   auto offs = [&](int64_t k0) {
+    const bool full = SR && k0 + BK <= p.K;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int64_t gka = k0 + ak[i];
-      oa[i] = goff<TA>(p.s_ak, p.a_k, gka < p.K ? gka : p.K - 1);
+      if constexpr (TA || !SR) {
+        const int64_t gka = k0 + ak[i];
+        oa[i] = goff<TA>(p.s_ak, p.a_k, full ? gka : (gka < p.K ? gka : p.K - 1));
+      }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int64_t gkb = k0 + bk[i];
-      ob[i] = goff<TB>(p.s_bk, p.b_k, gkb < p.K ? gkb : p.K - 1);
+      if constexpr (TB || !SR) {
+        const int64_t gkb = k0 + bk[i];
+        ob[i] = goff<TB>(p.s_bk, p.b_k, full ? gkb : (gkb < p.K ? gkb : p.K - 1));
+      }
     }
   };
-  // branch-free edges: every load reads an in-bounds element (clamped index), then zero is selected
+  if constexpr (SR && !TA) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) oa[i] = (int64_t)ak[i] * p.s_ak;
+  }
+  if constexpr (SR && !TB) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) ob[i] = (int64_t)bk[i] * p.s_bk;
+  }
+  // rows / columns past M / N (and, in the clamped form, k past K) read an in-bounds element and
+  // are zeroed
   auto load = [&](int64_t k0) {
     double va[NA], vb[NB];
+    if (!SR || k0 + BK <= p.K) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) va[i] = Ab[arow[i] + oa[i]];
+      for (int i = 0; i < NA; ++i) va[i] = Ab[arow[i] + oa[i]];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) vb[i] = Bb[ob[i] + bcol[i]];
+      for (int i = 0; i < NB; ++i) vb[i] = Bb[ob[i] + bcol[i]];
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = (aok[i] && k0 + ak[i] < p.K) ? va[i] : 0.0;
+      for (int i = 0; i < NA; ++i) ra[i] = (aok[i] && (SR || k0 + ak[i] < p.K)) ? va[i] : 0.0;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = (bok[i] && k0 + bk[i] < p.K) ? vb[i] : 0.0;
+      for (int i = 0; i < NB; ++i) rb[i] = (bok[i] && (SR || k0 + bk[i] < p.K)) ? vb[i] : 0.0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        double v = 0.0;
+        if (aok[i] && k0 + ak[i] < p.K) v = Ab[arow[i] + oa[i]];
+        ra[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        double v = 0.0;
+        if (bok[i] && k0 + bk[i] < p.K) v = Bb[ob[i] + bcol[i]];
+        rb[i] = v;
+      }
+    }
+    if constexpr (SR && !TA) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) oa[i] += dka;
+    }
+    if constexpr (SR && !TB) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) ob[i] += dkb;
+    }
   };
   d4 acc[FM][FN];
 #pragma unroll
