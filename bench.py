@@ -243,9 +243,12 @@ class Launcher:
         if self.kind != "direct":
             ms, self._hip_ms = getattr(self, "_hip_ms", None), None
             return ms if ms is not None else self.timer.stop_ms()
-        if len(self.qs) == 1:
-            return self.q.timer_stop_ms()
         spans = [q.timer_stop_ticks() for q in self.qs]  # one HSA system clock for every queue
+        stats = [q.dispatch_stats() for q in self.qs]
+        n = sum(c for _, c in stats)
+        # each timed dispatch's own duration, averaged: the per-launch figure rocprofv3's kernel trace
+        # reports (with several queues it includes the time the dispatch shares the GPU with others)
+        self.dispatch_avg_ms = (sum(t for t, _ in stats) * 1e3 / spans[0][2] / n) if n else None
         spans = [(a, b, f) for a, b, f in spans if b > a]
         if not spans:
             return 0.0
@@ -253,20 +256,26 @@ class Launcher:
 
 
 def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
-    """Average GPU span per launch of the plan's dispatch floor (PatternPlan.bind(floor=True)) over
-    args.steps launches, launched and timed as the measured kernel; outside the timed region, into
-    its own output buffer.  None when the specialised kernel is not in use."""
+    """(floor, kernel): average GPU span per launch of the plan's dispatch floor
+    (PatternPlan.bind(floor=True): same grid, loads and stores, no CPT arithmetic) and of the measured
+    kernel itself, each over args.steps launches on ONE queue into one output buffer, outside the timed
+    region — so the two are compared like for like.  (None, None) when the specialised kernel is not
+    in use."""
     if plan.kernel_name() != "pgm_rows_jit":
-        return None
-    out = plan.alloc_outputs(rows, marginals=True)
-    fl = launcher_cls(plan.bind(d_codes, rows, 0, rows, out, floor=True), args.launch)
-    fl.steps(max(args.warmup, 1))
-    fl.sync()
-    fl.timer_start()
-    fl.steps(args.steps)
-    ms = fl.timer_stop_ms()
-    fl.sync()
-    return ms / args.steps if ms > 0 else None
+        return None, None
+    res = []
+    for floor in (True, False):
+        out = plan.alloc_outputs(rows, marginals=True)
+        fl = launcher_cls(plan.bind(d_codes, rows, 0, rows, out, floor=floor), args.launch)
+        fl.steps(max(args.warmup, 1))
+        fl.sync()
+        fl.timer_start()
+        fl.steps(args.steps)
+        ms = fl.timer_stop_ms()
+        fl.sync()
+        res.append(ms / args.steps if ms > 0 else None)
+        del fl, out
+    return res[0], res[1]
 
 
 def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, qs, n_out=24, steps=200):
@@ -463,12 +472,13 @@ def bench_c3(args, dist, rank, world):
         kern_ms = (t_end - t_start) * 1e3 / args.steps
     bpr = plan.algorithmic_bytes_per_row(marginals=True)
     achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
-    floor_ms = dispatch_floor_ms(plan, d_codes, rows, args, Launcher)
+    floor_ms, single_ms = dispatch_floor_ms(plan, d_codes, rows, args, Launcher)
     working_set = bpr * rows * nb
     stream = None
     if args.launch == "direct" and working_set <= MALL_BYTES:
         stream = hbm_stream_roofline(plan, d_codes, rows, nb, args, err, launcher.qs)
-    kname = plan.kernel_name()
+    kname, k_blocks, k_wg = bounds[0].kernel()  # the kernel the bound launches run
+    kname = kname or plan.kernel_name()
     traffic, traffic_rows = load_traffic(kname)
     if traffic is not None and traffic_rows:
         traffic = traffic * rows / traffic_rows
@@ -510,17 +520,22 @@ def bench_c3(args, dist, rank, world):
             "traffic": traffic,
             "kernel": kname,
             "kernel_ms": kern_ms,
-            # the same dispatch with the CPT staging and arithmetic removed (pgm_rows_floor: same grid,
-            # same code loads, same write-through output stores), timed the same way after the timed
-            # region: what one launch of this shape costs before any inference work
+            "grid": {"blocks": k_blocks, "workgroup": k_wg},
+            # the same dispatch with the CPT staging and arithmetic removed (pgm_rows_floor[2]: same grid,
+            # same code loads, same write-through output stores) and the kernel itself, each on one queue
+            # after the timed region: what one launch of this shape costs before any inference work
             "dispatch_floor_ms": floor_ms,
-            "kernel_over_floor": (kern_ms / floor_ms) if floor_ms else None,
+            "single_queue_kernel_ms": single_ms,
+            "kernel_over_floor": (single_ms / floor_ms) if floor_ms and single_ms else None,
             "algorithmic_bytes_per_row": bpr,
             "bytes_per_launch": bpr * rows,
             # kernel_ms is the GPU span per step; with Q queues up to Q launches run at once, so the
             # achieved rate is the launches' aggregate bytes over the span (a single dispatch's own
             # duration, rocprofv3's per-kernel time, is longer by up to the overlap)
             "concurrent_queues": nq,
+            # the timed dispatches' own durations averaged (queue timestamps): the per-launch number to
+            # compare with the committed rocprofv3 kernel-trace average (profiles/*_kernel_stats.csv)
+            "dispatch_avg_ms": getattr(launcher, "dispatch_avg_ms", None),
             # the batches' outputs + inputs (algorithmic bytes): the default 24 batches (343 MB) exceed
             # the MI355X's 256 MiB Infinity Cache (MALL), so a step's output lines are evicted to HBM
             # before its buffer comes round again and the achieved rate is an HBM rate; with a set

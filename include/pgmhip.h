@@ -397,6 +397,9 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
                        double *gap, int32_t *err_flag, void *stream, void **bound);
 int pgm_rows_bound_run(void *bound);
 int pgm_rows_bound_destroy(void *bound);
+/* which kernel a bound launch runs: "pgm_rows_jit" (one row per thread), "pgm_rows_jit2" (two rows
+ * per thread, 16-B stores), "pgm_rows_floor" / "pgm_rows_floor2" (PGM_ROWS_FLOOR), or "" (an AOT kernel), with its grid and workgroup size */
+int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
 
 /* Direct AQL dispatch (pgmpy_amd/csrc/pgmdq.cpp).  A user-mode HSA queue on the GPU agent of a HIP
  * device; a bound launch of the plan-specialised kernel (pgm_rows_plan_bind) is re-bound to it and
@@ -425,6 +428,10 @@ int pgm_dq_timer_stop_ms(void *dq, float *ms);
 /* the same span as raw HSA system timestamps (start of the first timed dispatch, latest end) and their
  * frequency, so spans of several queues can be joined */
 int pgm_dq_timer_stop_ticks(void *dq, uint64_t *start, uint64_t *end, uint64_t *freq);
+/* after a timer stop: the sum of the timed dispatches' own durations (end - start, in the ticks of
+ * pgm_dq_timer_stop_ticks) and how many were summed (those still in the 256-signal ring) — the
+ * per-launch duration a kernel trace reports, which exceeds span / launches when queues overlap */
+int pgm_dq_timer_dispatch_stats(void *dq, uint64_t *sum_ticks, uint64_t *count);
 int pgm_dq_bound_destroy(void *dbound);
 
 #ifdef __cplusplus

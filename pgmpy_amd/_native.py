@@ -198,6 +198,8 @@ _SIGS = {
     "pgm_rows_plan_source": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
                              ctypes.c_int),
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
+    "pgm_rows_bound_kernel": ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
+                               ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "pgm_codes_remap": ([_P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32, _P, _P,
                          ctypes.c_int64, _P, _P, _P, _P, _P], ctypes.c_int),
     "pgm_sample_joint": ([_P, ctypes.c_int64, ctypes.c_int64, _P, _P, ctypes.c_int64, _P, _P], ctypes.c_int),
@@ -212,6 +214,8 @@ _SIGS = {
     "pgm_dq_timer_stop_ms": ([_P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "pgm_dq_timer_stop_ticks": ([_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "pgm_dq_timer_dispatch_stats": ([_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
+                                    ctypes.c_int),
     "pgm_dq_bound_destroy": ([_P], ctypes.c_int),
 }
 

@@ -70,6 +70,7 @@ struct DirectQueue {
   bool have_start = false;
   uint64_t t_first = 0;
   uint64_t start_ticks = 0;
+  uint64_t disp_ticks = 0, disp_n = 0;  // last span: sum of per-dispatch (end - start), dispatches summed
   bool hsa_up = false;
   bool profiling = true;
 };
@@ -514,6 +515,18 @@ int pgm_dq_timer_stop_ticks(void *handle, uint64_t *start, uint64_t *end, uint64
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
     te.end = std::max(te.end, t.end);
   }
+  // per-dispatch durations (what a kernel trace reports per launch) of the span's dispatches still in
+  // the signal ring
+  dq->disp_ticks = dq->disp_n = 0;
+  const uint64_t lo = std::max(dq->t_first, dq->issued >= kRing ? dq->issued - kRing : 0);
+  for (uint64_t i = lo; i <= dq->last_kernel && i < dq->issued; ++i) {
+    hsa_amd_profiling_dispatch_time_t t;
+    HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
+    if (t.end > t.start) {
+      dq->disp_ticks += t.end - t.start;
+      ++dq->disp_n;
+    }
+  }
   if (!dq->have_start) {
     hsa_amd_profiling_dispatch_time_t ts;
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[dq->t_first % kRing], &ts));
@@ -521,6 +534,15 @@ int pgm_dq_timer_stop_ticks(void *handle, uint64_t *start, uint64_t *end, uint64
   }
   *start = dq->start_ticks;
   *end = te.end > dq->start_ticks ? te.end : dq->start_ticks;
+  return PGM_OK;
+}
+
+int pgm_dq_timer_dispatch_stats(void *handle, uint64_t *sum_ticks, uint64_t *count) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq || !sum_ticks || !count) return fail(PGM_EINVAL, "dq_timer_dispatch_stats: null argument");
+  std::lock_guard<std::mutex> lk(dq->mu);
+  *sum_ticks = dq->disp_ticks;
+  *count = dq->disp_n;
   return PGM_OK;
 }
 

@@ -34,7 +34,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 12  // 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 13  // 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -1763,6 +1763,7 @@ struct RowsHandle {
   hipFunction_t jit_fn = nullptr;
   hipFunction_t jit_fn2 = nullptr;  // two rows per thread
   hipFunction_t jit_fn_floor = nullptr;  // PGM_ROWS_FLOOR: the same dispatch's loads + stores only
+  hipFunction_t jit_fn_floor2 = nullptr;  // ... of the two-rows-per-thread dispatch
   std::vector<char> jit_code;         // the compiled code object (the direct AQL path loads it again)
   bool jit_write_through = false;     // its output stores are write-through (jit_store() == 2)
 };
@@ -2300,12 +2301,16 @@ void pgmi_appendf(std::string &o, const char *fmt, ...) {
   o += buf;
 }
 
-// workgroup size of the specialised row kernel (tuning knob PGM_ROWS_JIT_WG: 64, 128 or 256 rows)
+// workgroup size of the specialised row kernels (tuning knob PGM_ROWS_JIT_WG: 64 ... 1024 threads).
+// 512 (r02br, MI355X, C3 = 100k-row launches on 4 queues, two rows per thread): 98 blocks of 1,024
+// rows per launch — one CPT staging per 1,024 rows and a quarter of the workgroup dispatches of
+// 256 x one row — 26.4 -> 29.1-31.1 G rows/s at 20 steps, 36.2 -> 47.1 G at 400; one queue and
+// 1M-row launches unchanged (profiles/r02bq_c3_wg_rowform_sweep.txt, r02br_c3_wg_rowform_confirm.txt)
 static int jit_wg() {
   static const int wg = [] {
     const char *e = getenv("PGM_ROWS_JIT_WG");
-    const int v = e ? atoi(e) : 256;
-    return (v == 64 || v == 128) ? v : 256;
+    const int v = e ? atoi(e) : 512;
+    return (v == 64 || v == 128 || v == 256 || v == 1024) ? v : 512;
   }();
   return wg;
 }
@@ -2465,35 +2470,50 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   }
 }
 
-// the dispatch floor of a plan (PGM_ROWS_FLOOR, measurement only): the one-row kernel's grid, its
-// evidence-column byte loads and its output stores (same addresses, same cache policy), with the CPT
-// staging, gathers and arithmetic replaced by one conversion of the loaded codes
-static void emit_rows_floor(std::string &o, const pgm_rows_plan *pl) {
+// the dispatch floor of a plan (PGM_ROWS_FLOOR, measurement only): the row kernel's grid (R rows per
+// thread, as pgm_rows_jit / pgm_rows_jit2), its evidence-column loads and its output stores (same
+// addresses, same widths, same cache policy), with the CPT staging, gathers and arithmetic replaced by
+// one conversion of the loaded codes
+static void emit_rows_floor(std::string &o, const pgm_rows_plan *pl, int R) {
   const int WG = jit_wg();
-  pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_floor(const double *__restrict__ V, "
+  const bool wt = jit_store() == 2;
+  pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_floor%s(const double *__restrict__ V, "
              "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
              "double *__restrict__ M, long long ldo, int *__restrict__ MP, double *__restrict__ G, "
-             "int *__restrict__ E, int mode) {\n", WG);
-  pgmi_appendf(o, "  const long long r = (long long)blockIdx.x * %d + threadIdx.x;\n  if (r >= n) return;\n", WG);
+             "int *__restrict__ E, int mode) {\n", WG, R == 2 ? "2" : "");
+  pgmi_appendf(o, "  const long long r = ((long long)blockIdx.x * %d + threadIdx.x) * %d;\n  if (r >= n) return;\n", WG, R);
+  if (R == 2 && wt)
+    o += "  const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(M, 0, 0x7fffffff, 0x00020000);\n"
+         "  const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc(G, 0, 0x7fffffff, 0x00020000);\n";
   std::vector<int> cols;
   for (int j = 0; j < pl->n_ev; ++j)
     if (std::find(cols.begin(), cols.end(), pl->ev_col[j]) == cols.end()) cols.push_back(pl->ev_col[j]);
   o += "  unsigned x = 0u;\n";
   if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + r;\n";
-  for (size_t i = 0; i < cols.size(); ++i) pgmi_appendf(o, "  x += cr[%dLL * ldc];\n", cols[i]);
+  for (size_t i = 0; i < cols.size(); ++i) {
+    if (R == 1) pgmi_appendf(o, "  x += cr[%dLL * ldc];\n", cols[i]);
+    else pgmi_appendf(o, "  x += *(const unsigned short *)(cr + %dLL * ldc);\n", cols[i]);
+  }
   o += "  const double v = (double)x;\n  if (mode & 1) {\n";
-  const bool wt = jit_store() == 2;
   for (int c = 0; c < pl->n_comp; ++c) {
     const int lb = pl->comp_loop_begin[c];
     if (pl->comp_n_query[c] != 1) continue;
     for (int q = 0; q < pl->loop_card[lb]; ++q) {
       const int mo = pl->loop_marg_off[lb] + q;
-      if (wt) pgmi_appendf(o, "    PGM_WT8(double, &M[%dLL * ldo + r], v);\n", mo);
+      if (R == 2 && wt) pgmi_appendf(o, "    PGM_WT16(rsM, %dLL * ldo + r, v, v);\n", mo);
+      else if (R == 2) pgmi_appendf(o, "    *(double2 *)(M + %dLL * ldo + r) = make_double2(v, v);\n", mo);
+      else if (wt) pgmi_appendf(o, "    PGM_WT8(double, &M[%dLL * ldo + r], v);\n", mo);
       else pgmi_appendf(o, "    M[%dLL * ldo + r] = v;\n", mo);
     }
   }
   o += "  }\n  if (mode & 12) {\n";
-  if (wt)
+  if (R == 2 && wt)
+    o += "    if (MP) PGM_WT8(unsigned long long, (unsigned long long *)(MP + r), (unsigned long long)x);\n"
+         "    if ((mode & 8) && G) PGM_WT16(rsG, r, v, v);\n  }\n}\n";
+  else if (R == 2)
+    o += "    if (MP) *(int2 *)(MP + r) = make_int2((int)x, (int)x);\n"
+         "    if ((mode & 8) && G) *(double2 *)(G + r) = make_double2(v, v);\n  }\n}\n";
+  else if (wt)
     o += "    if (MP) PGM_WT4(int, &MP[r], (int)x);\n    if ((mode & 8) && G) PGM_WT8(double, &G[r], v);\n  }\n}\n";
   else
     o += "    if (MP) MP[r] = (int)x;\n    if ((mode & 8) && G) G[r] = v;\n  }\n}\n";
@@ -2514,7 +2534,9 @@ static std::string rows_jit_source(const pgm_rows_plan *pl) {
   o += "\n";
   emit_rows_kernel(o, pl, 2);
   o += "\n";
-  emit_rows_floor(o, pl);
+  emit_rows_floor(o, pl, 1);
+  o += "\n";
+  emit_rows_floor(o, pl, 2);
   return o;
 }
 
@@ -2522,9 +2544,10 @@ static std::string rows_jit_source(const pgm_rows_plan *pl) {
 static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
                          const double *marg, int64_t ld_out, const int32_t *map, const double *gap, int n_marg) {
   static const bool off = getenv("PGM_NO_JIT2") != nullptr;  // testing / tuning
-  // measured (MI355X): one row per thread is faster while the launch is latency-bound (100k rows:
-  // 4.6 vs 5.2 us), two rows with 16-B stores once it is HBM-bound (4M rows: 110 vs 126 us)
-  static const int64_t min_rows = getenv("PGM_JIT2_MIN_ROWS") ? atoll(getenv("PGM_JIT2_MIN_ROWS")) : 400000;
+  // measured (MI355X): two rows with 16-B stores once the launch is HBM-bound (4M rows: 110 vs 126 us)
+  // and, since the 512-thread workgroups and concurrent queues, at 100k rows too (one queue: equal,
+  // 3.9 us; four queues: 2.7 -> 2.1 us per launch of GPU span, r02br); one row below 50k rows
+  static const int64_t min_rows = getenv("PGM_JIT2_MIN_ROWS") ? atoll(getenv("PGM_JIT2_MIN_ROWS")) : 50000;
   if (off || n_rows < min_rows || n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
   if ((mode & PGM_ROWS_MARGINALS) && (((uintptr_t)marg & 15) || ld_out % 2)) return false;
   if (map && ((uintptr_t)map & 7)) return false;
@@ -2555,7 +2578,8 @@ static bool rows_jit_ready(RowsHandle *h) {
   }
   if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess ||
       hipModuleGetFunction(&h->jit_fn2, h->jit_mod, "pgm_rows_jit2") != hipSuccess ||
-      hipModuleGetFunction(&h->jit_fn_floor, h->jit_mod, "pgm_rows_floor") != hipSuccess) {
+      hipModuleGetFunction(&h->jit_fn_floor, h->jit_mod, "pgm_rows_floor") != hipSuccess ||
+      hipModuleGetFunction(&h->jit_fn_floor2, h->jit_mod, "pgm_rows_floor2") != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -3687,9 +3711,9 @@ int pgm_rows_plan_bind(void *handle, int32_t mode, const uint8_t *codes, int64_t
   if (n_rows > 0 && h->jit_state > 0 &&
       !(mode & (PGM_ROWS_JOINT | PGM_ROWS_GENERIC | PGM_ROWS_NO_JIT | PGM_ROWS_VALUES_GLOBAL | PGM_ROWS_ONE_GROUP))) {
     const bool two = rows_jit2_ok(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, h->k.n_marg);
-    b->fn = floor ? h->jit_fn_floor : two ? h->jit_fn2 : h->jit_fn;
+    b->fn = floor ? (two ? h->jit_fn_floor2 : h->jit_fn_floor) : two ? h->jit_fn2 : h->jit_fn;
     b->args = RowsJitArgs{h->d_values, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, err_flag, mode, 0};
-    const uint64_t rpb = (uint64_t)jit_wg() * (two && !floor ? 2 : 1);
+    const uint64_t rpb = (uint64_t)jit_wg() * (two ? 2 : 1);
     b->blocks = (unsigned)(((uint64_t)n_rows + rpb - 1) / rpb);
   } else if (floor) {
     delete b;
@@ -3713,6 +3737,17 @@ int pgm_rows_bound_run(void *bound) {
                        b->map, b->gap, b->err, b->stream, false);
 }
 
+int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks, uint32_t *wg) {
+  RowsBound *b = (RowsBound *)bound;
+  if (!b || !name || cap == 0) return fail(PGM_EINVAL, "rows_bound_kernel: null argument");
+  RowsHandle *h = (RowsHandle *)b->handle;
+  const char *k = !b->fn ? "" : b->fn == h->jit_fn2 ? "pgm_rows_jit2" : b->fn == h->jit_fn_floor ? "pgm_rows_floor" : b->fn == h->jit_fn_floor2 ? "pgm_rows_floor2" : "pgm_rows_jit";
+  snprintf(name, cap, "%s", k);
+  if (blocks) *blocks = b->fn ? b->blocks : 0;
+  if (wg) *wg = b->fn ? (uint32_t)jit_wg() : 0;
+  return PGM_OK;
+}
+
 int pgm_rows_bound_destroy(void *bound) {
   STALE_PROBE();
   delete (RowsBound *)bound;
@@ -3729,7 +3764,7 @@ int pgmi_rows_bound_jit(void *bound, pgmi_jit_launch *out) {
   if (h->jit_code.empty()) return fail(PGM_EINVAL, "direct launch: no code object kept for this plan");
   out->code = h->jit_code.data();
   out->code_size = h->jit_code.size();
-  out->kernel = b->fn == h->jit_fn2 ? "pgm_rows_jit2" : b->fn == h->jit_fn_floor ? "pgm_rows_floor" : "pgm_rows_jit";
+  out->kernel = b->fn == h->jit_fn2 ? "pgm_rows_jit2" : b->fn == h->jit_fn_floor ? "pgm_rows_floor" : b->fn == h->jit_fn_floor2 ? "pgm_rows_floor2" : "pgm_rows_jit";
   out->args = &b->args;
   out->args_size = b->args_size;
   out->blocks = b->blocks;

@@ -565,6 +565,17 @@ class BoundRows:
             N.check(st, "rows_bound_run")
         return self.out
 
+    def kernel(self):
+        """(kernel name, blocks, workgroup size) this bound launch runs (pgm_rows_bound_kernel);
+        the name is "" for an AOT kernel."""
+        import ctypes
+
+        name = ctypes.create_string_buffer(64)
+        nb, wg = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().pgm_rows_bound_kernel(self._h, name, 64, ctypes.byref(nb), ctypes.byref(wg)),
+                "rows_bound_kernel")
+        return name.value.decode(), nb.value, wg.value
+
     def direct(self, queue=None):
         """The same launch dispatched on a DirectQueue (pgm_dq_bind_rows): one AQL packet per
         run(), no HIP runtime on the launch path.  Needs the plan-specialised kernel."""
@@ -630,6 +641,15 @@ class DirectQueue:
         N.check(N.lib().pgm_dq_timer_stop_ticks(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(f)),
                 "dq_timer_stop")
         return a.value, b.value, f.value
+
+    def dispatch_stats(self):
+        """(sum of the last timed span's per-dispatch durations in ticks, dispatches summed)."""
+        import ctypes
+
+        t, n = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().pgm_dq_timer_dispatch_stats(self._h, ctypes.byref(t), ctypes.byref(n)),
+                "dq_timer_dispatch_stats")
+        return t.value, n.value
 
     def __del__(self):
         h = getattr(self, "_h", None)

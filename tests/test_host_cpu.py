@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 12
+    assert lib.pgm_version() == 13
 
 
 def test_struct_layouts_match_header():
@@ -228,8 +228,11 @@ def test_specialised_row_kernel_source_compiles_for_gfx950():
     one_row = src[:src.index("pgm_rows_jit2(")]
     assert one_row.count("M[") == plan.n_acc == 17
     assert one_row.count("cr[") == 7  # the template's 7 evidence columns
-    floor = src[src.index("pgm_rows_floor("):]  # the dispatch floor: same loads and stores, no CPT math
+    # the dispatch floors: same loads and stores, no CPT math (one-row and two-row grids)
+    floor = src[src.index("pgm_rows_floor("):src.index("pgm_rows_floor2(")]
     assert floor.count("M[") == 17 and floor.count("cr[") == 7 and "S[" not in floor
+    floor2 = src[src.index("pgm_rows_floor2("):]
+    assert floor2.count("(cr + ") == 7 and floor2.count("PGM_WT16(rsM") == 17 and "S[" not in floor2
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")

@@ -419,10 +419,11 @@ def test_specialised_kernel_bit_identical(gpu, seed):
     assert checked >= 1
 
 
-@pytest.mark.parametrize("rows", [400_000, 400_001])
+@pytest.mark.parametrize("rows", [100_000, 100_001, 400_000, 400_001])
 def test_specialised_kernel_large_batches(gpu, rows):
-    """Large batches: even row counts take the two-rows-per-thread specialised kernel (16-B stores,
-    2-byte code loads), odd ones the one-row kernel; both bit-identical to k_rows_affine."""
+    """Large batches (>= 50k rows): even row counts take the two-rows-per-thread specialised kernel
+    (16-B stores, 2-byte code loads), odd ones the one-row kernel; both bit-identical to k_rows_affine.
+    The bound launch reports which one it runs (pgm_rows_bound_kernel)."""
     import random
 
     import torch
@@ -451,9 +452,15 @@ def test_specialised_kernel_large_batches(gpu, rows):
     torch.cuda.synchronize()
     for k in ("marg", "map", "gap"):
         assert torch.equal(res[0][k], res[1][k]), k
+    o = plan.alloc_outputs(rows, marginals=True)
+    name, blocks, wg = plan.bind(d, rows, 0, rows, o).kernel()
+    per_block = wg * (2 if rows % 2 == 0 else 1)
+    assert name == ("pgm_rows_jit2" if rows % 2 == 0 else "pgm_rows_jit")
+    assert blocks == (rows + per_block - 1) // per_block
 
 
-@pytest.mark.parametrize("row0,n", [(0, 1), (37, 1), (5, 255), (1000, 257), (2, 400_000), (3, 400_000)])
+@pytest.mark.parametrize("row0,n", [(0, 1), (37, 1), (5, 255), (1000, 257), (2, 100_000), (3, 100_000), (2, 400_000),
+                                   (3, 400_000)])
 def test_specialised_kernel_row_windows(gpu, row0, n):
     """Rows [row0, row0 + n) of a wider code matrix (ld > n): single rows, ragged counts, odd and even
     offsets (the two-rows kernel needs an even row0) give what a contiguous copy of the window gives."""

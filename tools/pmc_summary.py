@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a tools/gpu_profile.sh run (gpurun_out/prof_TAG, pmc_fetch_TAG, pmc_write_TAG) into
 profiles/TAG_kernel_stats.csv and profiles/TAG_pmc_pgm_rows_jit.json (+ profiles/pmc_pgm_rows_jit.json,
-which bench.py reads for roofline.traffic).  python tools/pmc_summary.py TAG"""
+which bench.py reads for roofline.traffic).  python tools/pmc_summary.py TAG [KERNEL]
+(KERNEL: pgm_rows_jit, default, or pgm_rows_jit2 — the kernel the bench's bound launch runs)"""
 import csv
 import glob
 import json
@@ -10,7 +11,12 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "pgm_rows_jit"
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "pgm_rows_jit"
+
+
+def is_kernel(name):
+    """name is KERNEL (possibly with a suffix such as ".kd"), not a longer kernel name"""
+    return name.startswith(KERNEL) and not name[len(KERNEL):len(KERNEL) + 1].isalnum()
 
 
 def counter(tag, what, name):
@@ -18,7 +24,7 @@ def counter(tag, what, name):
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{what}_{tag}", "**", "*counter_collection.csv"),
                        recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Kernel_Name"].startswith(KERNEL) and r["Counter_Name"] == name:
+            if is_kernel(r["Kernel_Name"]) and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -29,7 +35,7 @@ def main(tag):
     if stats:
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats[0])):
-            if r["Name"].startswith(KERNEL):
+            if is_kernel(r["Name"]):
                 avg = float(r["AverageNs"])
     fetch, write = counter(tag, "fetch", "FETCH_SIZE"), counter(tag, "write", "WRITE_SIZE")
     f_kb, w_kb = sum(fetch) / len(fetch), sum(write) / len(write)
