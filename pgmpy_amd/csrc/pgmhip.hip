@@ -2301,7 +2301,7 @@ void pgmi_appendf(std::string &o, const char *fmt, ...) {
   o += buf;
 }
 
-// workgroup size of the specialised row kernels (tuning knob PGM_ROWS_JIT_WG: 64 ... 1024 threads).
+// workgroup size of the specialised row kernels (tuning knob PGM_ROWS_JIT_WG: a multiple of 64, <= 1024).
 // 512 (r02br, MI355X, C3 = 100k-row launches on 4 queues, two rows per thread): 98 blocks of 1,024
 // rows per launch — one CPT staging per 1,024 rows and a quarter of the workgroup dispatches of
 // 256 x one row — 26.4 -> 29.1-31.1 G rows/s at 20 steps, 36.2 -> 47.1 G at 400; one queue and
@@ -2310,7 +2310,7 @@ static int jit_wg() {
   static const int wg = [] {
     const char *e = getenv("PGM_ROWS_JIT_WG");
     const int v = e ? atoi(e) : 512;
-    return (v == 64 || v == 128 || v == 256 || v == 1024) ? v : 512;
+    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 512;
   }();
   return wg;
 }
