@@ -590,6 +590,10 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // XCD-grouped blocks 933K; threshold 256K entries 648K at 1,000 rows)
   static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 18);
   static const int xi_knob = pm_knob("PGM_PM_XI", 0);  // 0: per step (below); 1 / 2 / 4 / 8: forced
+  // per step, at least this many row pairs per lane (1 / 2 / 4) when the rows fill them: 2 measured
+  // (MI355X, C4 4,000 rows: 1.146 -> 1.18 M calibrations/s; 1,000 rows unchanged, too few rows;
+  // forced 2 / 4 for every step, or a minimum of 4: slower, profiles/r02bw_c4_xi.txt)
+  static const int xi_min = pm_knob("PGM_PM_XI_MIN", 2);
   static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
   static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
   static const int nt = pm_knob("PGM_PM_NT", 1);
@@ -600,7 +604,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // operands, products without a reduction) does little work per lane — one 16-B store and a few
   // loads — so its lifetime, not HBM, bounds the step; XI pairs per lane give each lane ~8 entries of
   // work while keeping >= 2,048 blocks (8 per CU) in the step
-  int XI = 1;
+  int XI = (xi_min == 2 || xi_min == 4) && (uint64_t)k.NP >= 256ull * xi_min ? xi_min : 1;
   if (xi_knob == 1 || xi_knob == 2 || xi_knob == 4 || xi_knob == 8) {
     XI = xi_knob;
   } else {
