@@ -451,6 +451,13 @@ def bench_c3(args, dist, rank, world):
     launcher = Launcher(bounds, args.launch, group=args.group, queues=nq)
     launcher.steps(max(args.warmup, nb))
     launcher.sync()
+    if args.launch == "direct" and not args.acquire_in_window:
+        # the first dispatch on a queue after a sync acquires at system scope (so inputs HIP wrote since
+        # become visible); nothing writes the resident batches from here on, so one more untimed dispatch
+        # per queue takes that acquire and the timed window holds steady-state dispatches only
+        # (pgm_dq_wait: completion without a new release barrier, which would re-arm the acquire)
+        launcher.steps(len(launcher.qs))
+        launcher.wait()
     barrier(dist)
     # GPU span of the timed dispatches (queue timestamps or HIP events on the launch stream):
     # average launch duration, including the gap between back-to-back launches that rocprofv3's
@@ -508,6 +515,10 @@ def bench_c3(args, dist, rank, world):
             "batches": nb,
             "dispatch_group": args.group,
             "queues": nq,
+            # each queue's first dispatch after the pre-window sync carries the system-scope acquire that
+            # makes HIP-written inputs visible; it runs as an untimed warmup dispatch (the batches are not
+            # written again), so the window's K dispatches all acquire nothing (--acquire-in-window: A/B)
+            "acquire_before_window": args.launch == "direct" and not args.acquire_in_window,
             "parallelism": f"rows sharded over {world} GPU(s), no data-path collective",
             "plan": plan.describe(),
         },
@@ -894,6 +905,8 @@ def main():
     ap.add_argument("--queues", type=int, default=4,
                     help="c3 direct launch: spread the batches over this many user-mode HSA queues "
                          "(batch i on queue i %% Q; <= --batches)")
+    ap.add_argument("--acquire-in-window", action="store_true",
+                    help="c3 (A/B): leave each queue's first system-scope acquire inside the timed window")
     ap.add_argument("--launch", default="direct", choices=["direct", "hip"],
                     help="c3/c5: AQL packets on a user-mode HSA queue (direct) or hipModuleLaunchKernel (hip)")
     args = ap.parse_args()
