@@ -368,7 +368,10 @@ def cpu_baseline_c3_allcore(missing, codes_host, nodes, seconds):
     dt = time.perf_counter() - t0
     return {"value": sum(counts) / dt, "unit": "queries/s", "cores": W, "kind": "port",
             "sample": f"{sum(counts)} rows of the same synthetic munin sample, numpy oracle per row, "
-                      f"{W} worker processes, {dt:.1f} s wall (upper bound: pgmpy's predict is GIL-bound)"}
+                      f"{W} worker processes, {dt:.1f} s wall (upper bound: pgmpy's predict is GIL-bound); "
+                      f"W is capped at 16, the GPU box's CPU share per GPU (OMP_NUM_THREADS / MAX_JOBS there), "
+                      f"not the {os.cpu_count()} CPUs the host shows",
+            "cap_reason": "per-GPU CPU share of the box"}
 
 
 def cpu_baselines_c3(args):
