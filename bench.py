@@ -141,7 +141,14 @@ class HipTimer:
         self.N.check(self.L.pgm_event_record(self.a, self.N.stream_handle()))
 
     def stop_ms(self):
+        self.mark_end()
+        return self.elapsed_ms()
+
+    def mark_end(self):
         self.N.check(self.L.pgm_event_record(self.b, self.N.stream_handle()))
+
+    def elapsed_ms(self):
+        """start -> end event (both complete: call after the stream has been synchronized)."""
         ms = ctypes.c_float()
         self.N.check(self.L.pgm_event_elapsed_ms(self.a, self.b, ctypes.byref(ms)))
         return float(ms.value)
@@ -449,6 +456,9 @@ def bench_c3(args, dist, rank, world):
     # one step = one pass of the fused row plan over one resident batch (batch i = evidence columns
     # [i*rows, (i+1)*rows), its own output), launched through the prepared (bound) C-ABI entry:
     # validated and marshalled once, one argument-free call per step
+    if args.launch == "ring":
+        return bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_codes, outs, err, codes_all,
+                             nodes, perms)
     bounds = [plan.bind(d_codes, rows * nb, i * rows, rows, outs[i], err=err) for i in range(nb)]
     nq = args.queues if args.launch == "direct" else 1
     launcher = Launcher(bounds, args.launch, group=args.group, queues=nq)
@@ -582,6 +592,111 @@ def bench_c3(args, dist, rank, world):
         torch.cuda.synchronize()
         result["gather_ms"] = (time.perf_counter() - g0) * 1e3
         result["gather_backend"] = _BACKEND
+    return result
+
+
+def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_codes, outs, err, codes_all, nodes,
+                  perms):
+    """C3 through the resident ring (--launch ring, pgm_rows_ring_*): the K timed steps are K batches
+    posted one by one to ONE launch of the plan-specialised kernel that is started inside the timed
+    window.  Batch i runs the rows and output buffers of resident batch i % nb.  The window closes when
+    the launch has completed (hipStreamSynchronize: HIP's end-of-kernel system-scope release included).
+    The launch's own GPU span is bracketed by HIP events on its stream (kernel_ms = span / K); a
+    rocprofv3 kernel trace reports the same launch ("pgm_rows_ring", one dispatch per timed region)."""
+    import copy
+
+    import torch
+
+    rows = args.rows
+    nb = len(outs)
+    ring = plan.ring([(d_codes, rows * nb, i * rows, outs[i]) for i in range(nb)], rows, err=err)
+    kname, k_blocks, k_wg = ring.kernel()
+    ring.run(max(args.warmup, nb))  # every slot once
+    torch.cuda.synchronize()
+    timer = HipTimer()
+    barrier(dist)
+    t_start = time.perf_counter()
+    timer.start()
+    ring.start(args.steps)
+    timer.mark_end()  # the end event completes with the launch
+    for b in range(1, args.steps + 1):
+        ring.post(b)  # one step = one batch published to the resident launch
+    ring.finish()
+    t_end = time.perf_counter()
+    kern_ms = timer.elapsed_ms() / args.steps
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t_end - t_start)
+    assert int(err.item()) == 0
+    bpr = plan.algorithmic_bytes_per_row(marginals=True)
+    achieved = bpr * rows / (kern_ms * 1e-3) / 1e9
+    ms_per_step = elapsed * 1e3 / args.steps
+    hip_args = copy.copy(args)
+    hip_args.launch = "hip"
+    floor_ms, single_ms = dispatch_floor_ms(plan, d_codes, rows, hip_args, Launcher)
+    traffic, traffic_rows = load_traffic(kname)
+    if traffic is not None and traffic_rows:
+        traffic = traffic * rows / traffic_rows
+    working_set = bpr * rows * nb
+    result = {
+        "metric": METRIC,
+        "value": rows * world * args.steps / elapsed,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (forward-sampled munin evidence rows, seed 42+rank)",
+        "config": {
+            "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, fused row plan; "
+                        "one step = one 100k-row batch posted to the resident ring launch (pgm_rows_ring_*), "
+                        "batches resident in HBM, batch i on buffer set i % batches",
+            "launch": "one resident launch per timed region (started inside the window), K batches posted",
+            "network": "munin",
+            "missing": variables,
+            "rows_per_gpu_per_step": rows,
+            "global_rows_per_step": rows * world,
+            "batches": nb,
+            "parallelism": f"rows sharded over {world} GPU(s), no data-path collective",
+            "plan": plan.describe(),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            # the same algorithmic bytes over the driver-visible wall time per step (window includes
+            # the launch, the posts and the closing synchronize)
+            "frac_wall": bpr * rows / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": kname,
+            "kernel_ms": kern_ms,
+            "kernel_span_ms": kern_ms * args.steps,
+            "grid": {"blocks": k_blocks, "workgroup": k_wg},
+            "dispatch_floor_ms": floor_ms,
+            "single_launch_kernel_ms": single_ms,
+            "algorithmic_bytes_per_row": bpr,
+            "bytes_per_launch": bpr * rows * args.steps,
+            "bytes_per_step": bpr * rows,
+            "working_set_bytes": working_set,
+            "working_set_exceeds_mall": working_set > MALL_BYTES,
+        },
+    }
+    if rank == 0:
+        n_chk = max(16, 64 // nb)
+        checks = [parity_spot_check(model, missing, plan, outs[i], codes_all[:, perms[i][:n_chk]], nodes,
+                                    n_check=n_chk) for i in range(nb)]
+        result["parity"] = {"rows_checked": sum(c["rows_checked"] for c in checks), "batches_checked": nb,
+                            "max_rel_err": max(c["max_rel_err"] for c in checks),
+                            "ok": all(c["ok"] for c in checks)}
+        if world == 1 and args.cpu_pre is not None:
+            result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
+            result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
+    del ring
     return result
 
 
@@ -910,8 +1025,9 @@ def main():
                          "(batch i on queue i %% Q; <= --batches)")
     ap.add_argument("--acquire-in-window", action="store_true",
                     help="c3 (A/B): leave each queue's first system-scope acquire inside the timed window")
-    ap.add_argument("--launch", default="direct", choices=["direct", "hip"],
-                    help="c3/c5: AQL packets on a user-mode HSA queue (direct) or hipModuleLaunchKernel (hip)")
+    ap.add_argument("--launch", default="direct", choices=["direct", "hip", "ring"],
+                    help="c3/c5: AQL packets on a user-mode HSA queue (direct), hipModuleLaunchKernel (hip); "
+                         "c3: batches posted to one resident launch (ring)")
     args = ap.parse_args()
     if args.rows is None:
         args.rows = {"c3": 100_000, "c5": 1_000_000}.get(args.workload, 1000)

@@ -401,6 +401,36 @@ int pgm_rows_bound_destroy(void *bound);
  * per thread, 16-B stores), "pgm_rows_floor" / "pgm_rows_floor2" (PGM_ROWS_FLOOR), or "" (an AOT kernel), with its grid and workgroup size */
 int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
 
+/* Resident ring of row batches (streaming predict_probability / predict): one launch of the
+ * plan-specialised two-rows-per-lane kernel ("pgm_rows_ring") stays resident while the host publishes
+ * batches, so consecutive batches overlap on the chip instead of each paying a dispatch.  Replaces the
+ * reference's per-batch caller loop (pgmpy/models/DiscreteBayesianNetwork.py:867-910, 912-989) for a
+ * stream of equally sized batches.
+ *   create: n_slots buffer sets; batch b reads codes[b % n_slots] (rows [row0, row0 + n_rows), leading
+ *           dim ld_codes) and writes marg / map / gap[b % n_slots] (leading dim ld_out), as
+ *           pgm_rows_plan_run.  mode: PGM_ROWS_MARGINALS | PGM_ROWS_MAP | PGM_ROWS_MAPGAP only; the
+ *           two-rows-per-lane contract holds per slot (even n_rows / row0 / leading dims, 16-B aligned
+ *           outputs) else PGM_EINVAL.  Needs the plan-specialised kernel (hipRTC).
+ *   start:  launches the resident grid on `stream` for n_batches batches (the ring must not be
+ *           running); waves that reach a batch not yet posted wait, and give up after timeout_s
+ *           seconds (PGM_EDEVICE from finish).
+ *   post:   publishes batches [0, n_posted) (monotone, <= n_batches).  A batch's inputs must be
+ *           complete in device memory, and its slot's previous batch finished, before it is posted.
+ *   finish: all n_batches posted -> waits for the launch (stream synchronize) and checks it.
+ *   cancel: stops the launch early (waves exit at their next unposted batch) and waits.
+ * Outputs of batch b equal pgm_rows_plan_run's on the same rows bit for bit. */
+int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint8_t *const *codes,
+                         const int64_t *ld_codes, const int64_t *row0, int64_t n_rows, double *const *marg,
+                         int64_t ld_out, int32_t *const *map, double *const *gap, int32_t *err_flag, void *stream,
+                         void **ring);
+int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s);
+int pgm_rows_ring_post(void *ring, uint32_t n_posted);
+int pgm_rows_ring_finish(void *ring);
+int pgm_rows_ring_cancel(void *ring);
+/* the ring's kernel name ("pgm_rows_ring"), resident grid and workgroup size */
+int pgm_rows_ring_kernel(void *ring, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
+int pgm_rows_ring_destroy(void *ring);
+
 /* Direct AQL dispatch (pgmpy_amd/csrc/pgmdq.cpp).  A user-mode HSA queue on the GPU agent of a HIP
  * device; a bound launch of the plan-specialised kernel (pgm_rows_plan_bind) is re-bound to it and
  * each pgm_dq_launch writes one kernel-dispatch packet (barrier bit set) and rings the doorbell — no

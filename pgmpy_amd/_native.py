@@ -200,6 +200,17 @@ _SIGS = {
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
     "pgm_rows_bound_kernel": ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                                ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "pgm_rows_ring_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64),
+                              ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.POINTER(_P), ctypes.c_int64,
+                              ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P, ctypes.POINTER(ctypes.c_void_p)],
+                             ctypes.c_int),
+    "pgm_rows_ring_start": ([_P, ctypes.c_uint32, ctypes.c_double], ctypes.c_int),
+    "pgm_rows_ring_post": ([_P, ctypes.c_uint32], ctypes.c_int),
+    "pgm_rows_ring_finish": ([_P], ctypes.c_int),
+    "pgm_rows_ring_cancel": ([_P], ctypes.c_int),
+    "pgm_rows_ring_kernel": ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
+                              ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "pgm_rows_ring_destroy": ([_P], ctypes.c_int),
     "pgm_codes_remap": ([_P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32, _P, _P,
                          ctypes.c_int64, _P, _P, _P, _P, _P], ctypes.c_int),
     "pgm_sample_joint": ([_P, ctypes.c_int64, ctypes.c_int64, _P, _P, ctypes.c_int64, _P, _P], ctypes.c_int),

@@ -34,7 +34,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 13  // 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 14  // 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -1764,6 +1764,7 @@ struct RowsHandle {
   hipFunction_t jit_fn2 = nullptr;  // two rows per thread
   hipFunction_t jit_fn_floor = nullptr;  // PGM_ROWS_FLOOR: the same dispatch's loads + stores only
   hipFunction_t jit_fn_floor2 = nullptr;  // ... of the two-rows-per-thread dispatch
+  hipFunction_t jit_fn_ring = nullptr;    // the resident ring kernel (pgm_rows_ring_*)
   std::vector<char> jit_code;         // the compiled code object (the direct AQL path loads it again)
   bool jit_write_through = false;     // its output stores are write-through (jit_store() == 2)
 };
@@ -2332,6 +2333,24 @@ static int jit_store() {
   return m;
 }
 
+// workgroup size of the ring kernel (knob PGM_RING_WG, a multiple of 64 <= 1024): 256 = one wave per
+// SIMD per workgroup; the loop around the two-row body takes ~147 VGPRs (3 waves per SIMD), so three
+// workgroups are resident per CU (a 1,024-thread bound caps it at 128 VGPRs and spills to scratch;
+// 512 threads fit one workgroup per CU)
+static int ring_wg() {
+  static const int wg = [] {
+    const char *e = getenv("PGM_RING_WG");
+    const int v = e ? atoi(e) : 256;
+    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 256;
+  }();
+  return wg;
+}
+
+static std::vector<int> rows_cols(const pgm_rows_plan *pl);
+static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R);
+static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, const std::vector<int> &cols,
+                              const char *leave);
+
 // R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
 static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
@@ -2355,9 +2374,28 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
     pgmi_appendf(o, "  __shared__ double S[%d];\n", K * WG);
     for (int i = 0; i < K; ++i) pgmi_appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
   }
-  std::vector<int> cols;  // distinct evidence columns, each loaded once per row
+  const std::vector<int> cols = rows_cols(pl);
+  emit_rows_code_loads(o, cols, R);
+  if (lds) {
+    for (int i = 0; i < K; ++i) pgmi_appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
+    o += "  __syncthreads();\n#define VAL(i) S[i]\n";
+  } else {
+    o += "#define VAL(i) V[i]\n";
+  }
+  emit_rows_compute(o, pl, R, cols, "return");
+  o += "}\n#undef VAL\n";
+}
+
+// the distinct evidence columns of a plan, each loaded once per row
+static std::vector<int> rows_cols(const pgm_rows_plan *pl) {
+  std::vector<int> cols;
   for (int j = 0; j < pl->n_ev; ++j)
     if (std::find(cols.begin(), cols.end(), pl->ev_col[j]) == cols.end()) cols.push_back(pl->ev_col[j]);
+  return cols;
+}
+
+// the row's evidence codes (row rc of the columns at C + row0, leading dimension ldc): e<i>_<u>
+static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R) {
   if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + rc;\n";
   for (size_t i = 0; i < cols.size(); ++i) {
     if (R == 1) {
@@ -2367,12 +2405,13 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
       pgmi_appendf(o, "  const unsigned e%zu_0 = w%zu & 255u, e%zu_1 = w%zu >> 8;\n", i, i, i, i);
     }
   }
-  if (lds) {
-    for (int i = 0; i < K; ++i) pgmi_appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
-    o += "  __syncthreads();\n#define VAL(i) S[i]\n";
-  } else {
-    o += "#define VAL(i) V[i]\n";
-  }
+}
+
+// the row's sum-product, normalisation and stores (r, rc, n, M, ldo, MP, G, E, mode, rsM / rsG and the
+// loaded codes in scope; VAL(i) = CPT value i); rows past n leave through `leave` ("return" in a grid
+// kernel, "break" inside the ring kernel's do-while)
+static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, const std::vector<int> &cols,
+                              const char *leave) {
   o += "  unsigned bad = 0u;\n";
   const int NC = pl->n_comp;
   for (int u = 0; u < R; ++u) {
@@ -2410,7 +2449,7 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
     }
     pgmi_appendf(o, ";\n  const bool dead_%d = !(z_%d > 0.0);\n", u, u);
   }
-  o += "  if (bad && r < n && E) atomicOr(E, 1);\n  if (r >= n) return;\n";
+  pgmi_appendf(o, "  if (bad && r < n && E) atomicOr(E, 1);\n  if (r >= n) %s;\n", leave);
   o += "  if (mode & 1) {\n";
   for (int c = 0; c < NC; ++c) {
     const int lb = pl->comp_loop_begin[c], nq = pl->comp_n_query[c];
@@ -2457,17 +2496,106 @@ static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const bool wt = jit_store() == 2;
   if (R == 1 && wt) {
     o += "    if (MP) PGM_WT4(int, &MP[r], dead_0 ? 0 : m_0);\n"
-         "    if ((mode & 8) && G) PGM_WT8(double, &G[r], dead_0 ? 0.0 : mg_0);\n  }\n}\n";
+         "    if ((mode & 8) && G) PGM_WT8(double, &G[r], dead_0 ? 0.0 : mg_0);\n  }\n";
   } else if (R == 1) {
-    o += "    if (MP) MP[r] = dead_0 ? 0 : m_0;\n    if ((mode & 8) && G) G[r] = dead_0 ? 0.0 : mg_0;\n  }\n}\n";
+    o += "    if (MP) MP[r] = dead_0 ? 0 : m_0;\n    if ((mode & 8) && G) G[r] = dead_0 ? 0.0 : mg_0;\n  }\n";
   } else if (wt) {
     o += "    if (MP) PGM_WT8(unsigned long long, (unsigned long long *)(MP + r), "
          "((unsigned long long)(unsigned)(dead_1 ? 0 : m_1) << 32) | (unsigned)(dead_0 ? 0 : m_0));\n";
-    o += "    if ((mode & 8) && G) PGM_WT16(rsG, r, dead_0 ? 0.0 : mg_0, dead_1 ? 0.0 : mg_1);\n  }\n}\n";
+    o += "    if ((mode & 8) && G) PGM_WT16(rsG, r, dead_0 ? 0.0 : mg_0, dead_1 ? 0.0 : mg_1);\n  }\n";
   } else {
     o += "    if (MP) *(int2 *)(MP + r) = make_int2(dead_0 ? 0 : m_0, dead_1 ? 0 : m_1);\n";
-    o += "    if ((mode & 8) && G) *(double2 *)(G + r) = make_double2(dead_0 ? 0.0 : mg_0, dead_1 ? 0.0 : mg_1);\n  }\n}\n";
+    o += "    if ((mode & 8) && G) *(double2 *)(G + r) = make_double2(dead_0 ? 0.0 : mg_0, dead_1 ? 0.0 : mg_1);\n  }\n";
   }
+}
+
+// ---------------------------------------------------------------------------------------- ring kernel
+// pgm_rows_ring: the plan-specialised two-rows-per-thread body run by a RESIDENT grid over a stream of
+// row batches (pgm_rows_ring_*).  One launch consumes n_batches batches of n rows; batch b reads and
+// writes the buffers of slot b % n_slots (descriptor table D in device memory).  The host publishes
+// batches by raising a counter in pinned host memory (ctl[0] = batches posted); the launch may start
+// before the first post.  Work item = 128 rows (one wave, two rows per lane) of one batch; item j
+// goes to wave j mod W (W = resident waves), so consecutive batches overlap across the chip instead of
+// each paying a dispatch.  A wave about to start a batch not yet known to be posted reads the count
+// its workgroup last saw (LDS); if that is stale one wave per workgroup (an LDS token) polls the host
+// counter with a system-scope acquire and publishes it, the others sleep on LDS.  Exit conditions
+// every wave reaches: all items done; ctl[1] (cancel) set by the host; or `timeout` ticks of the
+// constant 100 MHz wall clock without the needed batch (ctl[2] |= 2).  The CPT values are staged in
+// LDS once per workgroup for the whole stream.
+static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
+  const int NV = pl->n_values + 1;
+  const int WG = ring_wg();
+  const int K = (NV + WG - 1) / WG;
+  o += "struct pgm_ring_slot { const unsigned char *C; long long ldc, row0; double *M; long long ldo; int *MP; "
+       "double *G; long long pad; };\n";
+  pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_ring(const double *__restrict__ V, "
+             "const pgm_ring_slot *__restrict__ D, unsigned n_slots, unsigned *ctl, unsigned n_batches, long long n, "
+             "int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
+  o += "  const int t = threadIdx.x;\n";
+  pgmi_appendf(o, "  __shared__ double S[%d];\n  __shared__ unsigned seen_s, token_s, stop_s;\n", K * WG);
+  for (int i = 0; i < K; ++i) pgmi_appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
+  for (int i = 0; i < K; ++i) pgmi_appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
+  o += "  if (t == 0) { seen_s = 0u; token_s = 0u; stop_s = 0u; }\n  __syncthreads();\n#define VAL(i) S[i]\n";
+  pgmi_appendf(o, "  const unsigned long long W = (unsigned long long)gridDim.x * %d;\n", WG / 64);
+  pgmi_appendf(o, "  const unsigned long long wv0 = (unsigned long long)blockIdx.x * %d + (t >> 6);\n", WG / 64);
+  o += "  const unsigned long long chunks = (unsigned long long)(n + 127) / 128;\n"
+       "  const unsigned long long items = chunks * n_batches;\n"
+       "  const unsigned long long t0 = wall_clock64();\n"
+       "  unsigned seen = 0u;\n"
+       "  for (unsigned long long j = wv0; j < items; j += W) {\n"
+       "    const unsigned bt = (unsigned)(j / chunks);\n"
+       "    bool stop = false;\n"
+       "    while (bt >= seen) {\n"
+       "      const unsigned sl = __hip_atomic_load(&seen_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "      if (sl > seen) { seen = sl; continue; }\n"
+       "      if (__hip_atomic_load(&stop_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }\n"
+       "      unsigned mine = 0u;\n"
+       "      if ((t & 63) == 0) mine = atomicCAS(&token_s, 0u, 1u) == 0u ? 1u : 0u;\n"
+       "      mine = __builtin_amdgcn_readfirstlane(mine);\n"
+       "      if (mine) {\n"
+       "        for (;;) {\n"
+       "          const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "          if (p > bt) {\n"
+       "            seen = p;\n"
+       "            if ((t & 63) == 0) atomicMax(&seen_s, p);\n"
+       "            break;\n"
+       "          }\n"
+       "          const bool cancel = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;\n"
+       "          const bool late = wall_clock64() - t0 > timeout;\n"
+       "          if (cancel || late) {\n"
+       "            if ((t & 63) == 0) {\n"
+       "              if (late) __hip_atomic_fetch_or(&ctl[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "              atomicExch(&stop_s, 1u);\n"
+       "            }\n"
+       "            stop = true;\n"
+       "            break;\n"
+       "          }\n"
+       "          __builtin_amdgcn_s_sleep(4);\n"
+       "        }\n"
+       "        if ((t & 63) == 0) atomicExch(&token_s, 0u);\n"
+       "        if (stop) break;\n"
+       "      } else {\n"
+       "        if (wall_clock64() - t0 > timeout) { stop = true; break; }\n"
+       "        __builtin_amdgcn_s_sleep(2);\n"
+       "      }\n"
+       "    }\n"
+       "    if (stop) break;\n"
+       "    const pgm_ring_slot d = D[bt % n_slots];\n"
+       "    const unsigned char *__restrict__ C = d.C;\n"
+       "    const long long ldc = d.ldc, row0 = d.row0, ldo = d.ldo;\n"
+       "    double *__restrict__ M = d.M;\n"
+       "    int *__restrict__ MP = d.MP;\n"
+       "    double *__restrict__ G = d.G;\n"
+       "    const long long r = (long long)(j - (unsigned long long)bt * chunks) * 128 + (t & 63) * 2;\n"
+       "    const long long rc = r < n ? r : n - 2;\n";
+  if (jit_store() == 2)
+    o += "    const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(M, 0, 0x7fffffff, 0x00020000);\n"
+         "    const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc(G, 0, 0x7fffffff, 0x00020000);\n";
+  o += "    do {\n";
+  const std::vector<int> cols = rows_cols(pl);
+  emit_rows_code_loads(o, cols, 2);
+  emit_rows_compute(o, pl, 2, cols, "break");
+  o += "    } while (0);\n  }\n}\n#undef VAL\n";
 }
 
 // the dispatch floor of a plan (PGM_ROWS_FLOOR, measurement only): the row kernel's grid (R rows per
@@ -2537,10 +2665,16 @@ static std::string rows_jit_source(const pgm_rows_plan *pl) {
   emit_rows_floor(o, pl, 1);
   o += "\n";
   emit_rows_floor(o, pl, 2);
+  o += "\n";
+  emit_rows_ring(o, pl);
   return o;
 }
 
-// the two-rows-per-thread kernel's alignment contract (else the one-row kernel runs)
+static bool rows2_aligned(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
+                          const double *marg, int64_t ld_out, const int32_t *map, const double *gap, int n_marg);
+
+// whether a launch runs the two-rows-per-thread kernel: big enough, and its alignment contract holds
+// (else the one-row kernel runs)
 static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
                          const double *marg, int64_t ld_out, const int32_t *map, const double *gap, int n_marg) {
   static const bool off = getenv("PGM_NO_JIT2") != nullptr;  // testing / tuning
@@ -2548,7 +2682,14 @@ static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, i
   // and, since the 512-thread workgroups and concurrent queues, at 100k rows too (one queue: equal,
   // 3.9 us; four queues: 2.7 -> 2.1 us per launch of GPU span, r02br); one row below 50k rows
   static const int64_t min_rows = getenv("PGM_JIT2_MIN_ROWS") ? atoll(getenv("PGM_JIT2_MIN_ROWS")) : 50000;
-  if (off || n_rows < min_rows || n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
+  if (off || n_rows < min_rows) return false;
+  return rows2_aligned(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, n_marg);
+}
+
+// the alignment / addressing contract of the two-rows-per-lane body (pgm_rows_jit2, pgm_rows_ring)
+static bool rows2_aligned(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
+                          const double *marg, int64_t ld_out, const int32_t *map, const double *gap, int n_marg) {
+  if (n_rows % 2 || ld_codes % 2 || row0 % 2 || ((uintptr_t)codes & 1)) return false;
   if ((mode & PGM_ROWS_MARGINALS) && (((uintptr_t)marg & 15) || ld_out % 2)) return false;
   if (map && ((uintptr_t)map & 7)) return false;
   if ((mode & PGM_ROWS_MAPGAP) && gap && ((uintptr_t)gap & 15)) return false;
@@ -2579,7 +2720,8 @@ static bool rows_jit_ready(RowsHandle *h) {
   if (hipModuleGetFunction(&h->jit_fn, h->jit_mod, "pgm_rows_jit") != hipSuccess ||
       hipModuleGetFunction(&h->jit_fn2, h->jit_mod, "pgm_rows_jit2") != hipSuccess ||
       hipModuleGetFunction(&h->jit_fn_floor, h->jit_mod, "pgm_rows_floor") != hipSuccess ||
-      hipModuleGetFunction(&h->jit_fn_floor2, h->jit_mod, "pgm_rows_floor2") != hipSuccess) {
+      hipModuleGetFunction(&h->jit_fn_floor2, h->jit_mod, "pgm_rows_floor2") != hipSuccess ||
+      hipModuleGetFunction(&h->jit_fn_ring, h->jit_mod, "pgm_rows_ring") != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -3752,6 +3894,192 @@ int pgm_rows_bound_destroy(void *bound) {
   STALE_PROBE();
   delete (RowsBound *)bound;
   return PGM_OK;
+}
+
+// ---------------------------------------------------------------------------- resident ring of batches
+struct PgmRingSlot {  // pgm_ring_slot of the generated source (64 B)
+  const uint8_t *C;
+  int64_t ldc, row0;
+  double *M;
+  int64_t ldo;
+  int32_t *MP;
+  double *G;
+  int64_t pad;
+};
+static_assert(sizeof(PgmRingSlot) == 64, "ring slot layout");
+
+struct RowsRing {
+  RowsHandle *h = nullptr;
+  int32_t mode = 0;
+  int64_t n_rows = 0;
+  uint32_t n_slots = 0;
+  PgmRingSlot *d_slots = nullptr;  // device
+  unsigned *ctl = nullptr;         // pinned host: [0] batches posted, [1] cancel, [2] status (|2: timed out)
+  unsigned *ctl_dev = nullptr;     // its device address
+  int32_t *err = nullptr;
+  hipStream_t stream = nullptr;
+  unsigned blocks = 0;
+  bool running = false;
+  uint32_t n_batches = 0, posted = 0;
+};
+
+int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint8_t *const *codes,
+                         const int64_t *ld_codes, const int64_t *row0, int64_t n_rows, double *const *marg,
+                         int64_t ld_out, int32_t *const *map, double *const *gap, int32_t *err_flag, void *stream,
+                         void **ring) {
+  STALE_PROBE();
+  if (!ring) return fail(PGM_EINVAL, "rows_ring_create: null output pointer");
+  *ring = nullptr;
+  RowsHandle *h = (RowsHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "rows_ring_create: null plan");
+  if (n_slots < 1 || !codes || !ld_codes || !row0) return fail(PGM_EINVAL, "rows_ring_create: no slots");
+  if (n_rows < 2) return fail(PGM_EINVAL, "rows_ring_create: n_rows %lld < 2", (long long)n_rows);
+  if (mode & ~(PGM_ROWS_MARGINALS | PGM_ROWS_MAP | PGM_ROWS_MAPGAP))
+    return fail(PGM_EINVAL, "rows_ring_create: the ring runs marginals / MAP / MAP-gap outputs only");
+  if (!(mode & (PGM_ROWS_MARGINALS | PGM_ROWS_MAP | PGM_ROWS_MAPGAP)))
+    return fail(PGM_EINVAL, "rows_ring_create: no output requested");
+  if (!rows_jit_ready(h)) return fail(PGM_EINVAL, "rows_ring_create: the ring needs the plan-specialised (hipRTC) kernel");
+  std::vector<PgmRingSlot> slots((size_t)n_slots);
+  for (int32_t i = 0; i < n_slots; ++i) {
+    double *m = (mode & PGM_ROWS_MARGINALS) ? (marg ? marg[i] : nullptr) : nullptr;
+    int32_t *mp = (mode & (PGM_ROWS_MAP | PGM_ROWS_MAPGAP)) && map ? map[i] : nullptr;
+    double *g = (mode & PGM_ROWS_MAPGAP) && gap ? gap[i] : nullptr;
+    if ((mode & PGM_ROWS_MARGINALS) && !m) return fail(PGM_EINVAL, "rows_ring_create: slot %d has no marginal buffer", i);
+    if ((mode & PGM_ROWS_MAP) && !mp) return fail(PGM_EINVAL, "rows_ring_create: slot %d has no MAP buffer", i);
+    if ((mode & PGM_ROWS_MAPGAP) && !g) return fail(PGM_EINVAL, "rows_ring_create: slot %d has no MAP-gap buffer", i);
+    if (h->max_nt > 0 && !codes[i]) return fail(PGM_EINVAL, "rows_ring_create: slot %d has no evidence codes", i);
+    if ((mode & PGM_ROWS_MARGINALS) && ld_out < n_rows)
+      return fail(PGM_EINVAL, "rows_ring_create: ld_out %lld < n_rows %lld", (long long)ld_out, (long long)n_rows);
+    if (!rows2_aligned(mode, codes[i], ld_codes[i], row0[i], n_rows, m, ld_out, mp, g, h->k.n_marg))
+      return fail(PGM_EINVAL, "rows_ring_create: slot %d breaks the two-rows-per-lane contract (even rows, row0 and "
+                  "leading dimensions, 16-B aligned outputs)", i);
+    slots[i] = PgmRingSlot{codes[i], ld_codes[i], row0[i], m, ld_out, mp, g, 0};
+  }
+  RowsRing *rg = new (std::nothrow) RowsRing;
+  if (!rg) return fail(PGM_ENOMEM, "rows_ring_create: out of host memory");
+  rg->h = h;
+  rg->mode = mode;
+  rg->n_rows = n_rows;
+  rg->n_slots = (uint32_t)n_slots;
+  rg->err = err_flag;
+  rg->stream = S(stream);
+  hipError_t e = hipMalloc((void **)&rg->d_slots, sizeof(PgmRingSlot) * slots.size());
+  if (e == hipSuccess)
+    e = hipMemcpy(rg->d_slots, slots.data(), sizeof(PgmRingSlot) * slots.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&rg->ctl, 64, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&rg->ctl_dev, rg->ctl, 0);
+  int dev = 0, cus = 0, per_cu = 0;
+  if (e == hipSuccess) e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess)
+    e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn_ring, ring_wg(), 0);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    if (rg->d_slots) (void)hipFree(rg->d_slots);
+    if (rg->ctl) (void)hipHostFree(rg->ctl);
+    delete rg;
+    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_ring_create: %s", hipGetErrorString(e));
+  }
+  memset(rg->ctl, 0, 64);
+  // every workgroup resident at once (one per CU at the default 1,024 threads)
+  rg->blocks = (unsigned)std::max(1, cus * std::max(1, per_cu));
+  *ring = rg;
+  return PGM_OK;
+}
+
+int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
+  STALE_PROBE();
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg) return fail(PGM_EINVAL, "rows_ring_start: null ring");
+  if (rg->running) return fail(PGM_EINVAL, "rows_ring_start: the ring is running (finish or cancel it first)");
+  if (!(timeout_s > 0.0) || timeout_s > 600.0) return fail(PGM_EINVAL, "rows_ring_start: timeout must be in (0, 600] s");
+  int dev = 0, khz = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;
+  unsigned long long ticks = (unsigned long long)(timeout_s * (double)khz * 1000.0);
+  __atomic_store_n(&rg->ctl[0], 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&rg->ctl[1], 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&rg->ctl[2], 0u, __ATOMIC_SEQ_CST);
+  rg->n_batches = n_batches;
+  rg->posted = 0;
+  if (n_batches == 0) return PGM_OK;
+  const double *v = rg->h->d_values;
+  const PgmRingSlot *d = rg->d_slots;
+  unsigned ns = rg->n_slots, nb = n_batches;
+  unsigned *ctl = rg->ctl_dev;
+  long long n = rg->n_rows;
+  int32_t *ef = rg->err;
+  int32_t md = rg->mode;
+  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, &nb, &n, (void *)&ef, &md, &ticks};
+  HIP_TRY(hipModuleLaunchKernel(rg->h->jit_fn_ring, rg->blocks, 1, 1, (unsigned)ring_wg(), 1, 1, 0, rg->stream, args,
+                                nullptr));
+  rg->running = true;
+  return PGM_OK;
+}
+
+int pgm_rows_ring_post(void *ring, uint32_t n_posted) {
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg) return fail(PGM_EINVAL, "rows_ring_post: null ring");
+  if (!rg->running) return fail(PGM_EINVAL, "rows_ring_post: the ring is not running");
+  if (n_posted < rg->posted || n_posted > rg->n_batches)
+    return fail(PGM_EINVAL, "rows_ring_post: %u batches posted, %u started, asked for %u", rg->posted, rg->n_batches,
+                n_posted);
+  rg->posted = n_posted;
+  // a sequentially consistent store: drained from the store buffer before this call returns
+  __atomic_store_n(&rg->ctl[0], n_posted, __ATOMIC_SEQ_CST);
+  return PGM_OK;
+}
+
+static int ring_wait(RowsRing *rg) {
+  HIP_TRY(hipStreamSynchronize(rg->stream));
+  rg->running = false;
+  return PGM_OK;
+}
+
+int pgm_rows_ring_finish(void *ring) {
+  STALE_PROBE();
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg) return fail(PGM_EINVAL, "rows_ring_finish: null ring");
+  if (!rg->running) return PGM_OK;
+  if (rg->posted < rg->n_batches)
+    return fail(PGM_EINVAL, "rows_ring_finish: only %u of %u batches posted (post them or cancel)", rg->posted,
+                rg->n_batches);
+  const int st = ring_wait(rg);
+  if (st != PGM_OK) return st;
+  if (__atomic_load_n(&rg->ctl[2], __ATOMIC_SEQ_CST) & 2u)
+    return fail(PGM_EDEVICE, "rows_ring_finish: the resident kernel timed out waiting for a batch");
+  return PGM_OK;
+}
+
+int pgm_rows_ring_cancel(void *ring) {
+  STALE_PROBE();
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg) return fail(PGM_EINVAL, "rows_ring_cancel: null ring");
+  if (!rg->running) return PGM_OK;
+  __atomic_store_n(&rg->ctl[1], 1u, __ATOMIC_SEQ_CST);
+  return ring_wait(rg);
+}
+
+int pgm_rows_ring_kernel(void *ring, char *name, size_t cap, uint32_t *blocks, uint32_t *wg) {
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg || !name || cap == 0) return fail(PGM_EINVAL, "rows_ring_kernel: null argument");
+  snprintf(name, cap, "%s", "pgm_rows_ring");
+  if (blocks) *blocks = rg->blocks;
+  if (wg) *wg = (uint32_t)ring_wg();
+  return PGM_OK;
+}
+
+int pgm_rows_ring_destroy(void *ring) {
+  STALE_PROBE();
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg) return PGM_OK;
+  int st = PGM_OK;
+  if (rg->running) st = pgm_rows_ring_cancel(rg);
+  if (rg->d_slots) (void)hipFree(rg->d_slots);
+  if (rg->ctl) (void)hipHostFree(rg->ctl);
+  delete rg;
+  return st;
 }
 
 // internal (pgm_internal.h): what the direct AQL path (pgmdq.cpp) needs to dispatch a bound

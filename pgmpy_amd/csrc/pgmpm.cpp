@@ -52,11 +52,27 @@ static std::string rtc_cache_dir() {
   return dir;
 }
 
+static const char *const kRtcOpts[] = {"--offload-arch=gfx950", "-O3"};
+
+// what else decides the code object besides the source: the hipRTC (compiler) version, the target
+// and the options; folded into the cache key so an upgraded compiler never reuses an old object
+static const std::string &rtc_toolchain_tag() {
+  static const std::string tag = [] {
+    int major = 0, minor = 0;
+    if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) major = minor = -1;
+    std::string t = "hiprtc " + std::to_string(major) + "." + std::to_string(minor);
+    for (const char *o : kRtcOpts) t += std::string(" ") + o;
+    return t;
+  }();
+  return tag;
+}
+
 static std::string rtc_cache_path(const std::string &src) {
   const std::string dir = rtc_cache_dir();
   if (dir.empty()) return dir;
-  uint64_t h = 1469598103934665603ull;  // FNV-1a over the source and the ABI version
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the source, the toolchain tag and the ABI version
   for (unsigned char c : src) h = (h ^ c) * 1099511628211ull;
+  for (unsigned char c : rtc_toolchain_tag()) h = (h ^ c) * 1099511628211ull;
   h = (h ^ (uint64_t)pgm_version()) * 1099511628211ull;
   char name[64];
   snprintf(name, sizeof name, "/k%016llx.co", (unsigned long long)h);
@@ -101,7 +117,9 @@ static void rtc_cache_store(const std::string &path, const std::string &src, con
 // gfx950 code object of a specialised kernel source: the disk cache, else hipRTC (then cached)
 bool pgmi_rtc_code(const std::string &src, const char *what, std::vector<char> &code) {
   const std::string path = rtc_cache_path(src);
-  if (rtc_cache_load(path, src, code)) return true;
+  // the stored header holds the toolchain tag and the source; both must match on load
+  const std::string keyed = rtc_toolchain_tag() + "\n" + src;
+  if (rtc_cache_load(path, keyed, code)) return true;
   // hipRTC programs compile concurrently from several threads (pgm_pm_prepare); PGM_RTC_SERIAL=1
   // serialises every compile
   static const bool serial = getenv("PGM_RTC_SERIAL") && atoi(getenv("PGM_RTC_SERIAL")) != 0;
@@ -109,8 +127,7 @@ bool pgmi_rtc_code(const std::string &src, const char *what, std::vector<char> &
   if (serial) lk.lock();
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "pgm_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return false;
-  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+  if (hiprtcCompileProgram(prog, (int)(sizeof kRtcOpts / sizeof kRtcOpts[0]), (const char **)kRtcOpts) != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
     std::string log(n, '\0');
@@ -124,7 +141,7 @@ bool pgmi_rtc_code(const std::string &src, const char *what, std::vector<char> &
   code.resize(sz);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
-  rtc_cache_store(path, src, code);
+  rtc_cache_store(path, keyed, code);
   return true;
 }
 

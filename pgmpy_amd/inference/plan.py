@@ -345,6 +345,15 @@ class PatternPlan:
         self._build_fused()
         return BoundRows(self, codes, ld, row0, n_rows, out, err, stream, floor=floor)
 
+    def ring(self, slots, n_rows, err=None, stream=None):
+        """A resident ring over equally sized row batches (pgm_rows_ring_*): slots = [(codes, ld, row0,
+        out), ...]; batch b reads rows [row0, row0 + n_rows) of slot b % len(slots)'s codes and writes
+        its outputs (marginal / MAP / gap dicts from alloc_outputs, one per slot).  See RowRing."""
+        if self.kind != "fused":
+            raise ValueError("ring(): fused plans only")
+        self._build_fused()
+        return RowRing(self, slots, n_rows, err, stream)
+
     def _dev_factors(self):
         if not hasattr(self, "_dev_cache"):
             self._dev_cache = [(cpd._d(), vars_) for vars_, cpd in self.factors]
@@ -586,6 +595,91 @@ class BoundRows:
         if h is not None and h.value:
             try:
                 N.load_library().pgm_rows_bound_destroy(h)
+            except Exception:
+                pass
+
+
+class RowRing:
+    """One resident launch of the plan-specialised row kernel consuming a stream of row batches
+    (pgm_rows_ring_*; DESIGN.md "Resident ring").  start(n) launches it for n batches, post(k) publishes
+    batches [0, k) (a batch's inputs must be complete on the device and its slot's previous batch
+    finished), finish() waits for the launch.  Outputs equal run()'s on the same rows bit for bit."""
+
+    def __init__(self, plan, slots, n_rows, err, stream):
+        import ctypes
+
+        L = N.lib()
+        slots = list(slots)
+        if not slots:
+            raise ValueError("RowRing: no slots")
+        outs = [s[3] for s in slots]
+        mode = plan._mode(outs[0])
+        if any(plan._mode(o) != mode for o in outs):
+            raise ValueError("RowRing: every slot needs the same outputs")
+        n = len(slots)
+        P = ctypes.c_void_p
+        codes = (P * n)(*[s[0].data_ptr() for s in slots])
+        lds = (ctypes.c_int64 * n)(*[int(s[1]) for s in slots])
+        row0 = (ctypes.c_int64 * n)(*[int(s[2]) for s in slots])
+
+        def ptrs(key):
+            if key not in outs[0]:
+                return None
+            return (P * n)(*[o[key].data_ptr() for o in outs])
+
+        ld_out = int(outs[0]["marg"].stride(0)) if "marg" in outs[0] else int(n_rows)
+        if "marg" in outs[0] and any(int(o["marg"].stride(0)) != ld_out for o in outs):
+            raise ValueError("RowRing: every slot's marginals need the same leading dimension")
+        h = ctypes.c_void_p()
+        N.check(L.pgm_rows_ring_create(plan._handle, mode, n, codes, lds, row0, int(n_rows), ptrs("marg"), ld_out,
+                                       ptrs("map"), ptrs("gap"), N.ptr(err), N.stream_handle(stream),
+                                       ctypes.byref(h)), "rows_ring_create")
+        self._keep = (plan, slots, err)
+        self._h = h
+        self._post = L.pgm_rows_ring_post
+        self.outs = outs
+        self.n_rows = int(n_rows)
+
+    def start(self, n_batches, timeout_s=5.0):
+        N.check(N.lib().pgm_rows_ring_start(self._h, int(n_batches), float(timeout_s)), "rows_ring_start")
+
+    def post(self, n_posted):
+        st = self._post(self._h, int(n_posted))
+        if st != 0:
+            N.check(st, "rows_ring_post")
+
+    def finish(self):
+        N.check(N.lib().pgm_rows_ring_finish(self._h), "rows_ring_finish")
+
+    def cancel(self):
+        N.check(N.lib().pgm_rows_ring_cancel(self._h), "rows_ring_cancel")
+
+    def kernel(self):
+        """(kernel name, resident blocks, workgroup size)."""
+        import ctypes
+
+        name = ctypes.create_string_buffer(64)
+        nb, wg = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().pgm_rows_ring_kernel(self._h, name, 64, ctypes.byref(nb), ctypes.byref(wg)),
+                "rows_ring_kernel")
+        return name.value.decode(), nb.value, wg.value
+
+    def run(self, n_batches, timeout_s=5.0):
+        """start + post every batch + finish (one resident launch over n_batches batches)."""
+        self.start(n_batches, timeout_s)
+        try:
+            for b in range(1, int(n_batches) + 1):
+                self.post(b)
+        except BaseException:
+            self.cancel()
+            raise
+        self.finish()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.load_library().pgm_rows_ring_destroy(h)
             except Exception:
                 pass
 

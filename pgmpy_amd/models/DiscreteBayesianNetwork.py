@@ -201,6 +201,16 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         return g
 
     # ------------------------------------------------------------------ junction tree
+    def to_markov_model(self):
+        """The moral graph with one potential per CPD (DiscreteBayesianNetwork.py:510-537)."""
+        from .DiscreteMarkovNetwork import DiscreteMarkovNetwork
+
+        moral = self.moralize()
+        mm = DiscreteMarkovNetwork(moral.edges())
+        mm.add_nodes_from(moral.nodes())
+        mm.add_factors(*[cpd.to_factor() for cpd in self.cpds])
+        return mm
+
     def to_junction_tree(self):
         """Junction tree with clique potentials = product of the CPDs assigned to each clique.
 

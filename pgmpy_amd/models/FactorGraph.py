@@ -97,6 +97,26 @@ class FactorGraph(nx.Graph):
         variable_nodes = self.get_variable_nodes()
         return list(set(self.nodes()) - set(variable_nodes))
 
+    def to_markov_model(self):
+        # FactorGraph.py:303-336: each factor's scope becomes a clique of the Markov network
+        from itertools import combinations
+
+        from .DiscreteMarkovNetwork import DiscreteMarkovNetwork
+
+        mm = DiscreteMarkovNetwork()
+        variable_nodes = self.get_variable_nodes()
+        if len(set(self.nodes()) - set(variable_nodes)) != len(self.factors):
+            raise ValueError("Factors not associated with all the factor nodes.")
+        mm.add_nodes_from(variable_nodes)
+        for factor in self.factors:
+            mm.add_edges_from(combinations(factor.scope(), 2))
+            mm.add_factors(factor)
+        return mm
+
+    def to_junction_tree(self):
+        # FactorGraph.py:338-361
+        return self.to_markov_model().to_junction_tree()
+
     def get_factors(self, node=None):
         # FactorGraph.py:363-397
         if node is None:

@@ -586,7 +586,174 @@ def gen_munin_c2():
     _dump("munin_c2_query.json", {"variables": q, "evidence": evidence, "result": _fac_json(r), "seconds": dt})
 
 
+# ----------------------------------------------------------------------------- Markov networks
+def _sorted_fac(phi):
+    """A factor as {variables sorted, values aligned to them} (hash-order independent)."""
+    order = sorted(phi.variables)
+    vals = np.asarray(phi.values, dtype=np.float64).transpose([phi.variables.index(v) for v in order])
+    return {"variables": order, "cardinality": [int(c) for c in vals.shape],
+            "values": [float(x) for x in vals.ravel()]}
+
+
+def _markov_case(mm, queries, maps, max_marginals, orders=None, bp=True, bp_queries=()):
+    """Run the reference on a DiscreteMarkovNetwork: VE greedy / explicit-order queries, map_query,
+    max_marginal, partition function, to_junction_tree structure, BP calibration and BP queries."""
+    from pgmpy.inference import BeliefPropagation, VariableElimination
+
+    ve = VariableElimination(mm)
+    out = {"nodes": sorted(mm.nodes()), "edges": sorted(sorted(e) for e in mm.edges()),
+           "factors": [_fac_json(f) for f in mm.factors], "queries": [], "maps": [], "max_marginals": []}
+    for variables, evidence in queries:
+        rec = {"variables": variables, "evidence": evidence,
+               "joint": _fac_json(ve.query(variables, evidence, show_progress=False)),
+               "separate": {k: _fac_json(v) for k, v in
+                            ve.query(variables, evidence, joint=False, show_progress=False).items()}}
+        if orders is not None:
+            elim = [v for v in orders if v not in variables and v not in evidence]
+            rec["order"] = elim
+            rec["joint_order"] = _fac_json(ve.query(variables, evidence, elimination_order=elim,
+                                                    show_progress=False))
+        out["queries"].append(rec)
+    for variables, evidence in maps:
+        r = ve.map_query(variables, evidence, show_progress=False)
+        out["maps"].append({"variables": variables, "evidence": evidence, "result": {k: str(v) for k, v in r.items()}})
+    for variables, evidence in max_marginals:
+        out["max_marginals"].append({"variables": variables, "evidence": evidence,
+                                     "result": float(ve.max_marginal(variables, evidence, show_progress=False))})
+    out["partition_function"] = float(mm.get_partition_function())
+    jt = mm.to_junction_tree()
+    out["jt_cliques"] = sorted(sorted(c) for c in jt.nodes())
+    out["jt_edges"] = sorted(sorted([sorted(a), sorted(b)]) for a, b in jt.edges())
+    if bp:
+        b = BeliefPropagation(mm)
+        b.calibrate()
+        out["bp_clique_beliefs"] = sorted(([sorted(c), _sorted_fac(v)] for c, v in b.get_clique_beliefs().items()),
+                                          key=lambda x: x[0])
+        out["bp_sepset_beliefs"] = sorted(([sorted(sorted(x) for x in k), _sorted_fac(v)]
+                                           for k, v in b.get_sepset_beliefs().items()), key=lambda x: x[0])
+        b2 = BeliefPropagation(mm)
+        b2.max_calibrate()
+        out["bp_max_clique_beliefs"] = sorted(([sorted(c), _sorted_fac(v)]
+                                               for c, v in b2.get_clique_beliefs().items()), key=lambda x: x[0])
+        out["bp_queries"] = []
+        for variables, evidence in bp_queries:
+            b3 = BeliefPropagation(mm)
+            q = b3.query(variables, evidence, show_progress=False)
+            m = BeliefPropagation(mm).map_query(variables, evidence, show_progress=False)
+            out["bp_queries"].append({"variables": variables, "evidence": evidence, "joint": _fac_json(q),
+                                      "map": {k: str(v) for k, v in m.items()}})
+    return out
+
+
+def gen_markov():
+    """DiscreteMarkovNetwork container, triangulation, junction tree and VE / BP over it
+    (pgmpy/models/DiscreteMarkovNetwork.py:16-882; test_ExactInference.py:639-889,
+    test_DiscreteMarkovNetwork.py:246-591)."""
+    from pgmpy.factors.discrete import DiscreteFactor, TabularCPD
+    from pgmpy.inference import VariableElimination
+    from pgmpy.models import DiscreteMarkovNetwork, FactorGraph
+
+    out = {}
+    # test_ExactInference.py:659-699: the moralised 6-node BN as a Markov network (SAMIAM values)
+    mm = DiscreteMarkovNetwork([("A", "J"), ("R", "J"), ("J", "Q"), ("J", "L"), ("G", "L"), ("A", "R"), ("J", "G")])
+    mm.add_factors(
+        TabularCPD("A", 2, values=[[0.2], [0.8]]).to_factor(),
+        TabularCPD("R", 2, values=[[0.4], [0.6]]).to_factor(),
+        TabularCPD("J", 2, values=[[0.9, 0.6, 0.7, 0.1], [0.1, 0.4, 0.3, 0.9]], evidence=["A", "R"],
+                   evidence_card=[2, 2]).to_factor(),
+        TabularCPD("Q", 2, values=[[0.9, 0.2], [0.1, 0.8]], evidence=["J"], evidence_card=[2]).to_factor(),
+        TabularCPD("L", 2, values=[[0.9, 0.45, 0.8, 0.1], [0.1, 0.55, 0.2, 0.9]], evidence=["J", "G"],
+                   evidence_card=[2, 2]).to_factor(),
+        TabularCPD("G", 2, [[0.6], [0.4]]).to_factor())
+    queries = [(["J"], {}), (["Q", "J"], {}), (["J"], {"A": 0, "R": 1}), (["J", "Q"], {"A": 0, "R": 0, "G": 0, "L": 1}),
+               (["L", "A"], {"Q": 1})]
+    maps = [([], {}), (["A", "R", "L"], {"J": 0, "Q": 1, "G": 0}), (["J"], {"L": 1})]
+    mms = [([], None), (["G"], None), (["G", "R"], None), (["G", "R", "A"], None), (["J"], {"L": 1})]
+    out["markov6"] = _markov_case(mm, queries, maps, mms, orders=["G", "Q", "A", "J", "L", "R"],
+                                  bp_queries=[(["J"], {}), (["J", "Q"], {"A": 0, "R": 0, "G": 0, "L": 1})])
+    ve = VariableElimination(mm)
+    ig = ve.induced_graph(["G", "Q", "A", "J", "L", "R"])
+    out["markov6"]["induced_graph"] = sorted(sorted(e) for e in ig.edges())
+    out["markov6"]["induced_width"] = int(ve.induced_width(["G", "Q", "A", "J", "L", "R"]))
+    out["markov6"]["triangulations"] = {
+        h: sorted(sorted(e) for e in mm.triangulate(heuristic=h).edges()) for h in ("H1", "H2", "H3", "H4", "H5", "H6")}
+
+    # test_ExactInference.py:639-656: duplicated (identical-valued) factors
+    dup = DiscreteMarkovNetwork([("A", "B"), ("A", "C")])
+    dup.add_factors(DiscreteFactor(["A", "B"], [2, 2], np.eye(2) * 2), DiscreteFactor(["A", "C"], [2, 2], np.eye(2) * 2))
+    out["duplicated"] = {"factors": [_fac_json(f) for f in dup.factors], "edges": [["A", "B"], ["A", "C"]],
+                         "query_A": _fac_json(VariableElimination(dup).query(["A"], show_progress=False))}
+
+    # test_DiscreteMarkovNetwork.py:246-259, 421-591: the 4-cycle with cardinalities 2/3/4/5
+    rng = np.random.default_rng(4242)
+    cyc = DiscreteMarkovNetwork([("a", "b"), ("b", "c"), ("c", "d"), ("d", "a")])
+    cyc.add_factors(DiscreteFactor(["a", "b"], [2, 3], rng.random(6)), DiscreteFactor(["b", "c"], [3, 4], rng.random(12)),
+                    DiscreteFactor(["c", "d"], [4, 5], rng.random(20)), DiscreteFactor(["d", "a"], [5, 2], rng.random(10)))
+    out["cycle4"] = _markov_case(cyc, [(["a"], {}), (["b", "d"], {"c": 2})], [(["a", "c"], {})], [([], None)],
+                                 orders=["a", "b", "c", "d"], bp_queries=[(["b"], {"a": 1})])
+    out["cycle4"]["triangulations"] = {
+        h: sorted(sorted(e) for e in cyc.triangulate(heuristic=h).edges()) for h in ("H1", "H2", "H3", "H4", "H5", "H6")}
+
+    # a seeded random pairwise + triangle Markov network (12 variables, cardinalities 2-4)
+    rng = np.random.default_rng(777)
+    names = [f"v{i:02d}" for i in range(12)]
+    card = {n: int(c) for n, c in zip(names, rng.integers(2, 5, size=12))}
+    edges = set()
+    for i in range(1, 12):  # a random spanning tree ...
+        edges.add(tuple(sorted((names[i], names[int(rng.integers(0, i))]))))
+    while len(edges) < 20:  # ... plus chords
+        a, b = rng.choice(12, size=2, replace=False)
+        edges.add(tuple(sorted((names[a], names[b]))))
+    edges = sorted(edges)
+    rnd = DiscreteMarkovNetwork(edges)
+    facs = [DiscreteFactor([a, b], [card[a], card[b]], rng.random(card[a] * card[b]) + 0.05) for a, b in edges]
+    adj = {n: set() for n in names}
+    for a, b in edges:
+        adj[a].add(b)
+        adj[b].add(a)
+    tri = sorted({tuple(sorted((a, b, c))) for a, b in edges for c in adj[a] & adj[b]})[:3]
+    for t in tri:
+        facs.append(DiscreteFactor(list(t), [card[v] for v in t], rng.random(int(np.prod([card[v] for v in t])))))
+    rnd.add_factors(*facs)
+    queries = [([names[0]], {}), ([names[3], names[7]], {names[1]: 1, names[10]: 0}),
+               ([names[5], names[11], names[2]], {names[8]: 1})]
+    out["random12"] = _markov_case(rnd, queries, [([names[4], names[9]], {names[0]: 1})],
+                                   [([names[6]], {names[3]: 0})], orders=list(reversed(names)),
+                                   bp_queries=[([names[3]], {names[1]: 1}), ([names[5], names[6]], {})])
+    # the heuristic scores of this network tie (cardinalities 2-4), and the reference breaks ties by
+    # set iteration order (string hashes): pin the fill-in of an explicit order instead
+    out["random12"]["order_triangulation"] = {
+        "order": names[::2] + names[1::2],
+        "edges": sorted(sorted(e) for e in rnd.triangulate(order=names[::2] + names[1::2]).edges())}
+
+    # the alarm network as a Markov network (to_markov_model): unnormalised greedy VE results
+    alarm = _model("alarm")
+    am = alarm.to_markov_model()
+    from pgmpy.sampling import BayesianModelSampling
+
+    s = BayesianModelSampling(alarm).forward_sample(size=6, seed=5, show_progress=False)
+    r = random.Random(5)
+    nodes = sorted(alarm.nodes())
+    aq = []
+    ve = VariableElimination(am)
+    for i in range(6):
+        picks = r.sample(nodes, 6)
+        qv, ev = picks[:2], {v: str(s.iloc[i][v]) for v in picks[2:]}
+        aq.append({"variables": qv, "evidence": ev, "joint": _fac_json(ve.query(qv, ev, show_progress=False))})
+    out["alarm_markov"] = {"edges": sorted(sorted(e) for e in am.edges()), "queries": aq}
+
+    # FactorGraph.to_markov_model (FactorGraph.py:303-336) on the 4-cycle potentials
+    fg = FactorGraph()
+    fg.add_nodes_from(["a", "b", "c", "d"])
+    fg.add_factors(*cyc.factors)
+    fg.add_nodes_from(cyc.factors)
+    fg.add_edges_from([(v, f) for f in cyc.factors for v in f.variables])
+    out["factor_graph_to_markov_edges"] = sorted(sorted(e) for e in fg.to_markov_model().edges())
+    _dump("markov_cases.json", out)
+
+
 GENS = {
+    "markov": gen_markov,
     "networks": gen_networks,
     "factor_ops": gen_factor_ops,
     "unit_cases": gen_unit_cases,

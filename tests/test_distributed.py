@@ -85,14 +85,14 @@ def test_two_rank_gather_matches_single_rank(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_hip_predict_matches_golden(tmp_path, world):
     """The sharded HIP path of C5 (BASELINE.json configs[4]) at world 2 and 3 (uneven blocks):
     each rank runs the bound fused row plan on its block of the 1,000 reference munin rows, the
     [17, rows] marginals and MAP indices are gathered to rank 0; the gathered result must equal
     the single-launch run bit for bit and the reference fixture (marginals 1e-6 relative, MAP
-    exact).  On a one-GPU box the ranks share the card through gloo; with a GPU per rank the
-    gather is RCCL."""
+    exact).  With a GPU per rank the gather is RCCL (world 1 on the one-GPU box: a one-rank RCCL
+    communicator, so the nccl backend really executes); ranks sharing one card use gloo."""
     import subprocess
     import sys
 
@@ -107,6 +107,8 @@ def test_sharded_hip_predict_matches_golden(tmp_path, world):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     z = np.load(out)
     assert int(z["world"]) == world
+    if world == 1:
+        assert str(z["backend"]) == "nccl"
     np.testing.assert_array_equal(z["sharded_marg"], z["full_marg"])
     np.testing.assert_array_equal(z["sharded_map"], z["full_map"])
     g = munin_predict()

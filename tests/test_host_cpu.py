@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 13
+    assert lib.pgm_version() == 14
 
 
 def test_struct_layouts_match_header():
@@ -231,8 +231,13 @@ def test_specialised_row_kernel_source_compiles_for_gfx950():
     # the dispatch floors: same loads and stores, no CPT math (one-row and two-row grids)
     floor = src[src.index("pgm_rows_floor("):src.index("pgm_rows_floor2(")]
     assert floor.count("M[") == 17 and floor.count("cr[") == 7 and "S[" not in floor
-    floor2 = src[src.index("pgm_rows_floor2("):]
+    floor2 = src[src.index("pgm_rows_floor2("):src.index("struct pgm_ring_slot")]
     assert floor2.count("(cr + ") == 7 and floor2.count("PGM_WT16(rsM") == 17 and "S[" not in floor2
+    # the resident ring kernel: the two-row body once per 128-row work item, the host counter polled
+    # with a system-scope acquire, a timeout every waiting wave checks
+    ring = src[src.index("pgm_rows_ring("):]
+    assert ring.count("(cr + ") == 7 and ring.count("PGM_WT16(rsM") == 17
+    assert "__HIP_MEMORY_SCOPE_SYSTEM" in ring and ring.count("> timeout") == 2 and "if (r >= n) break;" in ring
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")

@@ -144,6 +144,102 @@ def test_bound_rows_launch_matches_run(gpu):
                                                           device=d.device)})
 
 
+def _munin_template(rows, seed):
+    import random
+
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    m = get_example_model("munin")
+    missing = random.Random(0).sample(sorted(m.nodes()), 3)
+    codes, nodes = forward_sample_codes(m, rows, seed=seed)
+    obs = [v for v in nodes if v not in missing]
+    pos = {v: i for i, v in enumerate(nodes)}
+    ev = np.ascontiguousarray(codes[[pos[v] for v in obs]])
+    return PatternPlan(m, missing, obs, {v: i for i, v in enumerate(obs)}), ev
+
+
+@pytest.mark.parametrize("rows,n_batches", [(1000, 7), (100_000, 24)])
+def test_row_ring_matches_bound_launches(gpu, rows, n_batches):
+    """pgm_rows_ring_* (one resident launch consuming posted batches): after a stream of n_batches
+    batches over 3 slots (distinct evidence windows, each slot reused), every slot's marginals and MAP
+    indices equal the bound one-batch launch on the same rows bit for bit; the ring restarts for a
+    second stream; posting past the started count is refused."""
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+
+    plan, ev = _munin_template(rows * 3, seed=17)
+    d = upload_codes(ev)
+    ld = rows * 3
+    slots, refs = [], []
+    for s in range(3):
+        out = plan.alloc_outputs(rows, marginals=True, map_=True)
+        out["marg"].fill_(-1.0)
+        slots.append((d, ld, s * rows, out))
+        ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+        plan.bind(d, ld, s * rows, rows, ref).run()
+        refs.append(ref)
+    torch.cuda.synchronize()
+    err = torch.zeros(1, dtype=torch.int32, device=d.device)
+    ring = plan.ring(slots, rows, err=err)
+    name, blocks, wg = ring.kernel()
+    assert name == "pgm_rows_ring" and blocks >= 256 and wg % 64 == 0
+    for _ in range(2):
+        ring.run(n_batches)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        for s in range(3):
+            assert torch.equal(slots[s][3]["marg"], refs[s]["marg"]), s
+            assert torch.equal(slots[s][3]["map"], refs[s]["map"]), s
+        for s in range(3):
+            slots[s][3]["marg"].fill_(-1.0)
+        torch.cuda.synchronize()
+    ring.start(2)
+    ring.post(1)
+    with pytest.raises(ValueError):
+        ring.post(3)
+    with pytest.raises(ValueError):
+        ring.finish()  # one batch still unposted
+    ring.post(2)
+    ring.finish()
+
+
+def test_row_ring_exits_without_posts(gpu):
+    """Every exit path of the resident kernel ends the launch: cancel() with batches never posted,
+    and the timeout (the waves give up waiting; finish() then reports the timeout)."""
+    import time
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+
+    rows = 2000
+    plan, ev = _munin_template(rows, seed=3)
+    d = upload_codes(ev)
+    out = plan.alloc_outputs(rows, marginals=True)
+    ring = plan.ring([(d, rows, 0, out)], rows)
+    t0 = time.perf_counter()
+    ring.start(4, timeout_s=5.0)
+    ring.post(1)
+    ring.cancel()  # three batches never posted
+    assert time.perf_counter() - t0 < 4.0
+    ring.start(3, timeout_s=0.05)
+    time.sleep(0.3)  # past the deadline: every wave waiting for batch 0 has left
+    ring.post(3)
+    with pytest.raises(RuntimeError, match="timed out"):
+        ring.finish()
+    ring.run(3)  # usable again
+    torch.cuda.synchronize()
+    ref = plan.alloc_outputs(rows, marginals=True)
+    plan.bind(d, rows, 0, rows, ref).run()
+    torch.cuda.synchronize()
+    assert torch.equal(out["marg"], ref["marg"])
+    with pytest.raises(ValueError):  # odd row counts break the two-rows-per-lane contract
+        plan.ring([(d, rows, 0, plan.alloc_outputs(rows - 1, marginals=True))], rows - 1)
+
+
 @pytest.mark.parametrize("rows", [1000, 100_000, 1_000_000])
 def test_direct_queue_launch_matches_bound(gpu, rows):
     """pgm_dq_bind_rows / pgm_dq_launch (the AQL-packet launch of the same specialised kernel on a
