@@ -19,6 +19,7 @@ exact signatures of ``compat_fns``.  INTEGRATION.md shows the few lines a mainta
 pgmpy to select it.  There is no CPU path: every computing call goes to libpgmhip and raises
 ``NativeUnavailable`` without it.
 """
+import builtins
 import numbers
 
 import numpy as np
@@ -190,7 +191,7 @@ class HipArray:
         dims = [d for d, k in enumerate(norm) if isinstance(k, int)]
         shape = self.shape
         for d in dims:  # numpy's IndexError for an out-of-range state (test_Factor.py:555-565)
-            ax = sum(1 for k in norm[:d] if k is not None and k is not Ellipsis)
+            ax = builtins.sum(1 for k in norm[:d] if k is not None and k is not Ellipsis)
             if ax < len(shape) and not -shape[ax] <= norm[d] < shape[ax]:
                 raise IndexError(f"index {norm[d]} is out of bounds for axis {ax} with size {shape[ax]}")
         return HipArray(self.t[tuple(norm)])
@@ -250,12 +251,26 @@ class HipArray:
     def __iadd__(self, other):
         return self._binary(other, "add")
 
+    def __rsub__(self, other):
+        """``1 - values`` (the virtual-evidence child CPD, inference/base.py:286): other + (-1) * values."""
+        neg = self._binary(-1.0, "mul")
+        return neg._binary(other, "add")
+
+    def __neg__(self):
+        return self._binary(-1.0, "mul")
+
     # ------------------------------------------------------------------ reductions
     def sum(self, axis=None):
         return HipArray(_reduce(self, axis, "sum"))
 
     def max(self, axis=None):
         return HipArray(_reduce(self, axis, "max"))
+
+    def flatten(self):
+        """``values.flatten()`` (is_valid_cpd, DiscreteFactor.py:959-964): a contiguous 1-D array."""
+        return self.reshape(self.size)
+
+    ravel = flatten
 
 
 def _as_tensor(x):
@@ -361,11 +376,95 @@ def isnan(arr):
     return _NanMask(arr) if isinstance(arr, HipArray) else np.isnan(arr)
 
 
+def _is_torch(x):
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(x, torch.Tensor)
+
+
+def _host(x):
+    if isinstance(x, HipArray):
+        return np.asarray(x)
+    if _is_torch(x):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def unique(arr, axis=0, return_counts=False, return_inverse=False):
+    """compat_fns.unique (L123-131).  Its callers (sampling/base.py:148) use the results as host
+    bookkeeping, so a HipArray is reduced on the host (numpy's semantics)."""
+    if _is_torch(arr):
+        import torch
+
+        return torch.unique(arr, return_inverse=return_inverse, return_counts=return_counts, dim=axis)
+    return np.unique(_host(arr), axis=axis, return_counts=return_counts, return_inverse=return_inverse)
+
+
+def flip(arr, axis=0):
+    """compat_fns.flip (L134-138): assignment() flips its integer index table (DiscreteFactor.py:312)."""
+    if isinstance(arr, np.ndarray):
+        return np.flip(arr, axis=axis)
+    dims = tuple(axis) if isinstance(axis, (tuple, list)) else (int(axis),)
+    if isinstance(arr, HipArray):
+        return HipArray(arr.t.flip(dims))
+    import torch
+
+    return torch.flip(arr, dims=dims)
+
+
+def exp(arr):
+    """compat_fns.exp (L148-152) — elementwise, off the hot path (MirrorDescentEstimator)."""
+    if isinstance(arr, HipArray):
+        return HipArray(arr.t.exp())
+    if isinstance(arr, np.ndarray):
+        return np.exp(arr)
+    return arr.exp()
+
+
+def sum(arr):
+    """compat_fns.sum (L155-159): the partition function's total (DiscreteMarkovNetwork.py:844,
+    ClusterGraph.py:327) — one pgm_contract reduction to a scalar on the hip backend."""
+    if isinstance(arr, HipArray):
+        return float(HipArray(_reduce(arr, None, "sum")))
+    if isinstance(arr, np.ndarray):
+        return arr.sum()
+    import torch
+
+    return torch.sum(arr)
+
+
+def allclose(arr1, arr2, atol):
+    """compat_fns.allclose (L162-186) with numpy's tolerance rule (rtol 1e-5 + atol): DiscreteFactor.__eq__
+    (L1079) and is_valid_cpd (L959).  A comparison verdict, not a hot-path value: compared on the host."""
+    return bool(np.allclose(_host(arr1), _host(arr2), atol=atol))
+
+
 class _HipCompute:
-    """What compat_fns.get_compute_backend() returns on the hip backend (DiscreteFactor.py:863
-    calls its ``isnan``)."""
+    """What compat_fns.get_compute_backend() returns on the hip backend: the array-namespace calls
+    pgmpy makes through it — ``isnan`` (divide, DiscreteFactor.py:863), ``zeros`` (assignment's
+    integer table, L304-306: a torch integer tensor on the HIP device, as the torch backend builds
+    it next to the torch index of L293-298), ``allclose`` (is_valid_cpd, L959) and ``vstack`` (the
+    virtual-evidence CPD, inference/base.py:286)."""
 
     isnan = staticmethod(isnan)
+
+    @staticmethod
+    def zeros(shape, dtype=int):
+        import torch
+
+        tdt = torch.int64 if dtype in (int, np.int64, "int64") else torch.float64
+        return torch.zeros(shape, dtype=tdt, device=config.get_device())
+
+    @staticmethod
+    def allclose(a, b, atol=1e-08, rtol=1e-05):
+        return bool(np.allclose(_host(a), _host(b), atol=atol, rtol=rtol))
+
+    @staticmethod
+    def vstack(arrs):
+        parts = [_host(a) for a in arrs]
+        return HipArray.from_host(np.vstack(parts))
 
 
 def get_compute_backend():

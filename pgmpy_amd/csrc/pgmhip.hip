@@ -2516,12 +2516,18 @@ static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, co
 // batches by raising a counter in pinned host memory (ctl[0] = batches posted); the launch may start
 // before the first post.  Work item = 128 rows (one wave, two rows per lane) of one batch; item j
 // goes to wave j mod W (W = resident waves), so consecutive batches overlap across the chip instead of
-// each paying a dispatch.  A wave about to start a batch not yet known to be posted reads the count
-// its workgroup last saw (LDS); if that is stale one wave per workgroup (an LDS token) polls the host
-// counter with a system-scope acquire and publishes it, the others sleep on LDS.  Exit conditions
-// every wave reaches: all items done; ctl[1] (cancel) set by the host; or `timeout` ticks of the
-// constant 100 MHz wall clock without the needed batch (ctl[2] |= 2).  The CPT values are staged in
-// LDS once per workgroup for the whole stream.
+// each paying a dispatch.
+// Learning that a batch is posted, three levels deep so the host counter sees ONE reader at a time
+// (reads of host memory from the GPU are serialised: 768 concurrent first polls cost ~150 us, r03a):
+//   1. the count the wave's workgroup last saw (LDS seen_s);
+//   2. one wave per workgroup (LDS token) reads the device-memory mirror g[0];
+//   3. one wave on the chip (token g[1], agent scope) reads ctl[0] with a system-scope acquire and
+//      raises the mirror.
+// A wave that adopts a newer count from the mirror executes a system-scope acquire fence, so batch
+// inputs written before the post are visible to its workgroup.  Exit conditions every wave reaches:
+// all items done; ctl[1] (cancel) set by the host; or `timeout` ticks of the constant 100 MHz wall
+// clock without the needed batch (ctl[2] |= 2); either of the last two raises g[2] (stop) for all.
+// The CPT values are staged in LDS once per workgroup for the whole stream.
 static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
   const int NV = pl->n_values + 1;
   const int WG = ring_wg();
@@ -2529,8 +2535,8 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
   o += "struct pgm_ring_slot { const unsigned char *C; long long ldc, row0; double *M; long long ldo; int *MP; "
        "double *G; long long pad; };\n";
   pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_ring(const double *__restrict__ V, "
-             "const pgm_ring_slot *__restrict__ D, unsigned n_slots, unsigned *ctl, unsigned n_batches, long long n, "
-             "int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
+             "const pgm_ring_slot *__restrict__ D, unsigned n_slots, unsigned *ctl, unsigned *g, unsigned n_batches, "
+             "long long n, int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
   o += "  const int t = threadIdx.x;\n";
   pgmi_appendf(o, "  __shared__ double S[%d];\n  __shared__ unsigned seen_s, token_s, stop_s;\n", K * WG);
   for (int i = 0; i < K; ++i) pgmi_appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
@@ -2541,6 +2547,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
   o += "  const unsigned long long chunks = (unsigned long long)(n + 127) / 128;\n"
        "  const unsigned long long items = chunks * n_batches;\n"
        "  const unsigned long long t0 = wall_clock64();\n"
+       "  const bool lead = (t & 63) == 0;\n"
        "  unsigned seen = 0u;\n"
        "  for (unsigned long long j = wv0; j < items; j += W) {\n"
        "    const unsigned bt = (unsigned)(j / chunks);\n"
@@ -2550,34 +2557,51 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "      if (sl > seen) { seen = sl; continue; }\n"
        "      if (__hip_atomic_load(&stop_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }\n"
        "      unsigned mine = 0u;\n"
-       "      if ((t & 63) == 0) mine = atomicCAS(&token_s, 0u, 1u) == 0u ? 1u : 0u;\n"
+       "      if (lead) mine = atomicCAS(&token_s, 0u, 1u) == 0u ? 1u : 0u;\n"
        "      mine = __builtin_amdgcn_readfirstlane(mine);\n"
-       "      if (mine) {\n"
-       "        for (;;) {\n"
-       "          const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
-       "          if (p > bt) {\n"
-       "            seen = p;\n"
-       "            if ((t & 63) == 0) atomicMax(&seen_s, p);\n"
-       "            break;\n"
-       "          }\n"
-       "          const bool cancel = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;\n"
-       "          const bool late = wall_clock64() - t0 > timeout;\n"
-       "          if (cancel || late) {\n"
-       "            if ((t & 63) == 0) {\n"
-       "              if (late) __hip_atomic_fetch_or(&ctl[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
-       "              atomicExch(&stop_s, 1u);\n"
+       "      if (!mine) {\n"
+       "        if (wall_clock64() - t0 > timeout) { stop = true; break; }\n"
+       "        __builtin_amdgcn_s_sleep(2);\n"
+       "        continue;\n"
+       "      }\n"
+       "      for (;;) {  /* this wave speaks for its workgroup */\n"
+       "        unsigned m = __hip_atomic_load(&g[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "        if (m <= bt) {\n"
+       "          if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = true; break; }\n"
+       "          unsigned poll = 0u;\n"
+       "          if (lead) poll = atomicCAS(&g[1], 0u, 1u) == 0u ? 1u : 0u;\n"
+       "          poll = __builtin_amdgcn_readfirstlane(poll);\n"
+       "          if (poll) {  /* the one reader of the host counter */\n"
+       "            const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "            if (p > m && lead) __hip_atomic_fetch_max(&g[0], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "            if (p > m) m = p;\n"
+       "            if (m <= bt) {\n"
+       "              const bool cancel = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;\n"
+       "              const bool late = wall_clock64() - t0 > timeout;\n"
+       "              if ((cancel || late) && lead) {\n"
+       "                if (late) __hip_atomic_fetch_or(&ctl[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "                __hip_atomic_store(&g[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "              }\n"
+       "              stop = cancel || late;\n"
        "            }\n"
+       "            if (lead) __hip_atomic_store(&g[1], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "            if (stop) break;\n"
+       "          } else if (wall_clock64() - t0 > timeout) {\n"
        "            stop = true;\n"
        "            break;\n"
        "          }\n"
-       "          __builtin_amdgcn_s_sleep(4);\n"
        "        }\n"
-       "        if ((t & 63) == 0) atomicExch(&token_s, 0u);\n"
-       "        if (stop) break;\n"
-       "      } else {\n"
-       "        if (wall_clock64() - t0 > timeout) { stop = true; break; }\n"
-       "        __builtin_amdgcn_s_sleep(2);\n"
+       "        if (m > bt) {\n"
+       "          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"\");  /* system scope: the batch's inputs */\n"
+       "          seen = m;\n"
+       "          if (lead) atomicMax(&seen_s, m);\n"
+       "          break;\n"
+       "        }\n"
+       "        __builtin_amdgcn_s_sleep(4);\n"
        "      }\n"
+       "      if (stop && lead) atomicExch(&stop_s, 1u);\n"
+       "      if (lead) atomicExch(&token_s, 0u);\n"
+       "      if (stop) break;\n"
        "    }\n"
        "    if (stop) break;\n"
        "    const pgm_ring_slot d = D[bt % n_slots];\n"
@@ -3916,6 +3940,7 @@ struct RowsRing {
   PgmRingSlot *d_slots = nullptr;  // device
   unsigned *ctl = nullptr;         // pinned host: [0] batches posted, [1] cancel, [2] status (|2: timed out)
   unsigned *ctl_dev = nullptr;     // its device address
+  unsigned *gctl = nullptr;        // device memory: [0] mirror of ctl[0], [1] host-poll token, [2] stop
   int32_t *err = nullptr;
   hipStream_t stream = nullptr;
   unsigned blocks = 0;
@@ -3968,6 +3993,7 @@ int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint
     e = hipMemcpy(rg->d_slots, slots.data(), sizeof(PgmRingSlot) * slots.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipHostMalloc((void **)&rg->ctl, 64, hipHostMallocCoherent | hipHostMallocMapped);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&rg->ctl_dev, rg->ctl, 0);
+  if (e == hipSuccess) e = hipMalloc((void **)&rg->gctl, 64);
   int dev = 0, cus = 0, per_cu = 0;
   if (e == hipSuccess) e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3976,6 +4002,7 @@ int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint
   if (e != hipSuccess) {
     (void)hipGetLastError();
     if (rg->d_slots) (void)hipFree(rg->d_slots);
+    if (rg->gctl) (void)hipFree(rg->gctl);
     if (rg->ctl) (void)hipHostFree(rg->ctl);
     delete rg;
     return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_ring_create: %s", hipGetErrorString(e));
@@ -4007,11 +4034,12 @@ int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
   const double *v = rg->h->d_values;
   const PgmRingSlot *d = rg->d_slots;
   unsigned ns = rg->n_slots, nb = n_batches;
-  unsigned *ctl = rg->ctl_dev;
+  unsigned *ctl = rg->ctl_dev, *gc = rg->gctl;
   long long n = rg->n_rows;
   int32_t *ef = rg->err;
   int32_t md = rg->mode;
-  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, &nb, &n, (void *)&ef, &md, &ticks};
+  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, (void *)&gc, &nb, &n, (void *)&ef, &md, &ticks};
+  HIP_TRY(hipMemsetAsync(rg->gctl, 0, 64, rg->stream));  // the mirror, token and stop of this launch
   HIP_TRY(hipModuleLaunchKernel(rg->h->jit_fn_ring, rg->blocks, 1, 1, (unsigned)ring_wg(), 1, 1, 0, rg->stream, args,
                                 nullptr));
   rg->running = true;
@@ -4077,6 +4105,7 @@ int pgm_rows_ring_destroy(void *ring) {
   int st = PGM_OK;
   if (rg->running) st = pgm_rows_ring_cancel(rg);
   if (rg->d_slots) (void)hipFree(rg->d_slots);
+  if (rg->gctl) (void)hipFree(rg->gctl);
   if (rg->ctl) (void)hipHostFree(rg->ctl);
   delete rg;
   return st;
