@@ -401,6 +401,13 @@ int pgm_rows_bound_destroy(void *bound);
  * per thread, 16-B stores), "pgm_rows_floor" / "pgm_rows_floor2" (PGM_ROWS_FLOOR), or "" (an AOT kernel), with its grid and workgroup size */
 int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
 
+/* Host-side scan for evidence ingestion (no device needed): out[j] = 1 when any of the n int8 cells of
+ * column cols[j] is negative (a pandas Categorical NaN code), else 0; up to `threads` host threads.
+ * Finds the NaN-holding columns of a categorical frame in one native pass, so rows are grouped by
+ * missing-column pattern from those columns only (predict's per-row NaN handling,
+ * pgmpy/models/DiscreteBayesianNetwork.py:862-878). */
+int pgm_host_any_negative_i8(const int8_t *const *cols, int32_t n_cols, int64_t n, uint8_t *out, int32_t threads);
+
 /* Resident ring of row batches (streaming predict_probability / predict): one launch of the
  * plan-specialised two-rows-per-lane kernel ("pgm_rows_ring") stays resident while the host publishes
  * batches, so consecutive batches overlap on the chip instead of each paying a dispatch.  Replaces the

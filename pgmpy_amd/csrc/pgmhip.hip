@@ -2347,7 +2347,7 @@ static int ring_wg() {
 }
 
 static std::vector<int> rows_cols(const pgm_rows_plan *pl);
-static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R);
+static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R, bool coherent = false);
 static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, const std::vector<int> &cols,
                               const char *leave);
 
@@ -2395,11 +2395,17 @@ static std::vector<int> rows_cols(const pgm_rows_plan *pl) {
 }
 
 // the row's evidence codes (row rc of the columns at C + row0, leading dimension ldc): e<i>_<u>
-static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R) {
+// coherent: system-scope relaxed loads (past every non-coherent cache, no invalidation needed) — the
+// ring kernel's codes, which may be written after the launch started
+static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R, bool coherent) {
   if (!cols.empty()) o += "  const unsigned char *cr = C + row0 + rc;\n";
   for (size_t i = 0; i < cols.size(); ++i) {
     if (R == 1) {
       pgmi_appendf(o, "  const unsigned e%zu_0 = cr[%dLL * ldc];\n", i, cols[i]);
+    } else if (coherent) {
+      pgmi_appendf(o, "  const unsigned w%zu = __hip_atomic_load((__attribute__((address_space(1))) unsigned short *)(cr + %dLL * ldc), __ATOMIC_RELAXED, "
+                   "__HIP_MEMORY_SCOPE_SYSTEM);\n", i, cols[i]);
+      pgmi_appendf(o, "  const unsigned e%zu_0 = w%zu & 255u, e%zu_1 = w%zu >> 8;\n", i, i, i, i);
     } else {
       pgmi_appendf(o, "  const unsigned w%zu = *(const unsigned short *)(cr + %dLL * ldc);\n", i, cols[i]);
       pgmi_appendf(o, "  const unsigned e%zu_0 = w%zu & 255u, e%zu_1 = w%zu >> 8;\n", i, i, i, i);
@@ -2523,8 +2529,10 @@ static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, co
 //   2. one wave per workgroup (LDS token) reads the device-memory mirror g[0];
 //   3. one wave on the chip (token g[1], agent scope) reads ctl[0] with a system-scope acquire and
 //      raises the mirror.
-// A wave that adopts a newer count from the mirror executes a system-scope acquire fence, so batch
-// inputs written before the post are visible to its workgroup.  Exit conditions every wave reaches:
+// No acquire fences (an L2 invalidation per workgroup serialises per XCD: ~100 us per launch, r03b):
+// the counters are read with relaxed system/agent-scope atomics, and the evidence codes with
+// system-scope loads, which go past every non-coherent cache — so codes written (by DMA) after the
+// launch started but before their batch was posted are read fresh.  Exit conditions every wave reaches:
 // all items done; ctl[1] (cancel) set by the host; or `timeout` ticks of the constant 100 MHz wall
 // clock without the needed batch (ctl[2] |= 2); either of the last two raises g[2] (stop) for all.
 // The CPT values are staged in LDS once per workgroup for the whole stream.
@@ -2553,7 +2561,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "    const unsigned bt = (unsigned)(j / chunks);\n"
        "    bool stop = false;\n"
        "    while (bt >= seen) {\n"
-       "      const unsigned sl = __hip_atomic_load(&seen_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "      const unsigned sl = __hip_atomic_load(&seen_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
        "      if (sl > seen) { seen = sl; continue; }\n"
        "      if (__hip_atomic_load(&stop_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }\n"
        "      unsigned mine = 0u;\n"
@@ -2565,15 +2573,15 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "        continue;\n"
        "      }\n"
        "      for (;;) {  /* this wave speaks for its workgroup */\n"
-       "        unsigned m = __hip_atomic_load(&g[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "        unsigned m = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "        if (m <= bt) {\n"
        "          if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = true; break; }\n"
        "          unsigned poll = 0u;\n"
        "          if (lead) poll = atomicCAS(&g[1], 0u, 1u) == 0u ? 1u : 0u;\n"
        "          poll = __builtin_amdgcn_readfirstlane(poll);\n"
        "          if (poll) {  /* the one reader of the host counter */\n"
-       "            const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
-       "            if (p > m && lead) __hip_atomic_fetch_max(&g[0], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "            const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "            if (p > m && lead) __hip_atomic_fetch_max(&g[0], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "            if (p > m) m = p;\n"
        "            if (m <= bt) {\n"
        "              const bool cancel = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;\n"
@@ -2584,7 +2592,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "              }\n"
        "              stop = cancel || late;\n"
        "            }\n"
-       "            if (lead) __hip_atomic_store(&g[1], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "            if (lead) __hip_atomic_store(&g[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "            if (stop) break;\n"
        "          } else if (wall_clock64() - t0 > timeout) {\n"
        "            stop = true;\n"
@@ -2592,7 +2600,6 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "          }\n"
        "        }\n"
        "        if (m > bt) {\n"
-       "          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"\");  /* system scope: the batch's inputs */\n"
        "          seen = m;\n"
        "          if (lead) atomicMax(&seen_s, m);\n"
        "          break;\n"
@@ -2617,7 +2624,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
          "    const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc(G, 0, 0x7fffffff, 0x00020000);\n";
   o += "    do {\n";
   const std::vector<int> cols = rows_cols(pl);
-  emit_rows_code_loads(o, cols, 2);
+  emit_rows_code_loads(o, cols, 2, true);
   emit_rows_compute(o, pl, 2, cols, "break");
   o += "    } while (0);\n  }\n}\n#undef VAL\n";
 }
@@ -3458,6 +3465,45 @@ int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n
                      lut_stride, n_cols, n_rows, chunk, col_key, out, ld_out, (unsigned long long *)row_key, row_nmiss,
                      (unsigned long long *)row_hash, err_flag);
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+// host-side scan (no device): for each of n_cols int8 code columns (n cells each), whether any cell is
+// negative (pandas Categorical NaN = -1).  Columns are split over up to `threads` host threads; each
+// column is OR-reduced 8 cells per 64-bit word and tested on the sign bits.
+int pgm_host_any_negative_i8(const int8_t *const *cols, int32_t n_cols, int64_t n, uint8_t *out, int32_t threads) {
+  if (n_cols < 0 || n < 0 || (n_cols > 0 && (!cols || !out))) return fail(PGM_EINVAL, "host_any_negative_i8: bad argument");
+  for (int32_t j = 0; j < n_cols; ++j)
+    if (!cols[j] && n > 0) return fail(PGM_EINVAL, "host_any_negative_i8: column %d is null", j);
+  auto scan = [&](int32_t lo, int32_t hi) {
+    for (int32_t j = lo; j < hi; ++j) {
+      const int8_t *c = cols[j];
+      const int64_t words = n / 8;
+      uint64_t acc = 0;
+      for (int64_t w = 0; w < words; ++w) {
+        uint64_t x;
+        memcpy(&x, c + 8 * w, 8);
+        acc |= x;
+      }
+      bool neg = (acc & 0x8080808080808080ull) != 0;
+      for (int64_t i = words * 8; i < n && !neg; ++i) neg = c[i] < 0;
+      out[j] = neg ? 1 : 0;
+    }
+  };
+  const int64_t work = (int64_t)n_cols * n;
+  int nt = std::max(1, std::min<int>(threads, (int)std::min<int64_t>(64, work / (1 << 20) + 1)));
+  nt = std::min(nt, std::max(1, n_cols));
+  if (nt == 1) {
+    scan(0, n_cols);
+    return PGM_OK;
+  }
+  std::vector<std::thread> pool;
+  const int32_t per = (n_cols + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    const int32_t lo = t * per, hi = std::min(n_cols, lo + per);
+    if (lo < hi) pool.emplace_back(scan, lo, hi);
+  }
+  for (auto &th : pool) th.join();
   return PGM_OK;
 }
 

@@ -227,6 +227,160 @@ def ingest_frame(model, data, columns=None, row_hash=False):
     return ev
 
 
+_LUT_CACHE = {}  # (id(CategoricalDtype), variable) -> (dtype, state names, LUT, categories all valid)
+_LUT_CACHE_MAX = 16384
+_LUT_LOCK = threading.Lock()
+
+
+def _category_lut(col, st, dtype):
+    """(256-entry category index -> state code LUT, every category a state) of a categorical column
+    (uint8 view of the int8 codes: index 255 is NaN -> MISSING; 254 = a category that is not a state
+    name).  The reference's str() fallback applies per category (DiscreteFactor.py:589-597).  Cached
+    per dtype object (a strong reference is kept, so its id is not reused while cached): frames
+    built from one CategoricalDtype per variable, or the same frame again, pay this once."""
+    key = (id(dtype), col)
+    hit = _LUT_CACHE.get(key)
+    if hit is not None and hit[0] is dtype and hit[1] == st:
+        return hit[2], hit[3]
+    cats = np.asarray(dtype.categories, dtype=object)
+    t = _lookup_codes(cats, st) if len(cats) else np.zeros(0, dtype=np.int64)
+    miss = np.nonzero(t < 0)[0]
+    if len(miss):
+        sm = {str(x): i for i, x in enumerate(st)}
+        for i in miss:
+            t[i] = sm.get(str(cats[i]), 254)
+    lut = np.full(256, 254, dtype=np.uint8)
+    lut[:len(t)] = t
+    lut[255] = MISSING
+    ok = not (t == 254).any()
+    with _LUT_LOCK:
+        if len(_LUT_CACHE) >= _LUT_CACHE_MAX:
+            _LUT_CACHE.clear()
+        _LUT_CACHE[key] = (dtype, list(st), lut, ok)
+    return lut, ok
+
+
+def _host_threads():
+    """Host threads for native ingestion scans: the CPUs this process may run on, at most 16 (the GPU
+    box's CPU share per GPU)."""
+    import os
+
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:  # pragma: no cover
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+def _frame_categoricals(data, columns):
+    """The pandas Categorical of every column, in `columns` order (one block per categorical column:
+    read through the block manager, not per-column Series), or None."""
+    import pandas as pd
+
+    try:
+        mgr = data._mgr
+        arrays, blknos, blklocs = mgr.arrays, mgr.blknos, mgr.blklocs
+        loc = data.columns.get_indexer(columns)
+        out = []
+        for i in loc:
+            if i < 0 or blklocs[i] != 0:
+                return None
+            a = arrays[blknos[i]]
+            if not isinstance(a, pd.Categorical):
+                return None
+            out.append(a)
+        return out
+    except Exception:  # pandas internals moved: the public accessor
+        out = []
+        for c in columns:
+            a = data[c].array
+            if not isinstance(a, pd.Categorical):
+                return None
+            out.append(a)
+        return out
+
+
+class ColumnarEvidence:
+    """Evidence of a frame whose every column is categorical (pandas Categorical with <= 127
+    categories): the int8 category codes stay in the frame (zero copy).  Rows are grouped by their
+    missing-column pattern from the NaN-holding columns only (found by one native scan,
+    pgm_host_any_negative_i8), and a pattern's plan gets just the columns it reads
+    (PatternPlan.compact()), mapped through per-column LUTs and uploaded — a munin template frame
+    (1,038 columns) moves 7 of them.  Replaces the per-row state-name lookups of predict /
+    predict_probability (DiscreteBayesianNetwork.py:871-878, 974-979)."""
+
+    def __init__(self, raws, luts, groups, n):
+        self.raws, self.luts, self.groups, self.n = raws, luts, groups, n
+
+    def host_codes_for(self, cols, rows):
+        """uint8 state codes [len(cols), len(rows)] of the given frame columns and rows (host)."""
+        full = len(rows) == self.n
+        out = np.empty((len(cols), len(rows)), dtype=np.uint8)
+        for i, j in enumerate(cols):
+            r = self.raws[j].view(np.uint8)
+            np.take(self.luts[j], r if full else r[rows], out=out[i])
+        return out
+
+    def codes_for(self, cols, rows):
+        """The same codes on the device."""
+        return upload_codes(self.host_codes_for(cols, rows))
+
+
+def ingest_columnar(model, data, columns):
+    """ColumnarEvidence of `data`, or None when a column is not a (small) pandas Categorical.
+    Raises the reference's KeyError when a cell holds a category that is not a state name."""
+    if data.columns.has_duplicates:
+        return None
+    cats = _frame_categoricals(data, columns)
+    if cats is None:
+        return None
+    n = len(data)
+    raws, luts, addrs = [], [], []
+    i8 = np.dtype(np.int8)
+    for col, arr in zip(columns, cats):
+        raw = arr._codes
+        if raw.dtype is not i8 or not raw.flags.c_contiguous:
+            return None
+        addrs.append(raw.__array_interface__["data"][0])
+        cpd = model.get_cpds(col)
+        st = cpd.state_names[col]
+        if len(st) >= MISSING:
+            raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
+        lut, ok = _category_lut(col, st, arr.dtype)
+        if not ok:
+            bad = np.nonzero(lut[:len(arr.dtype.categories)] == 254)[0]
+            if np.isin(raw, bad.astype(np.int8)).any():
+                encode_frame(model, data, [col])  # raises the reference's KeyError for the cell
+                raise KeyError(f"evidence holds a category of {col} that is not a state name")
+        raws.append(raw)
+        luts.append(lut)
+    nc = len(columns)
+    has_nan = np.zeros(nc, dtype=np.uint8)
+    if nc and n:
+        ptrs = (ctypes.c_void_p * nc)(*addrs)
+        N.check(N.load_library().pgm_host_any_negative_i8(ptrs, nc, n, has_nan.ctypes.data_as(ctypes.c_void_p),
+                                                          _host_threads()), "host_any_negative_i8")
+    nan_cols = np.nonzero(has_nan)[0].tolist()
+    if not nan_cols or n == 0:
+        groups = [(np.ones(nc, dtype=bool), np.arange(n))]
+    else:
+        miss = np.stack([raws[j] < 0 for j in nan_cols])  # [k, n]
+        packed = np.packbits(miss.T, axis=1)
+        _, first, inv = np.unique(packed, axis=0, return_index=True, return_inverse=True)
+        inv = inv.reshape(-1)
+        order = np.argsort(inv, kind="stable")
+        bounds = np.searchsorted(inv[order], np.arange(len(first) + 1))
+        groups = []
+        for g in range(len(first)):
+            rows = order[bounds[g]:bounds[g + 1]]
+            mask = np.ones(nc, dtype=bool)
+            for k, j in enumerate(nan_cols):
+                if miss[k, rows[0]]:
+                    mask[j] = False
+            groups.append((mask, rows))
+        groups.sort(key=lambda gr: gr[1][0])
+    return ColumnarEvidence(raws, luts, groups, n)
+
+
 def _host_row_hash(codes):
     """[n, 2] int64 content hash of the rows of uint8 codes [n_cols, n] (host encoder path)."""
     rng = np.random.default_rng(_COL_KEY_SEED + 1)
@@ -293,8 +447,8 @@ def get_plan(model, variables, evidence_vars, col_of):
     used dropped first).  A cached plan is reused only while PatternPlan.is_current(): the model's
     structure and the values of the CPDs it read are unchanged (a CPD edited, replaced, added or
     removed recompiles, as the reference recomputes from the current CPDs on every call)."""
-    key = (tuple(variables), tuple(evidence_vars), tuple(sorted((k, v) for k, v in col_of.items()
-                                                                if k in set(evidence_vars))))
+    # evidence variable -> codes column, in evidence_vars order (one pass: munin patterns hold ~1,000)
+    key = (tuple(variables), tuple(evidence_vars), tuple(col_of.get(k, -1) for k in evidence_vars))
     with _plan_cache_lock:
         cache = model.__dict__.get(_PLAN_CACHE_ATTR)
         if cache is None:
@@ -312,13 +466,19 @@ def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars):
     """Yield (plan, rows, outputs-on-host) per evidence pattern."""
     columns = list(data.columns)
     col_of = {c: i for i, c in enumerate(columns)}
-    ev = ingest_frame(model, data, columns)
+    ev = ingest_columnar(model, data, columns)
+    if ev is None:
+        ev = ingest_frame(model, data, columns)
     for mask, rows in ev.groups:
         observed = [columns[j] for j in range(len(columns)) if mask[j]]
         nan_cols = [columns[j] for j in range(len(columns)) if not mask[j]]
         variables = list(base_vars) + ([c for c in nan_cols if c not in base_vars] if extra_nan_vars else [])
         plan = get_plan(model, variables, observed, col_of)
-        dcodes = ev.rows_codes(rows)
+        if isinstance(ev, ColumnarEvidence):  # only the columns this pattern's plan reads
+            dcodes = ev.codes_for([col_of[v] for v in plan.ev_used], rows)
+            plan = plan.compact()
+        else:
+            dcodes = ev.rows_codes(rows)
         n = len(rows)
         out = plan.alloc_outputs(n, marginals=want_marg, map_=want_map)
         err = None

@@ -345,6 +345,28 @@ class PatternPlan:
         self._build_fused()
         return BoundRows(self, codes, ld, row0, n_rows, out, err, stream, floor=floor)
 
+    def compact(self):
+        """This plan reading a compact codes array that holds only the evidence columns it uses, in
+        ev_used order (column i = ev_used[i]) — what ingestion uploads when it copies just the columns
+        a pattern reads.  Shares the pruning, factors and sources (so is_current() agrees); compiles
+        its own kernels.  Cached on the plan."""
+        import copy
+
+        c = self.__dict__.get("_compact")
+        if c is None:
+            with self._lock:
+                c = self.__dict__.get("_compact")
+                if c is None:
+                    c = copy.copy(self)
+                    for k in ("_handle", "_handle_joint", "_plan", "_progs", "_compact"):
+                        c.__dict__.pop(k, None)
+                    c._handle = None
+                    c._handle_joint = None
+                    c._lock = threading.RLock()
+                    c.col_of = {v: i for i, v in enumerate(self.ev_used)}
+                    self._compact = c
+        return c
+
     def ring(self, slots, n_rows, err=None, stream=None):
         """A resident ring over equally sized row batches (pgm_rows_ring_*): slots = [(codes, ld, row0,
         out), ...]; batch b reads rows [row0, row0 + n_rows) of slot b % len(slots)'s codes and writes

@@ -208,6 +208,45 @@ def test_encode_frame_categorical_numeric_and_nan():
     assert codes.tolist() == [[1, 0, 1], [1, 0, 1]]
 
 
+def test_columnar_ingestion_matches_host_encoder():
+    """ingest_columnar (categorical frames: zero-copy codes, NaN patterns from the NaN-holding
+    columns only, per-column LUTs) gives the host encoder's codes and patterns: shuffled category
+    orders, unused and str()-matched categories, NaN in several columns; a cell holding a category
+    that is not a state raises the reference's KeyError; other dtypes fall back (None)."""
+    from pgmpy_amd.inference.batch import encode_frame, group_patterns, ingest_columnar
+    from pgmpy_amd.utils import get_example_model
+
+    m = get_example_model("alarm")
+    rng = np.random.default_rng(4)
+    cols = sorted(m.nodes())[:12]
+    n = 1003  # not a multiple of 8: the NaN scan's tail
+    data = {}
+    for j, c in enumerate(cols):
+        st = [str(s) for s in m.states[c]]
+        cats = list(rng.permutation(st)) + (["unused"] if j % 3 == 0 else [])
+        codes = rng.integers(0, len(st), n)
+        vals = np.array([st[k] for k in codes], dtype=object)
+        if j in (2, 5, 9):
+            vals[rng.random(n) < 0.05] = None
+        data[c] = pd.Categorical(vals, categories=cats)
+    df = pd.DataFrame(data)
+    ev = ingest_columnar(m, df, cols)
+    want = encode_frame(m, df, cols)
+    rows = np.arange(n)
+    assert np.array_equal(ev.host_codes_for(list(range(len(cols))), rows), want)
+    sub = rows[::7]
+    assert np.array_equal(ev.host_codes_for([3, 9, 0], sub), want[[3, 9, 0]][:, sub])
+    exp = {tuple(np.nonzero(~mk)[0]): set(r.tolist()) for mk, r in group_patterns(want)}
+    got = {tuple(np.nonzero(~mk)[0]): set(r.tolist()) for mk, r in ev.groups}
+    assert got == exp and len(got) > 3
+    bad = df.copy()
+    bad[cols[0]] = pd.Categorical([str(m.states[cols[0]][0])] * (n - 1) + ["unused"],
+                                  categories=[str(s) for s in m.states[cols[0]]] + ["unused"])
+    with pytest.raises(KeyError):
+        ingest_columnar(m, bad, cols)
+    assert ingest_columnar(m, df.astype({cols[1]: object}), cols) is None
+
+
 def test_specialised_row_kernel_source_compiles_for_gfx950():
     """pgm_rows_plan_source (host-only) emits the C3 template's specialised kernel: every evidence
     column loaded once, one store per marginal entry, and it compiles for gfx950 with hipcc."""
