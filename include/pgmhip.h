@@ -434,6 +434,11 @@ int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s);
 int pgm_rows_ring_post(void *ring, uint32_t n_posted);
 int pgm_rows_ring_finish(void *ring);
 int pgm_rows_ring_cancel(void *ring);
+/* the ring's batch counter in pinned host memory and this launch's base: storing base + k (a plain,
+ * aligned 32-bit store, monotone, k <= n_batches) publishes batches [0, k) exactly as
+ * pgm_rows_ring_post(ring, k) does, without a library call per batch (finish then needs
+ * pgm_rows_ring_post(ring, n_batches) or the store of base + n_batches) */
+int pgm_rows_ring_counter(void *ring, uint32_t **counter, uint32_t *base);
 /* the ring's kernel name ("pgm_rows_ring"), resident grid and workgroup size */
 int pgm_rows_ring_kernel(void *ring, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
 int pgm_rows_ring_destroy(void *ring);

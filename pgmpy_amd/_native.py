@@ -209,6 +209,7 @@ _SIGS = {
     "pgm_rows_ring_post": ([_P, ctypes.c_uint32], ctypes.c_int),
     "pgm_rows_ring_finish": ([_P], ctypes.c_int),
     "pgm_rows_ring_cancel": ([_P], ctypes.c_int),
+    "pgm_rows_ring_counter": ([_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "pgm_rows_ring_kernel": ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                               ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "pgm_rows_ring_destroy": ([_P], ctypes.c_int),

@@ -2544,23 +2544,24 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "double *G; long long pad; };\n";
   pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_ring(const double *__restrict__ V, "
              "const pgm_ring_slot *__restrict__ D, unsigned n_slots, unsigned *ctl, unsigned *g, unsigned n_batches, "
-             "long long n, int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
+             "unsigned base, long long n, int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
   o += "  const int t = threadIdx.x;\n";
   pgmi_appendf(o, "  __shared__ double S[%d];\n  __shared__ unsigned seen_s, token_s, stop_s;\n", K * WG);
   for (int i = 0; i < K; ++i) pgmi_appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
   for (int i = 0; i < K; ++i) pgmi_appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
-  o += "  if (t == 0) { seen_s = 0u; token_s = 0u; stop_s = 0u; }\n  __syncthreads();\n#define VAL(i) S[i]\n";
+  o += "  if (t == 0) { seen_s = base; token_s = 0u; stop_s = 0u; }\n  __syncthreads();\n#define VAL(i) S[i]\n";
   pgmi_appendf(o, "  const unsigned long long W = (unsigned long long)gridDim.x * %d;\n", WG / 64);
   pgmi_appendf(o, "  const unsigned long long wv0 = (unsigned long long)blockIdx.x * %d + (t >> 6);\n", WG / 64);
   o += "  const unsigned long long chunks = (unsigned long long)(n + 127) / 128;\n"
        "  const unsigned long long items = chunks * n_batches;\n"
        "  const unsigned long long t0 = wall_clock64();\n"
        "  const bool lead = (t & 63) == 0;\n"
-       "  unsigned seen = 0u;\n"
+       "  unsigned seen = base;  /* counts are absolute over the ring's lifetime */\n"
        "  for (unsigned long long j = wv0; j < items; j += W) {\n"
        "    const unsigned bt = (unsigned)(j / chunks);\n"
+       "    const unsigned ab = base + bt;  /* the batch's absolute number: posted once ctl[0] > ab */\n"
        "    bool stop = false;\n"
-       "    while (bt >= seen) {\n"
+       "    while (ab >= seen) {\n"
        "      const unsigned sl = __hip_atomic_load(&seen_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
        "      if (sl > seen) { seen = sl; continue; }\n"
        "      if (__hip_atomic_load(&stop_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { stop = true; break; }\n"
@@ -2574,7 +2575,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "      }\n"
        "      for (;;) {  /* this wave speaks for its workgroup */\n"
        "        unsigned m = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-       "        if (m <= bt) {\n"
+       "        if (m <= ab) {\n"
        "          if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = true; break; }\n"
        "          unsigned poll = 0u;\n"
        "          if (lead) poll = atomicCAS(&g[1], 0u, 1u) == 0u ? 1u : 0u;\n"
@@ -2583,7 +2584,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "            const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
        "            if (p > m && lead) __hip_atomic_fetch_max(&g[0], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "            if (p > m) m = p;\n"
-       "            if (m <= bt) {\n"
+       "            if (m <= ab) {\n"
        "              const bool cancel = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;\n"
        "              const bool late = wall_clock64() - t0 > timeout;\n"
        "              if ((cancel || late) && lead) {\n"
@@ -2599,7 +2600,7 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "            break;\n"
        "          }\n"
        "        }\n"
-       "        if (m > bt) {\n"
+       "        if (m > ab) {\n"
        "          seen = m;\n"
        "          if (lead) atomicMax(&seen_s, m);\n"
        "          break;\n"
@@ -3991,7 +3992,10 @@ struct RowsRing {
   hipStream_t stream = nullptr;
   unsigned blocks = 0;
   bool running = false;
-  uint32_t n_batches = 0, posted = 0;
+  bool reset_gctl = true;   // the device counters need zeroing before the next launch (first / after a stop)
+  uint32_t n_batches = 0, posted = 0;  // this launch: batches to run, batches posted
+  uint32_t base = 0;        // absolute number of batches posted over the ring's lifetime before this launch
+  int wall_khz = 100000;    // the device's constant wall clock (timeout ticks)
 };
 
 int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint8_t *const *codes,
@@ -4054,6 +4058,9 @@ int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint
     return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_ring_create: %s", hipGetErrorString(e));
   }
   memset(rg->ctl, 0, 64);
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0) rg->wall_khz = khz;
+  (void)hipGetLastError();
   // every workgroup resident at once (one per CU at the default 1,024 threads)
   rg->blocks = (unsigned)std::max(1, cus * std::max(1, per_cu));
   *ring = rg;
@@ -4066,14 +4073,13 @@ int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
   if (!rg) return fail(PGM_EINVAL, "rows_ring_start: null ring");
   if (rg->running) return fail(PGM_EINVAL, "rows_ring_start: the ring is running (finish or cancel it first)");
   if (!(timeout_s > 0.0) || timeout_s > 600.0) return fail(PGM_EINVAL, "rows_ring_start: timeout must be in (0, 600] s");
-  int dev = 0, khz = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-  if (khz <= 0) khz = 100000;
-  unsigned long long ticks = (unsigned long long)(timeout_s * (double)khz * 1000.0);
-  __atomic_store_n(&rg->ctl[0], 0u, __ATOMIC_SEQ_CST);
+  unsigned long long ticks = (unsigned long long)(timeout_s * (double)rg->wall_khz * 1000.0);
+  // ctl[0] counts batches posted over the ring's lifetime (never reset: a launch's batch b is
+  // absolute batch base + b), so no device-side reset is needed between launches
   __atomic_store_n(&rg->ctl[1], 0u, __ATOMIC_SEQ_CST);
   __atomic_store_n(&rg->ctl[2], 0u, __ATOMIC_SEQ_CST);
+  rg->base = __atomic_load_n(&rg->ctl[0], __ATOMIC_SEQ_CST);
+  if (rg->base > 0xF0000000u) return fail(PGM_EINVAL, "rows_ring_start: batch counter exhausted (recreate the ring)");
   rg->n_batches = n_batches;
   rg->posted = 0;
   if (n_batches == 0) return PGM_OK;
@@ -4081,11 +4087,17 @@ int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
   const PgmRingSlot *d = rg->d_slots;
   unsigned ns = rg->n_slots, nb = n_batches;
   unsigned *ctl = rg->ctl_dev, *gc = rg->gctl;
+  unsigned base = rg->base;
   long long n = rg->n_rows;
   int32_t *ef = rg->err;
   int32_t md = rg->mode;
-  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, (void *)&gc, &nb, &n, (void *)&ef, &md, &ticks};
-  HIP_TRY(hipMemsetAsync(rg->gctl, 0, 64, rg->stream));  // the mirror, token and stop of this launch
+  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, (void *)&gc, &nb, &base, &n, (void *)&ef, &md, &ticks};
+  if (rg->reset_gctl) {  // mirror = base, token free, stop clear
+    unsigned init[16] = {base, 0u, 0u};
+    HIP_TRY(hipMemcpyAsync(rg->gctl, init, sizeof init, hipMemcpyHostToDevice, rg->stream));
+    HIP_TRY(hipStreamSynchronize(rg->stream));
+    rg->reset_gctl = false;
+  }
   HIP_TRY(hipModuleLaunchKernel(rg->h->jit_fn_ring, rg->blocks, 1, 1, (unsigned)ring_wg(), 1, 1, 0, rg->stream, args,
                                 nullptr));
   rg->running = true;
@@ -4096,12 +4108,13 @@ int pgm_rows_ring_post(void *ring, uint32_t n_posted) {
   RowsRing *rg = (RowsRing *)ring;
   if (!rg) return fail(PGM_EINVAL, "rows_ring_post: null ring");
   if (!rg->running) return fail(PGM_EINVAL, "rows_ring_post: the ring is not running");
+  rg->posted = std::max(rg->posted, __atomic_load_n(&rg->ctl[0], __ATOMIC_SEQ_CST) - rg->base);  // direct stores
   if (n_posted < rg->posted || n_posted > rg->n_batches)
     return fail(PGM_EINVAL, "rows_ring_post: %u batches posted, %u started, asked for %u", rg->posted, rg->n_batches,
                 n_posted);
   rg->posted = n_posted;
   // a sequentially consistent store: drained from the store buffer before this call returns
-  __atomic_store_n(&rg->ctl[0], n_posted, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&rg->ctl[0], rg->base + n_posted, __ATOMIC_SEQ_CST);
   return PGM_OK;
 }
 
@@ -4116,13 +4129,16 @@ int pgm_rows_ring_finish(void *ring) {
   RowsRing *rg = (RowsRing *)ring;
   if (!rg) return fail(PGM_EINVAL, "rows_ring_finish: null ring");
   if (!rg->running) return PGM_OK;
+  rg->posted = std::max(rg->posted, __atomic_load_n(&rg->ctl[0], __ATOMIC_SEQ_CST) - rg->base);  // direct stores
   if (rg->posted < rg->n_batches)
     return fail(PGM_EINVAL, "rows_ring_finish: only %u of %u batches posted (post them or cancel)", rg->posted,
                 rg->n_batches);
   const int st = ring_wait(rg);
   if (st != PGM_OK) return st;
-  if (__atomic_load_n(&rg->ctl[2], __ATOMIC_SEQ_CST) & 2u)
+  if (__atomic_load_n(&rg->ctl[2], __ATOMIC_SEQ_CST) & 2u) {
+    rg->reset_gctl = true;
     return fail(PGM_EDEVICE, "rows_ring_finish: the resident kernel timed out waiting for a batch");
+  }
   return PGM_OK;
 }
 
@@ -4132,7 +4148,16 @@ int pgm_rows_ring_cancel(void *ring) {
   if (!rg) return fail(PGM_EINVAL, "rows_ring_cancel: null ring");
   if (!rg->running) return PGM_OK;
   __atomic_store_n(&rg->ctl[1], 1u, __ATOMIC_SEQ_CST);
+  rg->reset_gctl = true;
   return ring_wait(rg);
+}
+
+int pgm_rows_ring_counter(void *ring, uint32_t **counter, uint32_t *base) {
+  RowsRing *rg = (RowsRing *)ring;
+  if (!rg || !counter || !base) return fail(PGM_EINVAL, "rows_ring_counter: null argument");
+  *counter = rg->ctl;
+  *base = rg->base;
+  return PGM_OK;
 }
 
 int pgm_rows_ring_kernel(void *ring, char *name, size_t cap, uint32_t *blocks, uint32_t *wg) {

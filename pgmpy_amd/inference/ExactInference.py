@@ -38,82 +38,94 @@ def _product_all(factors):
     return factor_product(*factors)
 
 
+_HEURISTICS = {"weightedminfill": WeightedMinFill, "minneighbors": MinNeighbors, "minweight": MinWeight,
+               "minfill": MinFill}
+
+
 class VariableElimination(Inference):
     # ------------------------------------------------------------------ classic VE
-    def _get_working_factors(self, evidence):
-        """Evidence-reduced working factors (ExactInference.py:35-66).
-
-        Identity-keyed dicts instead of sets of (factor, origin) tuples: hashing a
-        device factor would download its values."""
-        working = {node: {id(f): (f, None) for f in self.factors[node]} for node in self.factors}
-        if evidence:
-            for evidence_var in evidence:
-                for key, (factor, origin) in list(working[evidence_var].items()):
-                    reduced = factor.reduce([(evidence_var, evidence[evidence_var])], inplace=False)
-                    for var in reduced.scope():
-                        working[var].pop(key, None)
-                        working[var][id(reduced)] = (reduced, evidence_var)
-                del working[evidence_var]
-        return working
+    def _unique_factors(self):
+        """Every factor of the structures once, in first-seen order (self.factors lists a factor
+        under each of its variables)."""
+        seen = {}
+        for fs in self.factors.values():
+            for f in fs:
+                seen.setdefault(id(f), f)
+        return list(seen.values())
 
     def _get_elimination_order(self, variables, evidence, elimination_order, show_progress=True):
-        # ExactInference.py:68-139
-        to_eliminate = set(self.variables) - set(variables) - set(evidence.keys() if evidence else [])
-        if hasattr(elimination_order, "__iter__") and not isinstance(elimination_order, str):
-            if any(var in elimination_order for var in set(variables).union(set(evidence.keys() if evidence else []))):
-                raise ValueError("Elimination order contains variables which are in variables or evidence args")
-            elif any(var not in self.model.nodes() for var in elimination_order):
-                elimination_order = list(filter(lambda t: t in self.model.nodes(), elimination_order))
-            elif to_eliminate != set(elimination_order):
-                raise ValueError(f"Elimination order doesn't contain all the variables which need to be eliminated. "
-                                 f"The variables which need to be eliminated are {to_eliminate}")
-            return elimination_order
-        elif elimination_order is None or not isinstance(self.model, DiscreteBayesianNetwork):
-            return to_eliminate
-        elif isinstance(elimination_order, str):
-            heuristic = {"weightedminfill": WeightedMinFill, "minneighbors": MinNeighbors, "minweight": MinWeight,
-                         "minfill": MinFill}[elimination_order.lower()]
+        """The variables to eliminate, in order (ExactInference.py:68-139): an explicit order is
+        validated (no query / evidence variable in it; names outside the model dropped; otherwise it
+        must be exactly the variables to eliminate); None, or any order on a model that is not a
+        Bayesian network, leaves the set as it is; a name picks an EliminationOrder heuristic."""
+        ev = set(evidence) if evidence else set()
+        to_eliminate = set(self.variables) - set(variables) - ev
+        if isinstance(elimination_order, str):
+            if not isinstance(self.model, DiscreteBayesianNetwork):
+                return to_eliminate
+            heuristic = _HEURISTICS[elimination_order.lower()]
             return heuristic(self.model).get_elimination_order(nodes=to_eliminate, show_progress=show_progress)
+        if elimination_order is None or not hasattr(elimination_order, "__iter__"):
+            return to_eliminate
+        given = list(elimination_order)
+        if ev.union(variables).intersection(given):
+            raise ValueError("Elimination order contains variables which are in variables or evidence args")
+        nodes = self.model.nodes()
+        if any(v not in nodes for v in given):
+            return [v for v in given if v in nodes]
+        if set(given) != to_eliminate:
+            raise ValueError(f"Elimination order doesn't contain all the variables which need to be eliminated. "
+                             f"The variables which need to be eliminated are {to_eliminate}")
+        return given
 
     def _variable_elimination(self, variables, operation, evidence=None, elimination_order="MinFill", joint=True,
                               show_progress=True):
-        """Generalised VE (ExactInference.py:141-244): per variable, product then marginalize/maximize."""
+        """Classic variable elimination (ExactInference.py:141-244) as ONE planned contraction.
+
+        The reference multiplies and sums out one variable at a time over Python sets of working
+        factors.  Here every factor gets the evidence as a strided slice; a factor the evidence
+        reduces to a scalar is dropped (the reference's working sets lose it, L55-65); and the
+        elimination order becomes a contraction path (contraction.order_path: per variable, the live
+        operands holding it multiplied smallest-first, the variable summed — or maxed, operation
+        "maximize" — out of the last product), run as fused product+marginalize kernels.  What is
+        left is the product of the remaining factors over the query variables; its variable order is
+        the reference's list(set(...)) of them (L225-229), normalised for a Bayesian network."""
         if isinstance(variables, str):
             raise TypeError("variables must be a list of strings")
         if isinstance(evidence, str):
             raise TypeError("evidence must be a list of strings")
         if not variables:
-            all_factors = []
-            for factor_li in self.factors.values():
-                all_factors.extend(factor_li)
-            uniq = list({id(f): f for f in all_factors}.values())
+            uniq = self._unique_factors()
             return factor_product(*uniq) if joint else set(uniq)
-        eliminated = set()
-        working = self._get_working_factors(evidence)
-        order = self._get_elimination_order(variables, evidence, elimination_order, show_progress=show_progress)
-        for var in order:
-            factors = [f for f, _ in working[var].values() if not set(f.variables).intersection(eliminated)]
-            phi = factor_product(*factors)
-            phi = getattr(phi, operation)([var], inplace=False)
-            del working[var]
-            for variable in phi.variables:
-                working[variable][id(phi)] = (phi, var)
-            eliminated.add(var)
-        final = {}
-        for node in working:
-            for key, (factor, origin) in working[node].items():
-                if not set(factor.variables).intersection(eliminated):
-                    final[key] = factor
-        final = list(final.values())
+        order = list(self._get_elimination_order(variables, evidence, elimination_order,
+                                                 show_progress=show_progress))
+        evidence = evidence or {}
+        operands, names, card = [], {}, {}
+        for f in self._unique_factors():
+            fixed = {v: f.get_state_no(v, evidence[v]) for v in f.variables if v in evidence}
+            rest = [v for v in f.variables if v not in fixed]
+            if not rest:
+                continue
+            t = f._d()
+            if fixed:
+                t = t[tuple(fixed.get(v, slice(None)) for v in f.variables)]
+            operands.append((t, rest))
+            for v in rest:
+                names.setdefault(v, f.state_names[v])
+                card[v] = int(t.shape[rest.index(v)])
+        eliminated = set(order)
+        out_vars = list(set(v for v in names if v not in eliminated))
+        reduce = "sum" if operation == "marginalize" else "max"
+        values = contract_factors(operands, out_vars, reduce=reduce, order=order)
+        phi = DiscreteFactor(out_vars, [card[v] for v in out_vars], values,
+                             state_names={v: names[v] for v in out_vars})
+        is_bn = isinstance(self.model, DiscreteBayesianNetwork)
         if joint:
-            if isinstance(self.model, DiscreteBayesianNetwork):
-                return factor_product(*final).normalize(inplace=False)
-            return factor_product(*final)
+            return phi.normalize(inplace=False) if is_bn else phi
         out = {}
-        for query_var in variables:
-            phi = factor_product(*final)
-            m = phi.marginalize(list(set(variables) - set([query_var])), inplace=False)
-            out[query_var] = m.normalize(inplace=False) if isinstance(self.model, DiscreteBayesianNetwork) else m
+        for q in variables:
+            m = phi.marginalize(list(set(variables) - {q}), inplace=False)
+            out[q] = m.normalize(inplace=False) if is_bn else m
         return out
 
     # ------------------------------------------------------------------ queries
@@ -428,43 +440,70 @@ class BeliefPropagation(Inference):
         return all(frozenset(e) in self.sepset_beliefs and self.sepset_beliefs[frozenset(e)] is not None
                    for e in self.junction_tree.edges()) or len(self.junction_tree.nodes()) == 1
 
+    def _spanning_cliques(self, needed):
+        """The smallest subtree of the junction tree holding every clique that contains a variable
+        of `needed`: repeatedly drop leaves that hold none (in a tree this is the union of the paths
+        between those cliques, the subtree of ExactInference.py:1047-1073).  Returns (cliques, edges)."""
+        jt = self.junction_tree
+        keep = {c for c in jt.nodes() if needed.intersection(c)}
+        alive = set(jt.nodes())
+        deg = {c: jt.degree(c) for c in alive}
+        leaves = [c for c in alive if deg[c] <= 1 and c not in keep]
+        while leaves and len(alive) > 1:
+            c = leaves.pop()
+            if c not in alive:
+                continue
+            alive.discard(c)
+            for nb in jt.neighbors(c):
+                if nb in alive:
+                    deg[nb] -= 1
+                    if deg[nb] <= 1 and nb not in keep:
+                        leaves.append(nb)
+        edges = [(a, b) for a, b in jt.edges() if a in alive and b in alive]
+        return [c for c in jt.nodes() if c in alive], edges
+
     def _query(self, variables, operation, evidence=None, joint=True, show_progress=True):
-        """Out-of-clique inference on the calibrated tree (ExactInference.py:997-1115)."""
+        """Out-of-clique inference on the calibrated tree (ExactInference.py:997-1115; Koller &
+        Friedman Alg. 10.4).
+
+        A calibrated junction tree holds the unnormalised distribution as prod_C beta_C / prod_S mu_S
+        over its cliques and separators, and so does the smallest subtree spanning the cliques that
+        hold a query or evidence variable.  The query is that product, with each separator's mu
+        divided into the belief on one side of its edge (0/0 -> 0, the reference's divide,
+        DiscreteFactor.py:859-863) and the evidence applied as strided slices, contracted to the
+        query variables in one planned device contraction.  "marginalize" returns the normalised
+        joint (or per-variable marginals); "maximize" the first-index argmax of the joint over the
+        query variables (the reference's VariableElimination.map_query on the subtree)."""
         if not self._is_converged(operation=operation):
             self.calibrate()
-        query_variables = [variables] if not isinstance(variables, (list, tuple, set)) else list(variables)
-        query_variables.extend(evidence.keys() if evidence else [])
-        nodes_with_query_variables = set()
-        for var in query_variables:
-            nodes_with_query_variables.update(filter(lambda x: var in x, self.junction_tree.nodes()))
-        subtree_nodes = set(nodes_with_query_variables)
-        nq = tuple(nodes_with_query_variables)
-        for i in range(len(nq) - 1):
-            subtree_nodes.update(nx.shortest_path(self.junction_tree, nq[i], nq[i + 1]))
-        sub_graph = self.junction_tree.subgraph(subtree_nodes)
-        if len(subtree_nodes) == 1:
-            subtree = JunctionTree()
-            subtree.add_node(next(iter(subtree_nodes)))
-        else:
-            subtree = JunctionTree(sub_graph.edges())
-        if len(subtree.nodes()) == 1:
-            root_node = list(subtree.nodes())[0]
-        else:
-            root_node = tuple(filter(lambda x: len(list(subtree.neighbors(x))) == 1, subtree.nodes()))[0]
-        potentials = [self.clique_beliefs[root_node]]
-        parent_nodes = {root_node}
-        traversed = set()
-        while parent_nodes:
-            parent = parent_nodes.pop()
-            for child in set(subtree.neighbors(parent)) - traversed:
-                potentials.append(self.clique_beliefs[child] / self.sepset_beliefs[frozenset([parent, child])])
-                parent_nodes.update([child])
-            traversed.update([parent])
-        subtree.add_factors(*potentials)
-        ve = VariableElimination(subtree)
-        if operation == "marginalize":
-            return ve.query(variables=variables, evidence=evidence, joint=joint, show_progress=show_progress)
-        return ve.map_query(variables=variables, evidence=evidence, show_progress=show_progress)
+        variables = [variables] if not isinstance(variables, (list, tuple, set)) else list(variables)
+        evidence = evidence or {}
+        cliques, edges = self._spanning_cliques(set(variables) | set(evidence))
+        terms = {c: self.clique_beliefs[c] for c in cliques}
+        if edges:  # orient the edges away from the first clique; mu joins the child's belief
+            tree = nx.Graph(edges)
+            for parent, child in nx.bfs_edges(tree, cliques[0]):
+                terms[child] = terms[child] / self.sepset_beliefs[frozenset((parent, child))]
+        operands, names = [], {}
+        for f in terms.values():
+            fixed = {v: f.get_state_no(v, evidence[v]) for v in f.variables if v in evidence}
+            rest = [v for v in f.variables if v not in fixed]
+            t = f._d()
+            if fixed:
+                t = t[tuple(fixed.get(v, slice(None)) for v in f.variables)]
+            operands.append((t, rest))
+            for v in rest:
+                names.setdefault(v, f.state_names[v])
+        values = contract_factors(operands, list(variables))
+        phi = DiscreteFactor(list(variables), list(values.shape), values,
+                             state_names={v: names[v] for v in variables})
+        if operation == "maximize":
+            idx = int(E.to_host(E.argmax_rows(phi._d(), list(range(phi._d().dim()))).double())[0])
+            return {var: value for var, value in phi.assignment([idx])[0]}
+        if joint:
+            return phi.normalize(inplace=False)
+        return {v: phi.marginalize([u for u in variables if u != v], inplace=False).normalize(inplace=False)
+                for v in variables}
 
     @E.serialized
     def query(self, variables, evidence=None, virtual_evidence=None, joint=True, show_progress=True):

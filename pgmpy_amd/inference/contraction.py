@@ -206,6 +206,58 @@ def elimination_path(operand_labels, out_labels, dims):
     return steps, final_id
 
 
+def order_path(operand_labels, out_labels, dims, order):
+    """A contraction path that eliminates variables in a GIVEN order (classic variable elimination,
+    pgmpy/inference/ExactInference.py:141-244, whose order comes from an EliminationOrder heuristic or
+    the caller): for each variable, the live operands holding it are multiplied smallest-first and
+    the variable is summed (or maxed) out with the last product; a label no other operand or the
+    output needs is summed in the same pass.  Labels the order omits are eliminated afterwards,
+    then what is left (output labels only) is multiplied smallest-first.  greedy_path's format."""
+    out_set = set(out_labels)
+    ops = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    holders = {}
+    for i, ls in ops.items():
+        for l in ls:
+            holders.setdefault(l, set()).add(i)
+    steps = []
+    ids = count(len(operand_labels))
+
+    def kept(labels, exclude):
+        return [l for l in labels if l in out_set or len(holders[l] - exclude) > 0]
+
+    def retire(olds, keep, kind):
+        nid = next(ids)
+        steps.append((kind,) + tuple(olds) + (keep, nid))
+        for o in olds:
+            for l in ops[o]:
+                holders[l].discard(o)
+            del ops[o]
+        for l in keep:
+            holders[l].add(nid)
+        ops[nid] = keep
+        return nid
+
+    def size_key(i):
+        return (_size(ops[i], dims), i)
+
+    rest = [l for l in holders if l not in out_set and l not in set(order)]
+    for v in list(order) + rest:
+        if v in out_set or not holders.get(v):
+            continue
+        inv = sorted(holders[v], key=size_key)
+        while len(inv) > 1:
+            a, b = inv[0], inv[1]
+            nid = retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
+            inv = sorted([nid] + inv[2:], key=size_key)
+        if v in ops[inv[0]]:
+            retire([inv[0]], [l for l in ops[inv[0]] if l != v], "reduce")
+    while len(ops) > 1:
+        a, b = sorted(ops, key=size_key)[:2]
+        retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
+    (final_id,) = ops.keys() if ops else (None,)
+    return steps, final_id
+
+
 def path_cost(steps, operand_labels, dims):
     """(bytes, flops, depth) of a path: 8 (|A| + |B| + |C|) bytes and 2 |index space| flops per
     pairwise step, |A| + |C| per reduction; depth = the longest chain of dependent steps."""
@@ -272,16 +324,21 @@ PACK_MIN_WORK = 1 << 20   # ... and at least this large an index space
 PATH_CACHE_SIZE = 256
 
 
-def compiled_path(operand_labels, out_labels, dims):
-    """greedy_path plus, per pairwise step, the dense-GEMM classification (engine.gemm_shape),
-    cached on the contraction's structure: repeated queries with the same query / evidence
-    variables (C2's pattern; every row batch of a predict pattern) re-plan nothing."""
-    key = (tuple(tuple((l, int(dims[l])) for l in ls) for ls in operand_labels), tuple(out_labels))
+def compiled_path(operand_labels, out_labels, dims, order=None):
+    """choose_path (or, with `order`, order_path) plus, per pairwise step, the dense-GEMM
+    classification (engine.gemm_shape), cached on the contraction's structure: repeated queries with
+    the same query / evidence variables (C2's pattern; every row batch of a predict pattern) re-plan
+    nothing."""
+    key = (tuple(tuple((l, int(dims[l])) for l in ls) for ls in operand_labels), tuple(out_labels),
+           None if order is None else tuple(order))
     hit = _PATHS.get(key)
     if hit is not None:
         _PATHS.move_to_end(key)
         return hit
-    steps, final_id = choose_path(operand_labels, out_labels, dims)
+    if order is None:
+        steps, final_id = choose_path(operand_labels, out_labels, dims)
+    else:
+        steps, final_id = order_path(operand_labels, out_labels, dims, order)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     plan = []
     for st in steps:
@@ -319,13 +376,14 @@ def compiled_path(operand_labels, out_labels, dims):
     return hit
 
 
-def contract_factors(operands, out_labels, reduce="sum", prog=None):
+def contract_factors(operands, out_labels, reduce="sum", prog=None, order=None):
     """sum_{labels not in out} prod operands, on the device.
 
     operands: list of (device tensor, labels).  Returns a tensor over
     out_labels (C-order).  reduce="max" gives the max-product variant.  With a
     pgmpy_amd.program.Program the launches are recorded (buffers preallocated)
-    instead of issued."""
+    instead of issued.  order: eliminate the labels in this order (order_path)
+    instead of the planner's choice."""
     run = prog if prog is not None else E
     if not operands:
         raise ValueError("nothing to contract")
@@ -340,7 +398,7 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None):
     for l in out_labels:
         if l not in dims:
             raise ValueError(f"output label {l!r} not in any operand")
-    plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims)
+    plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims, order=order)
     live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
 
     after = []  # contractions that read operands packed in the same level (recorded after its batch)

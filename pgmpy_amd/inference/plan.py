@@ -659,16 +659,31 @@ class RowRing:
         self._keep = (plan, slots, err)
         self._h = h
         self._post = L.pgm_rows_ring_post
+        self._n, self._posted = -1, 0  # no launch yet: a post is refused by the library
+        self._start = L.pgm_rows_ring_start
+        ptr, base = ctypes.c_void_p(), ctypes.c_uint32()
+        N.check(L.pgm_rows_ring_counter(h, ctypes.byref(ptr), ctypes.byref(base)), "rows_ring_counter")
+        # the pinned host counter as a one-element uint32 array: a post is one aligned store
+        self._counter = np.ctypeslib.as_array((ctypes.c_uint32 * 1).from_address(ptr.value))
+        self._base = base.value
         self.outs = outs
         self.n_rows = int(n_rows)
 
     def start(self, n_batches, timeout_s=5.0):
-        N.check(N.lib().pgm_rows_ring_start(self._h, int(n_batches), float(timeout_s)), "rows_ring_start")
+        base = int(self._counter[0])  # the launch's base: batches posted over the ring's lifetime
+        N.check(self._start(self._h, int(n_batches), float(timeout_s)), "rows_ring_start")
+        self._base = base
+        self._n = int(n_batches)
+        self._posted = 0
 
     def post(self, n_posted):
-        st = self._post(self._h, int(n_posted))
-        if st != 0:
+        """Publish batches [0, n_posted) of the running launch: one store into the pinned counter
+        (pgm_rows_ring_counter; the same as pgm_rows_ring_post without a library call)."""
+        if not self._posted <= n_posted <= self._n:
+            st = self._post(self._h, int(n_posted))  # the library reports the misuse
             N.check(st, "rows_ring_post")
+        self._posted = n_posted
+        self._counter[0] = self._base + n_posted
 
     def finish(self):
         N.check(N.lib().pgm_rows_ring_finish(self._h), "rows_ring_finish")
