@@ -550,6 +550,37 @@ def predict_frame(model, data):
     return out.sort_index()
 
 
+def _hash_groups_exact(ev, first, inv):
+    """Every row's codes equal its hash group's representative row (no 128-bit collision merged two
+    different evidence rows): one device comparison of the codes against the representatives."""
+    import torch
+
+    if len(first) == ev.n:
+        return True
+    idx = torch.as_tensor(first[inv].astype(np.int64), device=ev.codes.device)
+    return bool(torch.equal(ev.codes.index_select(1, idx), ev.codes))
+
+
+def _raw_values_ambiguous(model, data, columns):
+    """Whether two distinct raw cell values of a column map to one state (the str() fallback:
+    1 and "1"; or two categories with the same state), so grouping by state codes would merge rows
+    the reference's groupby over raw values keeps apart."""
+    import pandas as pd
+
+    states = model.states
+    for col in columns:
+        v = data[col]
+        st = list(states[col])
+        if isinstance(v.dtype, pd.CategoricalDtype):
+            v = pd.Series(v.cat.categories)
+        if v.dtype != object:
+            continue  # one numeric/bool dtype: str() is one to one on it
+        vals = v.dropna().to_numpy(dtype=object)
+        if len(vals) and (_lookup_codes(vals, st) < 0).any():
+            return True  # some cell reaches its state through str(): mixed raw types may merge
+    return False
+
+
 def predict_stochastic_frame(model, data, seed=None):
     """DiscreteBayesianNetwork.predict(stochastic=True) (DiscreteBayesianNetwork.py:866-910).
 
@@ -573,6 +604,12 @@ def predict_stochastic_frame(model, data, seed=None):
     ev = ingest_frame(model, data, columns, row_hash=True)
     _, first, inv = np.unique(ev.row_hash, axis=0, return_index=True, return_inverse=True)
     inv = inv.reshape(-1)
+    if not _hash_groups_exact(ev, first, inv) or _raw_values_ambiguous(model, data, columns):
+        # a hash collision, or cells whose raw values differ but reach the same state (1 and "1"
+        # through the str() fallback): the reference's own grouping of the raw values (L867)
+        gid = data.groupby(columns, dropna=False, sort=False).ngroup().to_numpy()
+        _, first, inv = np.unique(gid, return_index=True, return_inverse=True)
+        inv = inv.reshape(-1)
     counts = np.bincount(inv, minlength=len(first))
     srt = np.argsort(inv, kind="stable")
     starts = np.concatenate([[0], np.cumsum(counts)[:-1]])

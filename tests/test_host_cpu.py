@@ -207,6 +207,15 @@ def test_encode_frame_categorical_numeric_and_nan():
     codes = encode_frame(bn, pd.DataFrame({"a": [1, 0, 1], "b": ["1", "0", 1]}))
     assert codes.tolist() == [[1, 0, 1], [1, 0, 1]]
 
+    # predict(stochastic=True) groups by state codes only where raw value <-> state is one to one
+    from pgmpy_amd.inference.batch import _raw_values_ambiguous
+
+    assert not _raw_values_ambiguous(bn, pd.DataFrame({"a": ["1", "0", None]}), ["a"])
+    assert not _raw_values_ambiguous(bn, pd.DataFrame({"a": [1, 0, 1]}), ["a"])  # one int dtype
+    assert _raw_values_ambiguous(bn, pd.DataFrame({"a": [1, "1", "0"]}), ["a"])  # 1 and "1" merge
+    assert not _raw_values_ambiguous(bn, pd.DataFrame({"a": pd.Categorical(["1", "0"])}), ["a"])
+    assert _raw_values_ambiguous(bn, pd.DataFrame({"a": pd.Categorical([1, "1"])}), ["a"])
+
 
 def test_columnar_ingestion_matches_host_encoder():
     """ingest_columnar (categorical frames: zero-copy codes, NaN patterns from the NaN-holding
