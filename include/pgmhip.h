@@ -304,8 +304,18 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
 /* a findings-indicator job (pgm_indicator's arguments): all of a BP sweep's findings in one launch */
 int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
                             int64_t s_state, int64_t s_row, int32_t *err_flag);
+/* Levelled batch (several dependency levels of a compiled contraction path in ONE launch): jobs added
+ * after pgm_batch_add_level belong to the next level and may read earlier levels' outputs.  run then
+ * launches one persistent kernel whose workgroups (all resident: the grid is capped by the occupancy)
+ * stride over each level's blocks and meet at a grid barrier (agent-scope release/acquire) between
+ * levels — the levels of ExactInference.py:404-406's contraction without one launch each.  A barrier
+ * that waits > 2 s (residency violated by another persistent kernel) gives up; pgm_batch_info then
+ * reports timed_out = 1 (and resets the barrier).  One handle must not run on two streams at once. */
+int pgm_batch_add_level(void *handle);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
+/* levels, persistent grid (0: one launch per level), and (synchronising) whether a barrier timed out */
+int pgm_batch_info(void *handle, int32_t *n_levels, int32_t *grid, int32_t *timed_out);
 int pgm_batch_destroy(void *handle);
 
 

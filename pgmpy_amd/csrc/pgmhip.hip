@@ -1321,11 +1321,66 @@ __device__ __forceinline__ void batch_contract_c(const BatchJob &J, uint64_t tid
   }
 }
 
+__device__ __forceinline__ void batch_block(const BatchJob *__restrict__ jobs, const uint32_t *__restrict__ block_job,
+                                            uint32_t b);
+
 __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs,
                                                const uint32_t *__restrict__ block_job) {
-  const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[blockIdx.x]);
+  batch_block(jobs, block_job, blockIdx.x);
+}
+
+// Grid-wide barrier of a persistent launch whose G workgroups are all resident (the host sizes the grid
+// from the occupancy).  bar[0] counts arrivals, bar[1] is the generation (monotonic over launches, so
+// nothing is reset between runs), bar[2] the timeout status.  Workgroup stores are made visible at
+// agent scope before arriving (release) and other workgroups' stores after leaving (acquire).
+__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned G, unsigned long long deadline) {
+  __shared__ int ok_s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned a = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    if (a == G - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 1, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        if (wall_clock64() > deadline) {
+          ok = 0;
+          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    ok_s = ok;
+  }
+  __syncthreads();
+  return ok_s != 0;
+}
+
+// Several dependency levels of batch jobs in ONE launch: G resident workgroups stride over each level's
+// blocks (level_off[l] .. level_off[l+1] of the block map), then meet at a grid barrier before the next
+// level.  Replaces one launch per level (C2's 29-level plan) with one launch + 28 barriers.
+__global__ __launch_bounds__(256) void k_batch_levels(const BatchJob *__restrict__ jobs,
+                                                      const uint32_t *__restrict__ block_job,
+                                                      const uint32_t *__restrict__ level_off, uint32_t n_levels,
+                                                      unsigned *bar, unsigned long long timeout) {
+  const unsigned G = gridDim.x;
+  const unsigned long long deadline = wall_clock64() + timeout;
+  for (uint32_t l = 0; l < n_levels; ++l) {
+    const uint32_t e = level_off[l + 1];
+    for (uint32_t b = level_off[l] + blockIdx.x; b < e; b += G) batch_block(jobs, block_job, b);
+    if (l + 1 < n_levels && !grid_barrier(bar, G, deadline)) return;
+  }
+}
+
+__device__ __forceinline__ void batch_block(const BatchJob *__restrict__ jobs, const uint32_t *__restrict__ block_job,
+                                            uint32_t b) {
+  const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[b]);
   const BatchJob &J = jobs[j];
-  const uint64_t tid = (uint64_t)(blockIdx.x - J.block0) * blockDim.x + threadIdx.x;
+  const uint64_t tid = (uint64_t)(b - J.block0) * blockDim.x + threadIdx.x;
   const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
   if (J.kind == 1) {
     gather_body(J.g, J.A, J.codes, J.C, J.err, tid, n);
@@ -3152,9 +3207,34 @@ static int plan_gather(const pgm_gather_desc *d, GatherK &k) {
 struct BatchHandle {
   std::vector<BatchJob> jobs;
   std::vector<uint32_t> block_job;
+  std::vector<uint32_t> level_off{0};  // levelled batch: first block of each level (+ the end)
   BatchJob *d_jobs = nullptr;
   uint32_t *d_map = nullptr;
+  uint32_t *d_level = nullptr;
+  unsigned *d_bar = nullptr;  // grid barrier: arrivals, generation, timeout status
+  unsigned grid = 0;          // persistent grid (levelled batch)
+  unsigned long long timeout_ticks = 0;
 };
+
+// workgroups of k_batch_levels that are resident at once (the grid barrier needs all of them),
+// capped by PGM_BATCH_LEVELS_GRID (A/B knob)
+static unsigned batch_levels_cap() {
+  static unsigned cap = 0;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_batch_levels, 256, 0) == hipSuccess)
+      cap = (unsigned)std::max(0, cus * per);
+    (void)hipGetLastError();
+    if (const char *e = getenv("PGM_BATCH_LEVELS_GRID")) {
+      const long v = atol(e);
+      if (v > 0 && cap) cap = std::min<unsigned>(cap, (unsigned)v);
+    }
+  });
+  return cap;
+}
 
 static const uint32_t kBatchMaxBlocksPerJob = 256;
 
@@ -3300,23 +3380,57 @@ int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, 
   return batch_append(h, J, (uint64_t)(n_rows * card));
 }
 
+int pgm_batch_add_level(void *handle) {
+  STALE_PROBE();
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "batch_add_level: null handle");
+  if (h->d_jobs) return fail(PGM_EINVAL, "batch_add_level: already finalized");
+  if (h->block_job.size() > h->level_off.back()) h->level_off.push_back((uint32_t)h->block_job.size());
+  return PGM_OK;
+}
+
+static void batch_free(BatchHandle *h) {
+  if (h->d_jobs) (void)hipFree(h->d_jobs);
+  if (h->d_map) (void)hipFree(h->d_map);
+  if (h->d_level) (void)hipFree(h->d_level);
+  if (h->d_bar) (void)hipFree(h->d_bar);
+  h->d_jobs = nullptr;
+  h->d_map = nullptr;
+  h->d_level = nullptr;
+  h->d_bar = nullptr;
+}
+
 int pgm_batch_finalize(void *handle) {
   STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "batch_finalize: null handle");
   if (h->d_jobs || h->jobs.empty()) return PGM_OK;
+  if (h->level_off.back() < h->block_job.size()) h->level_off.push_back((uint32_t)h->block_job.size());
+  const size_t n_levels = h->level_off.size() - 1;
   hipError_t e = hipMalloc((void **)&h->d_jobs, sizeof(BatchJob) * h->jobs.size());
   if (e == hipSuccess) e = hipMalloc((void **)&h->d_map, sizeof(uint32_t) * h->block_job.size());
   if (e == hipSuccess)
     e = hipMemcpy(h->d_jobs, h->jobs.data(), sizeof(BatchJob) * h->jobs.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipMemcpy(h->d_map, h->block_job.data(), sizeof(uint32_t) * h->block_job.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && n_levels > 1) {
+    uint32_t widest = 0;
+    for (size_t l = 0; l < n_levels; ++l) widest = std::max(widest, h->level_off[l + 1] - h->level_off[l]);
+    h->grid = std::min(widest, batch_levels_cap());
+    int dev = 0, khz = 100000;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    (void)hipGetLastError();
+    h->timeout_ticks = (unsigned long long)std::max(khz, 1) * 1000ull * 2ull;  // 2 s per launch
+    e = hipMalloc((void **)&h->d_level, sizeof(uint32_t) * h->level_off.size());
+    if (e == hipSuccess)
+      e = hipMemcpy(h->d_level, h->level_off.data(), sizeof(uint32_t) * h->level_off.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void **)&h->d_bar, 4 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->d_bar, 0, 4 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    if (h->d_jobs) (void)hipFree(h->d_jobs);
-    if (h->d_map) (void)hipFree(h->d_map);
-    h->d_jobs = nullptr;
-    h->d_map = nullptr;
+    batch_free(h);
     return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "batch_finalize: %s", hipGetErrorString(e));
   }
   return PGM_OK;
@@ -3328,8 +3442,40 @@ int pgm_batch_run(void *handle, void *stream) {
   if (!h) return fail(PGM_EINVAL, "batch_run: null handle");
   if (h->jobs.empty()) return PGM_OK;
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
-  hipLaunchKernelGGL(k_batch, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
+  const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
+  if (n_levels > 1 && h->grid > 0) {
+    hipLaunchKernelGGL(k_batch_levels, dim3(h->grid), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level,
+                       n_levels, h->d_bar, h->timeout_ticks);
+  } else if (n_levels > 1) {  // no occupancy figure: one launch per level, in order on the stream
+    for (uint32_t l = 0; l < n_levels; ++l)
+      hipLaunchKernelGGL(k_batch, dim3(h->level_off[l + 1] - h->level_off[l]), dim3(256), 0, S(stream), h->d_jobs,
+                         h->d_map + h->level_off[l]);
+  } else {
+    hipLaunchKernelGGL(k_batch, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
+  }
   HIP_TRY(hipGetLastError());
+  return PGM_OK;
+}
+
+int pgm_batch_info(void *handle, int32_t *n_levels, int32_t *grid, int32_t *timed_out) {
+  STALE_PROBE();
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "batch_info: null handle");
+  if (n_levels) *n_levels = (int32_t)h->level_off.size() - 1;
+  if (grid) *grid = (int32_t)h->grid;
+  if (timed_out) {
+    *timed_out = 0;
+    if (h->d_bar) {  // after the launches completed: a barrier that timed out leaves its words reset
+      unsigned w[4] = {0, 0, 0, 0};
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipMemcpy(w, h->d_bar, sizeof w, hipMemcpyDeviceToHost));
+      if (w[2]) {
+        *timed_out = 1;
+        HIP_TRY(hipMemset(h->d_bar, 0, sizeof w));
+        HIP_TRY(hipDeviceSynchronize());
+      }
+    }
+  }
   return PGM_OK;
 }
 
@@ -3337,8 +3483,7 @@ int pgm_batch_destroy(void *handle) {
   STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return PGM_OK;
-  if (h->d_jobs) (void)hipFree(h->d_jobs);
-  if (h->d_map) (void)hipFree(h->d_map);
+  batch_free(h);
   delete h;
   return PGM_OK;
 }

@@ -22,6 +22,9 @@ PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
 # specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
 # take or that are below the engine's own threshold, PGM_PM_JIT_MIN)
 PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 18))  # C4 1,000 rows: 745K -> 856K
+# consecutive dependency levels made only of batch jobs run as ONE persistent launch with a grid barrier
+# between levels (pgm_batch_add_level) instead of one launch each.  A/B knob: PGM_BATCH_LEVELS=0.
+LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "1") != "0"
 
 
 def _key(t):
@@ -71,6 +74,7 @@ class Program:
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
         self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
+        self._chains = []  # levelled batch handles (several dependency levels in one launch)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
@@ -158,41 +162,102 @@ class Program:
         by_level = [[] for _ in range(n_lv)]
         for r in self._recs:
             by_level[r.level].append(r)
+        chain = []  # consecutive levels of batch jobs only, run as ONE levelled batch launch
         for lv, recs in enumerate(by_level):
-            small = [r for r in recs if r.job is not None]
-            n0 = len(self._steps)
-            merged = self._merge_pm([r for r in recs if r.job is None and r.pm is not None])
-            for r in recs:
-                if r in merged:
-                    continue
-                if r.job is None or len(small) == 1:
-                    self._steps.append(r.fn)
-                    self.notes.append(r.note)
-                    self.step_bytes.append(r.nbytes)
-                    if r.pm is not None:
-                        self._pm_launch.append(r.pm)
-            if len(small) < 2:
-                self.step_levels.extend([lv] * (len(self._steps) - n0))
+            if LEVEL_CHAIN and recs and all(r.job is not None for r in recs):
+                chain.append((lv, recs))
                 continue
-            L = N.lib()
-            h = ctypes.c_void_p()
-            N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
-            self._handles.append(h)
-            for r in small:
-                kind, args = r.job
-                if kind == "contract":
-                    N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
-                elif kind == "gather":
-                    N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
-                elif kind == "indicator":
-                    N.check(L.pgm_batch_add_indicator(h, *args), "batch_add_indicator")
-                else:
-                    N.check(L.pgm_batch_add_product_n(h, *args), "batch_add_product_n")
-            N.check(L.pgm_batch_finalize(h), "batch_finalize")
-            self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
-            self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
-            self.step_bytes.append(sum(r.nbytes for r in small))
+            self._flush_chain(chain)
+            chain = []
+            self._emit_level(lv, recs)
+        self._flush_chain(chain)
+
+    @staticmethod
+    def _add_jobs(h, recs):
+        L = N.lib()
+        for r in recs:
+            kind, args = r.job
+            if kind == "contract":
+                N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
+            elif kind == "gather":
+                N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
+            elif kind == "indicator":
+                N.check(L.pgm_batch_add_indicator(h, *args), "batch_add_indicator")
+            else:
+                N.check(L.pgm_batch_add_product_n(h, *args), "batch_add_product_n")
+
+    def _new_batch(self):
+        h = ctypes.c_void_p()
+        N.check(N.lib().pgm_batch_create(ctypes.byref(h)), "batch_create")
+        self._handles.append(h)
+        return h
+
+    def _flush_chain(self, chain):
+        """Consecutive levels made only of batch jobs: one levelled batch (pgm_batch_add_level between
+        levels; one persistent launch with a grid barrier per level boundary)."""
+        if len(chain) < 2:
+            for lv, recs in chain:
+                self._emit_level(lv, recs)
+            return
+        L = N.lib()
+        h = self._new_batch()
+        for i, (_, recs) in enumerate(chain):
+            if i:
+                N.check(L.pgm_batch_add_level(h), "batch_add_level")
+            self._add_jobs(h, recs)
+        N.check(L.pgm_batch_finalize(h), "batch_finalize")
+        self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+        self._chains.append(h)
+        n_jobs = sum(len(recs) for _, recs in chain)
+        self.notes.append(f"levels {chain[0][0]}-{chain[-1][0]} as one levelled batch of {n_jobs} jobs")
+        self.step_bytes.append(sum(r.nbytes for _, recs in chain for r in recs))
+        self.step_levels.append(chain[0][0])
+
+    def _emit_level(self, lv, recs):
+        """One dependency level: its unbatched launches, then one batch launch of its small jobs."""
+        small = [r for r in recs if r.job is not None]
+        n0 = len(self._steps)
+        merged = self._merge_pm([r for r in recs if r.job is None and r.pm is not None])
+        for r in recs:
+            if r in merged:
+                continue
+            if r.job is None or len(small) == 1:
+                self._steps.append(r.fn)
+                self.notes.append(r.note)
+                self.step_bytes.append(r.nbytes)
+                if r.pm is not None:
+                    self._pm_launch.append(r.pm)
+        if len(small) < 2:
             self.step_levels.extend([lv] * (len(self._steps) - n0))
+            return
+        L = N.lib()
+        h = self._new_batch()
+        self._add_jobs(h, small)
+        N.check(L.pgm_batch_finalize(h), "batch_finalize")
+        self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+        self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
+        self.step_bytes.append(sum(r.nbytes for r in small))
+        self.step_levels.extend([lv] * (len(self._steps) - n0))
+
+    def barrier_timed_out(self):
+        """Whether a levelled batch's grid barrier gave up since the last check (synchronises)."""
+        L = N.lib()
+        out = False
+        for h in self._chains:
+            t = ctypes.c_int32()
+            N.check(L.pgm_batch_info(h, None, None, ctypes.byref(t)), "batch_info")
+            out = out or bool(t.value)
+        return out
+
+    def chain_info(self):
+        """[(levels, persistent grid)] of the levelled batches (profiling aid)."""
+        L = N.lib()
+        res = []
+        for h in self._chains:
+            nl, g = ctypes.c_int32(), ctypes.c_int32()
+            N.check(L.pgm_batch_info(h, ctypes.byref(nl), ctypes.byref(g), None), "batch_info")
+            res.append((nl.value, g.value))
+        return res
 
     def _merge_pm(self, recs):
         """A level's specialised product+marginal steps as one launch per 64 (pgm_pm_merge); returns

@@ -627,13 +627,73 @@ def test_batch_product_n_jobs(gpu):
     e_ = rng.random((3, 7))
     o4 = prog.product_n([(E.to_device(e_), ["x", "q"]), (c, ["x"])], ["x", "q"])
     assert prog.n_levels == 2
-    assert len(prog) == 2 and prog.notes[0].startswith("level batch of 3")
+    from pgmpy_amd.program import LEVEL_CHAIN
+
+    if LEVEL_CHAIN:  # both levels are batch jobs only: one levelled launch
+        assert len(prog) == 1 and prog.notes[0].startswith("levels 0-1 as one levelled batch of 4")
+    else:
+        assert len(prog) == 2 and prog.notes[0].startswith("level batch of 3")
     prog.run()
     np.testing.assert_array_equal(E.to_host(o4), e_ * E.to_host(c)[:, None])
     np.testing.assert_array_equal(E.to_host(o1), ref1)
     np.testing.assert_array_equal(E.to_host(x), ref2)
     np.testing.assert_array_equal(E.to_host(o3), np.transpose(ref1, (1, 0, 2)) * E.to_host(c)[:, None, None])
     assert not np.array_equal(x_before, ref2)
+
+
+def test_levelled_batch_chain_matches_numpy(gpu):
+    """Twelve dependent levels of batch jobs (two independent chains of contractions, each level
+    reading the previous level's outputs) run as ONE persistent launch with a grid barrier between
+    levels (pgm_batch_add_level / k_batch_levels): every level's output equals numpy's, on repeated
+    runs (the barrier's generation carries over) and through a captured HIP graph; no barrier timed out."""
+    import torch
+
+    from pgmpy_amd.program import LEVEL_CHAIN, Program
+
+    if not LEVEL_CHAIN:
+        pytest.skip("PGM_BATCH_LEVELS=0")
+    E = _e()
+    rng = np.random.default_rng(5)
+    n_lv = 12
+    xs = [rng.random((64, 300)) for _ in range(2)]
+    Ws = [[rng.random((64, 64)) / 32 for _ in range(n_lv)] for _ in range(2)]
+    prog = Program(levels=True)
+    outs = [[], []]
+    for c in range(2):
+        cur = E.to_device(xs[c])
+        for lv in range(n_lv):
+            cur = prog.contract(E.to_device(Ws[c][lv]), ["b", "a"], cur, ["a", "r"], ["b", "r"], reduce="sum")
+            outs[c].append(cur)
+    assert prog.n_levels == n_lv
+    assert len(prog) == 1, prog.notes
+    (levels, grid), = prog.chain_info()
+    assert levels == n_lv and grid > 0
+    want = [[None] * n_lv for _ in range(2)]
+    for c in range(2):
+        h = xs[c]
+        for lv in range(n_lv):
+            h = Ws[c][lv] @ h
+            want[c][lv] = h
+
+    def check():
+        torch.cuda.synchronize()
+        assert not prog.barrier_timed_out()
+        for c in range(2):
+            for lv in range(n_lv):
+                np.testing.assert_allclose(E.to_host(outs[c][lv]), want[c][lv], rtol=1e-12)
+
+    prog.run()
+    check()
+    for o in outs[0] + outs[1]:
+        o.zero_()
+    prog.run()
+    prog.run()
+    check()
+    prog.capture()
+    for o in outs[0] + outs[1]:
+        o.zero_()
+    prog.run()
+    check()
 
 
 @pytest.mark.parametrize("operation", ["marginalize", "maximize"])
