@@ -48,7 +48,9 @@ int pgm_set_device(int device);
 int pgm_alloc(void **ptr, size_t bytes);
 int pgm_free(void *ptr);
 int pgm_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
-int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);  /* synchronises the stream */
+/* stream-ordered D2H without the synchronize (graph-capturable; dst pinned host memory) */
+int pgm_memcpy_d2h_async(void *dst, const void *src, size_t bytes, void *stream);
 int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
 int pgm_memset(void *dst, int value, size_t bytes, void *stream);
 int pgm_stream_sync(void *stream);

@@ -139,6 +139,7 @@ _SIGS = {
     "pgm_free": ([_P], ctypes.c_int),
     "pgm_memcpy_h2d": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_memcpy_d2h": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_memcpy_d2h_async": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_memcpy_d2d": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_memset": ([_P, ctypes.c_int, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_stream_sync": ([_P], ctypes.c_int),

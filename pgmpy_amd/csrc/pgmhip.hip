@@ -2879,6 +2879,13 @@ int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
   return PGM_OK;
 }
 
+int pgm_memcpy_d2h_async(void *dst, const void *src, size_t bytes, void *stream) {
+  STALE_PROBE();
+  if (bytes == 0) return PGM_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)));
+  return PGM_OK;
+}
+
 int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
   STALE_PROBE();
   if (bytes == 0) return PGM_OK;

@@ -424,12 +424,16 @@ class PatternPlan:
         mx, tot = self.intermediates_per_row()
         return max(1, min(n_rows, (1 << 26) // mx, (1 << 28) // tot))
 
-    def _steps_program(self, n, outs):
+    def _steps_program(self, n, outs, host_io=False):
         """The steps path for n rows compiled once: evidence gathers from the plan's own codes
         buffer, the greedy contraction (dense steps on FP64 MFMA), normalisation and the requested
-        outputs into preallocated buffers, captured as one HIP graph."""
+        outputs into preallocated buffers, captured as one HIP graph.  host_io: the graph also holds
+        the copy of the evidence codes from a pinned host buffer (plan.ev_used order) and the copies
+        of the outputs into pinned host buffers, so a single query is one graph launch + one
+        synchronize (QueryRunner).  Returns (program, codes buffer, error flag, outputs, device column
+        map, host buffers or None)."""
         progs = self.__dict__.setdefault("_progs", {})
-        hit = progs.get((n, outs))
+        hit = progs.get((n, outs, host_io))
         if hit is not None:
             return hit
         import torch
@@ -437,12 +441,20 @@ class PatternPlan:
         from ..program import Program
 
         dev = E.device()
+        L = N.lib()
         prog = Program()
         ev_set = set(self.evidence_vars)
         cols = list(self.ev_used)
         local = {v: i for i, v in enumerate(cols)}
         codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
         perr = torch.zeros(1, dtype=torch.int32, device=dev)
+        host = None
+        if host_io:
+            host = {"codes": torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, pin_memory=True)}
+            hptr, nb = ctypes.c_void_p(host["codes"].data_ptr()), host["codes"].numel()
+            prog.raw_step(lambda s: N.check(L.pgm_memcpy_h2d(N.ptr(codes_buf), hptr, nb, s), "memcpy_h2d"),
+                          "evidence codes from pinned host memory")
+            prog.raw_step(lambda s: N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset"), "error flag reset")
         ops = []
         prog.begin_batch()  # every factor's evidence slice: one launch
         for t, vars_ in self._dev_factors():
@@ -475,11 +487,41 @@ class PatternPlan:
             bufs["joint"] = E.empty([self.P, n])
             prog.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw",
                           out=bufs["joint"])
+        if host_io:
+            for k, b in bufs.items():
+                h = torch.empty(tuple(b.shape), dtype=b.dtype, pin_memory=True)
+                host[k] = h
+                prog.raw_step(lambda s, h=h, b=b: N.check(L.pgm_memcpy_d2h_async(
+                    ctypes.c_void_p(h.data_ptr()), N.ptr(b), b.numel() * b.element_size(), s), "memcpy_d2h_async"),
+                    f"{k} to pinned host memory")
+            host["err"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            prog.raw_step(lambda s, h=host["err"]: N.check(L.pgm_memcpy_d2h_async(
+                ctypes.c_void_p(h.data_ptr()), N.ptr(perr), 4, s), "memcpy_d2h_async"), "error flag to host")
         prog.capture()
         cols_dev = torch.tensor([self.col_of[v] for v in cols], dtype=torch.int32, device=dev) if cols else None
-        hit = (prog, codes_buf, perr, bufs, cols_dev)
-        progs[(n, outs)] = hit
+        hit = (prog, codes_buf, perr, bufs, cols_dev, host)
+        progs[(n, outs, host_io)] = hit
         return hit
+
+    def query_one(self, codes, key):
+        """One evidence row (codes: state numbers of plan.evidence_vars, in order) through the steps
+        program with host I/O in the graph: fill the pinned codes, one graph launch, one synchronize.
+        Returns a new fp64 ndarray (`key` "marg" or "joint")."""
+        L = N.lib()
+        with self._lock:
+            prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
+            sel = self.__dict__.get("_ev_sel")
+            if sel is None:
+                pos = {v: i for i, v in enumerate(self.evidence_vars)}
+                sel = self._ev_sel = [pos[v] for v in self.ev_used]
+            hc = host["codes"].numpy()
+            if sel:
+                hc[:, 0] = [codes[i] for i in sel]
+            prog.run()
+            N.check(L.pgm_stream_sync(N.stream_handle()), "stream_sync")
+            if int(host["err"].numpy()[0]) != 0:
+                raise IndexError("evidence state code out of range")
+            return host[key].numpy().reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
         """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
@@ -494,7 +536,7 @@ class PatternPlan:
         chunk = self._steps_chunk(n_rows)
         for c0 in range(0, n_rows, chunk):
             n = min(chunk, n_rows - c0)
-            prog, cbuf, perr, bufs, cols_dev = self._steps_program(n, outs)
+            prog, cbuf, perr, bufs, cols_dev, _ = self._steps_program(n, outs)
             if cols_dev is not None:
                 N.check(L.pgm_codes_select(N.ptr(codes), int(ld), int(row0 + c0), N.ptr(cols_dev), len(self.ev_used),
                                            int(n), N.ptr(cbuf), s), "codes_select")
@@ -558,6 +600,8 @@ class QueryRunner:
         the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
         L = N.lib()
         with self.lock:
+            if self.plan.kind != "fused":  # host copies inside the captured graph: one launch + one sync
+                return self.plan.query_one(codes, self.key)
             s = N.stream_handle()
             hc = self.h_codes.numpy()
             hc[:len(codes), 0] = codes

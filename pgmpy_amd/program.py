@@ -86,29 +86,78 @@ class Program:
         self._batch = _Batch()
 
     def end_batch(self):
+        """Close the batch.  It becomes a step when the program is lowered (first run / capture):
+        consecutive batches (the levels of a contraction path, each reading the ones before) run as
+        ONE levelled batch launch; a lone batch is one launch, a batch of one the job's own launch."""
         b, self._batch = self._batch, None
         if b is None or not b.jobs:
             return
+        self._steps.append(b)
+        self.notes.append(f"batch of {len(b.jobs)}")
+
+    def raw_step(self, fn, note):
+        """Append a launch `fn(stream)` as is (plain Program; e.g. a stream-ordered host copy that the
+        captured graph then holds as a memcpy node)."""
+        if self._levels:
+            raise RuntimeError("raw_step: plain Program only")
+        self._steps.append(fn)
+        self.notes.append(note)
+
+    @staticmethod
+    def _add_batch_jobs(h, jobs):
         L = N.lib()
-        if len(b.jobs) == 1:  # a batch of one is just the job (with its own planner's launch)
-            kind, _, args = b.jobs[0]
-            if kind == "contract":
-                self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
-            else:
-                self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
-            self.notes.append(f"{kind} (batch of one)")
-            return
-        h = ctypes.c_void_p()
-        N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
-        self._handles.append(h)
-        for kind, args, _ in b.jobs:
+        for kind, args, _ in jobs:
             if kind == "contract":
                 N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
             else:
                 N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
+
+    def _batch_step(self, b):
+        L = N.lib()
+        if len(b.jobs) == 1:  # a batch of one is just the job (with its own planner's launch)
+            kind, _, args = b.jobs[0]
+            if kind == "contract":
+                return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), f"{kind} (batch of one)"
+            return (lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather")), f"{kind} (batch of one)"
+        h = self._new_batch()
+        self._add_batch_jobs(h, b.jobs)
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
-        self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
-        self.notes.append(f"batch of {len(b.jobs)}")
+        return (lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")), f"batch of {len(b.jobs)}"
+
+    def _lower_batches(self):
+        """Plain Program: closed batches -> launches (see end_batch)."""
+        if not any(isinstance(s, _Batch) for s in self._steps):
+            return
+        L = N.lib()
+        steps, notes = [], []
+        i, n = 0, len(self._steps)
+        while i < n:
+            if not isinstance(self._steps[i], _Batch):
+                steps.append(self._steps[i])
+                notes.append(self.notes[i])
+                i += 1
+                continue
+            j = i
+            while j < n and isinstance(self._steps[j], _Batch):
+                j += 1
+            group = self._steps[i:j]
+            if LEVEL_CHAIN and len(group) >= 2:
+                h = self._new_batch()
+                for k, b in enumerate(group):
+                    if k:
+                        N.check(L.pgm_batch_add_level(h), "batch_add_level")
+                    self._add_batch_jobs(h, b.jobs)
+                N.check(L.pgm_batch_finalize(h), "batch_finalize")
+                self._chains.append(h)
+                steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+                notes.append(f"{len(group)} levels as one levelled batch of {sum(len(b.jobs) for b in group)} jobs")
+            else:
+                for b in group:
+                    fn, note = self._batch_step(b)
+                    steps.append(fn)
+                    notes.append(note)
+            i = j
+        self._steps, self.notes = steps, notes
 
     # ------------------------------------------------------------------ levelled recording
     def _emit(self, fn, note, reads, writes, job=None, pm=None):
@@ -141,7 +190,10 @@ class Program:
 
     def _lower(self):
         """Levelled Program -> steps: per level, its unbatched launches then one batch launch."""
-        if not self._levels or self._lowered:
+        if not self._levels:
+            self._lower_batches()
+            return
+        if self._lowered:
             return
         self._lowered = True
         self._pm_launch = []

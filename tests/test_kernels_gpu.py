@@ -655,8 +655,8 @@ def test_levelled_batch_chain_matches_numpy(gpu):
     E = _e()
     rng = np.random.default_rng(5)
     n_lv = 12
-    xs = [rng.random((64, 300)) for _ in range(2)]
-    Ws = [[rng.random((64, 64)) / 32 for _ in range(n_lv)] for _ in range(2)]
+    xs = [rng.random((16, 256)) for _ in range(2)]  # 64 K-entry index space per step: a batch job
+    Ws = [[rng.random((16, 16)) / 8 for _ in range(n_lv)] for _ in range(2)]
     prog = Program(levels=True)
     outs = [[], []]
     for c in range(2):
