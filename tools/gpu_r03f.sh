@@ -4,14 +4,18 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r03f}
+set --
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 timeout -k 10 300 $T tests/test_kernels_gpu.py -k "levelled or batch" > gpurun_out/${TAG}_pytest_lv.log 2>&1 || { echo levelled tests failed; tail -60 gpurun_out/${TAG}_pytest_lv.log; exit 1; }
 tail -2 gpurun_out/${TAG}_pytest_lv.log
+for CFG in "1 0" "1 32" "1 128" "0 0"; do
+set -- $CFG; LV=$1; GR=$2; N=lv${LV}g${GR}
+PGM_BATCH_LEVELS=$LV PGM_BATCH_LEVELS_GRID=$GR timeout -k 10 300 python bench.py --workload c2 --steps 20 --warmup 2 > gpurun_out/${TAG}_bench_c2_$N.json 2> gpurun_out/${TAG}_bench_c2_$N.err || { tail -30 gpurun_out/${TAG}_bench_c2_$N.err; exit 1; }
+done
 for LV in 1 0; do
-PGM_BATCH_LEVELS=$LV timeout -k 10 300 python bench.py --workload c2 --steps 20 --warmup 2 > gpurun_out/${TAG}_bench_c2_lv$LV.json 2> gpurun_out/${TAG}_bench_c2_lv$LV.err || { tail -30 gpurun_out/${TAG}_bench_c2_lv$LV.err; exit 1; }
 PGM_BATCH_LEVELS=$LV timeout -k 10 300 python bench.py --workload c1 --steps 50 --warmup 5 > gpurun_out/${TAG}_bench_c1_lv$LV.json 2> gpurun_out/${TAG}_bench_c1_lv$LV.err || { tail -30 gpurun_out/${TAG}_bench_c1_lv$LV.err; exit 1; }
 done
-head -c 400 gpurun_out/${TAG}_bench_c2_lv*.json gpurun_out/${TAG}_bench_c1_lv*.json; echo
+head -c 300 gpurun_out/${TAG}_bench_c2_*.json gpurun_out/${TAG}_bench_c1_lv*.json; echo
 LEVELS=1 TOP=10 timeout -k 10 300 python tools/program_steps.py c2 > gpurun_out/${TAG}_c2_levels.txt 2>&1 || { tail -30 gpurun_out/${TAG}_c2_levels.txt; exit 1; }
 PGM_BATCH_LEVELS=0 LEVELS=1 TOP=10 timeout -k 10 300 python tools/program_steps.py c2 > gpurun_out/${TAG}_c2_levels_lv0.txt 2>&1 || { tail -30 gpurun_out/${TAG}_c2_levels_lv0.txt; exit 1; }
 head -3 gpurun_out/${TAG}_c2_levels.txt gpurun_out/${TAG}_c2_levels_lv0.txt
