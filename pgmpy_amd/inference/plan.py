@@ -504,16 +504,15 @@ class PatternPlan:
         return hit
 
     def query_one(self, codes, key):
-        """One evidence row (codes: state numbers of plan.evidence_vars, in order) through the steps
+        """One evidence row (codes[col_of[v]]: the state number of evidence variable v) through the steps
         program with host I/O in the graph: fill the pinned codes, one graph launch, one synchronize.
         Returns a new fp64 ndarray (`key` "marg" or "joint")."""
         L = N.lib()
         with self._lock:
             prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
             sel = self.__dict__.get("_ev_sel")
-            if sel is None:
-                pos = {v: i for i, v in enumerate(self.evidence_vars)}
-                sel = self._ev_sel = [pos[v] for v in self.ev_used]
+            if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
+                sel = self._ev_sel = [self.col_of[v] for v in self.ev_used]
             hc = host["codes"].numpy()
             if sel:
                 hc[:, 0] = [codes[i] for i in sel]
