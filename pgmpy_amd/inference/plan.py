@@ -427,10 +427,8 @@ class PatternPlan:
     def _steps_program(self, n, outs, host_io=False):
         """The steps path for n rows compiled once: evidence gathers from the plan's own codes
         buffer, the greedy contraction (dense steps on FP64 MFMA), normalisation and the requested
-        outputs into preallocated buffers, captured as one HIP graph.  host_io: the graph also holds
-        the copy of the evidence codes from a pinned host buffer (plan.ev_used order) and the copies
-        of the outputs into pinned host buffers, so a single query is one graph launch + one
-        synchronize (QueryRunner).  Returns (program, codes buffer, error flag, outputs, device column
+        outputs into preallocated buffers, captured as one HIP graph.  host_io: the graph also resets
+        the error flag, and pinned host buffers are made for QueryRunner's copies (query_one).  Returns (program, codes buffer, error flag, outputs, device column
         map, host buffers or None)."""
         progs = self.__dict__.setdefault("_progs", {})
         hit = progs.get((n, outs, host_io))
@@ -449,11 +447,9 @@ class PatternPlan:
         codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
         perr = torch.zeros(1, dtype=torch.int32, device=dev)
         host = None
-        if host_io:
-            host = {"codes": torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, pin_memory=True)}
-            hptr, nb = ctypes.c_void_p(host["codes"].data_ptr()), host["codes"].numel()
-            prog.raw_step(lambda s: N.check(L.pgm_memcpy_h2d(N.ptr(codes_buf), hptr, nb, s), "memcpy_h2d"),
-                          "evidence codes from pinned host memory")
+        if host_io:  # pinned staging buffers for QueryRunner's copies (stream-ordered, outside the graph)
+            host = {"codes": torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, pin_memory=True),
+                    "err": torch.zeros(1, dtype=torch.int32, pin_memory=True)}
             prog.raw_step(lambda s: N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset"), "error flag reset")
         ops = []
         prog.begin_batch()  # every factor's evidence slice: one launch
@@ -489,14 +485,7 @@ class PatternPlan:
                           out=bufs["joint"])
         if host_io:
             for k, b in bufs.items():
-                h = torch.empty(tuple(b.shape), dtype=b.dtype, pin_memory=True)
-                host[k] = h
-                prog.raw_step(lambda s, h=h, b=b: N.check(L.pgm_memcpy_d2h_async(
-                    ctypes.c_void_p(h.data_ptr()), N.ptr(b), b.numel() * b.element_size(), s), "memcpy_d2h_async"),
-                    f"{k} to pinned host memory")
-            host["err"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            prog.raw_step(lambda s, h=host["err"]: N.check(L.pgm_memcpy_d2h_async(
-                ctypes.c_void_p(h.data_ptr()), N.ptr(perr), 4, s), "memcpy_d2h_async"), "error flag to host")
+                host[k] = torch.empty(tuple(b.shape), dtype=b.dtype, pin_memory=True)
         prog.capture()
         cols_dev = torch.tensor([self.col_of[v] for v in cols], dtype=torch.int32, device=dev) if cols else None
         hit = (prog, codes_buf, perr, bufs, cols_dev, host)
@@ -505,22 +494,28 @@ class PatternPlan:
 
     def query_one(self, codes, key):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v) through the steps
-        program with host I/O in the graph: fill the pinned codes, one graph launch, one synchronize.
+        program: the plan's evidence columns copied from a pinned buffer, one graph launch (error-flag
+        reset inside), the result and the flag copied back asynchronously, ONE synchronize.
         Returns a new fp64 ndarray (`key` "marg" or "joint")."""
         L = N.lib()
         with self._lock:
-            prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
+            prog, cbuf, perr, bufs, _, host = self._steps_program(1, frozenset([key]), host_io=True)
             sel = self.__dict__.get("_ev_sel")
             if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
                 sel = self._ev_sel = [self.col_of[v] for v in self.ev_used]
-            hc = host["codes"].numpy()
+            s = N.stream_handle()
+            hc = host["codes"]
             if sel:
-                hc[:, 0] = [codes[i] for i in sel]
+                hc.numpy()[:, 0] = [codes[i] for i in sel]
+                N.check(L.pgm_memcpy_h2d(N.ptr(cbuf), ctypes.c_void_p(hc.data_ptr()), hc.numel(), s), "memcpy_h2d")
             prog.run()
-            N.check(L.pgm_stream_sync(N.stream_handle()), "stream_sync")
-            if int(host["err"].numpy()[0]) != 0:
+            ho, he, b = host[key], host["err"], bufs[key]
+            N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(ho.data_ptr()), N.ptr(b), b.numel() * 8, s), "memcpy_d2h")
+            N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(he.data_ptr()), N.ptr(perr), 4, s), "memcpy_d2h")
+            N.check(L.pgm_stream_sync(s), "stream_sync")
+            if int(he.numpy()[0]) != 0:
                 raise IndexError("evidence state code out of range")
-            return host[key].numpy().reshape(-1).copy()
+            return ho.numpy().reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
         """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
