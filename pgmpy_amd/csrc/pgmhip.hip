@@ -1746,25 +1746,90 @@ __global__ __launch_bounds__(256) void k_codes_remap(const int8_t *__restrict__ 
   if (bad && err) atomicOr(err, 1);
 }
 
+// numpy's float64 add.reduce of a strided run (the pairwise summation of numpy's umath loops): runs
+// of < 8 summed in order; runs of <= 128 in 8 interleaved accumulators combined as
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail in order; longer runs split in two at a
+// multiple of 8 below the half, each half summed the same way.  Post-order over an explicit stack.
+// numpy hands the loop at most one 8,192-element buffer at a time and adds the buffers' sums in
+// order (np_sum); checked bit for bit against numpy 2.2 up to 40,000 elements (tests).
+__device__ double np_block_sum(const double *a, int64_t n, int64_t s) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int64_t i = 0; i < n; ++i) res += a[i * s];
+    return res;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j * s];
+  int64_t i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * s];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i * s];
+  return res;
+}
+
+__device__ double np_pairwise_sum(const double *a, int64_t n, int64_t s) {
+  if (n <= 128) return np_block_sum(a, n, s);
+  int64_t off[40], len[40];
+  double left[40];
+  int stage[40];
+  int top = 0;
+  off[0] = 0, len[0] = n, stage[0] = 0;
+  double val = 0.0;
+  bool have = false;
+  for (;;) {
+    if (!have) {
+      if (len[top] <= 128) {
+        val = np_block_sum(a + off[top] * s, len[top], s);
+        have = true;
+        --top;
+      } else {  // descend into the left half
+        int64_t n2 = len[top] / 2;
+        n2 -= n2 % 8;
+        stage[top] = 1;
+        off[top + 1] = off[top], len[top + 1] = n2, stage[top + 1] = 0;
+        ++top;
+      }
+    } else {
+      if (top < 0) return val;
+      if (stage[top] == 1) {  // left done: the right half next
+        int64_t n2 = len[top] / 2;
+        n2 -= n2 % 8;
+        left[top] = val;
+        stage[top] = 2;
+        off[top + 1] = off[top] + n2, len[top + 1] = len[top] - n2, stage[top + 1] = 0;
+        ++top;
+        have = false;
+      } else {
+        val = left[top] + val;
+        --top;
+      }
+    }
+  }
+}
+
 // predict(stochastic=True) (DiscreteBayesianNetwork.py:889-892 -> DiscreteFactor.sample L868-912):
-// numpy's Generator.choice(P, p=joint) for each output row r: cdf = cumsum(p); cdf /= cdf[-1];
-// index = searchsorted(cdf, u[r], side="right") — the same sequential sums, the uniforms u drawn on
-// the host from the reference's seeded stream.  joint column group[r] (a deduplicated evidence row).
+// sample() normalises the joint (values / values.sum(), DiscreteFactor.py:530: numpy's pairwise sum)
+// and numpy's Generator.choice(P, p=p) then takes cdf = cumsum(p) (in order), cdf /= cdf[-1] and
+// index = searchsorted(cdf, u, side="right") = the number of cdf entries <= u.  The same operations
+// in the same order per output row r, so a uniform on a CDF boundary lands where numpy puts it; the
+// uniforms u come from the reference's seeded stream on the host.  joint column group[r].
 __global__ __launch_bounds__(256) void k_sample_joint(const double *__restrict__ joint, int64_t ld, int64_t P,
                                                       const int32_t *__restrict__ group,
                                                       const double *__restrict__ u, int64_t n,
                                                       int32_t *__restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= n) return;
-  const double *p = joint + group[r];
-  double total = 0.0;
-  for (int64_t i = 0; i < P; ++i) total += p[i * ld];
+  const double *q = joint + group[r];
+  const double total = np_pairwise_sum(q, P, ld);
+  double last = 0.0;
+  for (int64_t i = 0; i < P; ++i) last = i ? last + q[i * ld] / total : q[0] / total;
   const double x = u[r];
   double acc = 0.0;
   int64_t idx = 0;
   for (int64_t i = 0; i < P; ++i) {
-    acc += p[i * ld];
-    if (acc / total <= x) idx = i + 1;
+    acc = i ? acc + q[i * ld] / total : q[0] / total;
+    if (acc / last <= x) idx = i + 1;
   }
   out[r] = (int32_t)(idx < P ? idx : P - 1);
 }
