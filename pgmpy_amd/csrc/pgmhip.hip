@@ -1821,7 +1821,8 @@ __global__ __launch_bounds__(256) void k_sample_joint(const double *__restrict__
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= n) return;
   const double *q = joint + group[r];
-  const double total = np_pairwise_sum(q, P, ld);
+  double total = 0.0;
+  for (int64_t c = 0; c < P; c += 8192) total += np_pairwise_sum(q + c * ld, P - c < 8192 ? P - c : 8192, ld);
   double last = 0.0;
   for (int64_t i = 0; i < P; ++i) last = i ? last + q[i * ld] / total : q[0] / total;
   const double x = u[r];
