@@ -29,29 +29,23 @@ def main():
         pick = rng.sample(nodes_sorted, 8)
         pats.append((pick[:3], {v: m.states[v][codes[pos[v], r]] for v in pick[3:]}))
     ve = VariableElimination(m)
-    for i in (4, 9, 4, 9):
+    ve.query(*pats[4], show_progress=False)
+    for i in range(50):
+        if i == 4:
+            continue
         q, e = pats[i]
+        ve.query(q, e, show_progress=False)
+        key = [k for k in ve._compiled if list(k[0]) == q][0]
+        pl = ve._compiled[key].plan
         try:
-            ve.query(q, e, show_progress=False)
+            ve.query(*pats[4], show_progress=False)
             ok = "ok"
         except IndexError as ex:
             ok = str(ex)
-        key = [k for k in ve._compiled if list(k[0]) == q][0]
-        pl = ve._compiled[key].plan
-        prog, cbuf, perr, bufs, cols_dev, host = list(pl._progs.values())[0]
-        torch.cuda.synchronize()
-        print(i, ok, "plan", id(pl), "ev_used", pl.ev_used, "codes", [pl.card[v] for v in pl.ev_used],
-              "host", host["codes"].numpy().ravel().tolist(), "dev", cbuf.cpu().numpy().ravel().tolist(),
-              "perr", int(perr.item()), "cbuf ptr", hex(cbuf.data_ptr()), "perr ptr", hex(perr.data_ptr()), flush=True)
-    q, e = pats[4]
-    key = [k for k in ve._compiled if list(k[0]) == q][0]
-    pl = ve._compiled[key].plan
-    prog, cbuf, perr, bufs, cols_dev, host = list(pl._progs.values())[0]
-    s = N.stream_handle()
-    for j, (step, note) in enumerate(zip(prog._steps, prog.notes)):
-        step(s)
-        torch.cuda.synchronize()
-        print("step", j, note[:90], "perr", int(perr.item()), flush=True)
+        print(i, pl.kind, pl.variables, pl.ev_used, "n_comp", pl.n_comp, "-> pattern 4:", ok, flush=True)
+        if ok != "ok":
+            print("culprit", i, pl.describe(), flush=True)
+            break
 
 
 if __name__ == "__main__":
