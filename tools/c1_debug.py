@@ -29,23 +29,29 @@ def main():
         pick = rng.sample(nodes_sorted, 8)
         pats.append((pick[:3], {v: m.states[v][codes[pos[v], r]] for v in pick[3:]}))
     ve = VariableElimination(m)
-    ve.query(*pats[4], show_progress=False)
-    for i in range(50):
-        if i == 4:
-            continue
-        q, e = pats[i]
-        ve.query(q, e, show_progress=False)
-        key = [k for k in ve._compiled if list(k[0]) == q][0]
-        pl = ve._compiled[key].plan
-        try:
-            ve.query(*pats[4], show_progress=False)
-            ok = "ok"
-        except IndexError as ex:
-            ok = str(ex)
-        print(i, pl.kind, pl.variables, pl.ev_used, "n_comp", pl.n_comp, "-> pattern 4:", ok, flush=True)
-        if ok != "ok":
-            print("culprit", i, pl.describe(), flush=True)
-            break
+    s = N.stream_handle()
+    for rep in range(2):
+        for i, (q, e) in enumerate(pats):
+            try:
+                ve.query(q, e, show_progress=False)
+                continue
+            except IndexError as ex:
+                ok = str(ex)
+            key = [k for k in ve._compiled if list(k[0]) == q][0]
+            pl = ve._compiled[key].plan
+            prog, cbuf, perr, bufs, cols_dev, host = list(pl._progs.values())[0]
+            torch.cuda.synchronize()
+            print("rep", rep, "pattern", i, ok, pl.ev_used, [pl.card[v] for v in pl.ev_used], "dev codes",
+                  cbuf.cpu().numpy().ravel().tolist(), "perr", int(perr.item()), flush=True)
+            for j, (step, note) in enumerate(zip(prog._steps, prog.notes)):
+                step(s)
+                torch.cuda.synchronize()
+                print("  step", j, note[:100], "perr", int(perr.item()), flush=True)
+            print("graph replay:", flush=True)
+            prog.run()
+            torch.cuda.synchronize()
+            print("  perr after graph", int(perr.item()), flush=True)
+            return
 
 
 if __name__ == "__main__":
