@@ -427,8 +427,8 @@ class PatternPlan:
     def _steps_program(self, n, outs, host_io=False):
         """The steps path for n rows compiled once: evidence gathers from the plan's own codes
         buffer, the greedy contraction (dense steps on FP64 MFMA), normalisation and the requested
-        outputs into preallocated buffers, captured as one HIP graph.  host_io: the graph also resets
-        the error flag, and pinned host buffers are made for QueryRunner's copies (query_one).  Returns (program, codes buffer, error flag, outputs, device column
+        outputs into preallocated buffers, captured as one HIP graph.  host_io: pinned host buffers for
+        QueryRunner's copies (query_one).  Returns (program, codes buffer, error flag, outputs, device column
         map, host buffers or None)."""
         progs = self.__dict__.setdefault("_progs", {})
         hit = progs.get((n, outs, host_io))
@@ -450,7 +450,6 @@ class PatternPlan:
         if host_io:  # pinned staging buffers for QueryRunner's copies (stream-ordered, outside the graph)
             host = {"codes": torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, pin_memory=True),
                     "err": torch.zeros(1, dtype=torch.int32, pin_memory=True)}
-            prog.raw_step(lambda s: N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset"), "error flag reset")
         ops = []
         prog.begin_batch()  # every factor's evidence slice: one launch
         for t, vars_ in self._dev_factors():
@@ -494,8 +493,8 @@ class PatternPlan:
 
     def query_one(self, codes, key):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v) through the steps
-        program: the plan's evidence columns copied from a pinned buffer, one graph launch (error-flag
-        reset inside), the result and the flag copied back asynchronously, ONE synchronize.
+        program: the plan's evidence columns copied from a pinned buffer, the error flag reset, one graph
+        launch, the result and the flag copied back asynchronously, ONE synchronize.
         Returns a new fp64 ndarray (`key` "marg" or "joint")."""
         L = N.lib()
         with self._lock:
@@ -508,6 +507,9 @@ class PatternPlan:
             if sel:
                 hc.numpy()[:, 0] = [codes[i] for i in sel]
                 N.check(L.pgm_memcpy_h2d(N.ptr(cbuf), ctypes.c_void_p(hc.data_ptr()), hc.numel(), s), "memcpy_h2d")
+            # the flag is reset outside the graph: a captured 4-byte memset node replayed later wrote
+            # 0x02020202 after other graphs had run (r03g, tools/c1_debug.py) — never captured here
+            N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset")
             prog.run()
             ho, he, b = host[key], host["err"], bufs[key]
             N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(ho.data_ptr()), N.ptr(b), b.numel() * 8, s), "memcpy_d2h")

@@ -4,7 +4,6 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r03g}
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-timeout -k 10 120 python -u tools/c1_debug.py > gpurun_out/${TAG}_c1_debug.txt 2>&1; echo "debug rc=$?"; tail -40 gpurun_out/${TAG}_c1_debug.txt; exit 0
 timeout -k 10 300 python -u tools/c1_check.py --chain > gpurun_out/${TAG}_c1_check.txt 2>&1 || { tail -8 gpurun_out/${TAG}_c1_check.txt; exit 1; }; tail -3 gpurun_out/${TAG}_c1_check.txt
 timeout -k 10 300 python bench.py --workload c1 --steps 50 --warmup 5 > gpurun_out/${TAG}_bench_c1.json 2> gpurun_out/${TAG}_bench_c1.err || { tail -30 gpurun_out/${TAG}_bench_c1.err; exit 1; }
 timeout -k 10 300 python bench.py --workload c2 --steps 20 --warmup 2 > gpurun_out/${TAG}_bench_c2.json 2> gpurun_out/${TAG}_bench_c2.err || { tail -30 gpurun_out/${TAG}_bench_c2.err; exit 1; }
