@@ -227,6 +227,14 @@ class Launcher:
                 q.sync()
         torch.cuda.synchronize()
 
+    def release_and_wait(self):
+        """End of a timed region with the outputs released at system scope: direct queues append their
+        release barriers together, then wait; HIP: wait() (end event + device synchronize)."""
+        if self.kind == "direct":
+            for q in self.qs:
+                q.release()
+        self.wait()
+
     def wait(self):
         """End of a timed region: every launch issued so far has completed (direct queues: their
         completion signals; HIP: the device)."""
@@ -394,6 +402,32 @@ def cpu_baselines_c3(args):
     return single, allcore
 
 
+def api_e2e_rate(model, codes_all, nodes, missing, reps=3):
+    """The shipped API on the same rows: DiscreteBayesianNetwork.predict_probability over a pandas
+    Categorical DataFrame of the observed columns (host frame in, DataFrame out: ingestion, pattern
+    grouping, the fused kernel, the result frame), best of `reps`, outside the timed region (ADVICE r02:
+    the line's `value` is the device-resident launch rate; this is what a DataFrame caller gets)."""
+    import pandas as pd
+    import torch
+
+    st = model.states
+    pos = {v: i for i, v in enumerate(nodes)}
+    keep = [v for v in nodes if v not in missing]
+    df = pd.DataFrame({c: pd.Categorical.from_codes(codes_all[pos[c]].astype(np.int8), categories=list(st[c]))
+                       for c in keep})
+    model.predict_probability(df.iloc[:1000])  # compile the pattern's plan
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        model.predict_probability(df)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"value": len(df) / best, "unit": "rows/s", "rows": len(df), "seconds": best,
+            "path": "DiscreteBayesianNetwork.predict_probability(pandas Categorical frame) -> DataFrame"}
+
+
 def parity_spot_check(model, missing, plan, out, codes_host, nodes, n_check=64, r0=0):
     """First rows of the device output (evidence columns r0.. of codes_host) against the oracle
     (1e-6 relative, BASELINE.json)."""
@@ -479,12 +513,9 @@ def bench_c3(args, dist, rank, world):
     t_start = time.perf_counter()
     launcher.steps(args.steps)
     # the window closes on every step's dispatch complete AND its outputs visible system-wide: on the
-    # direct queues one system-scope release barrier packet per queue, waited for (pgm_dq_sync);
-    # HIP: the end event + torch.cuda.synchronize
-    if args.launch == "direct":
-        launcher.sync()
-    else:
-        launcher.wait()
+    # direct queues one system-scope release barrier packet per queue, all appended before any is waited
+    # for (pgm_dq_release, then pgm_dq_wait); HIP: the end event + torch.cuda.synchronize
+    launcher.release_and_wait()
     t_end = time.perf_counter()
     kern_ms_total = launcher.timer_stop_ms()  # dispatch timestamps, read after the timed region
     barrier(dist)
@@ -527,6 +558,10 @@ def bench_c3(args, dist, rank, world):
             "launch": {"direct": "AQL packet on user-mode HSA queues (pgm_dq_launch; batch i on queue i % queues)",
                        "hip": "hipModuleLaunchKernel (pgm_rows_bound_run)"}[args.launch],
             "network": "munin",
+            # what `value` measures: the fused row plan over evidence batches already resident in HBM
+            # (prepared launch: kernel + dispatch); the public DataFrame API's end-to-end rate on the same
+            # rows is `api_e2e` (host ingestion-bound)
+            "value_measures": "device-resident evidence batches through the prepared fused-plan launch",
             "missing": variables,
             "rows_per_gpu_per_step": rows,
             "global_rows_per_step": rows * world,
@@ -588,6 +623,8 @@ def bench_c3(args, dist, rank, world):
         if world == 1 and args.cpu_pre is not None:
             result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
+        if world == 1 and not args.no_api_e2e:
+            result["api_e2e"] = api_e2e_rate(model, codes_all, nodes, missing)
     if dist is not None:
         # the result delivery (outside the timed region in this weak-scaling line; --workload c5
         # times it inside the step): every rank's [17, rows] marginals to rank 0
@@ -623,10 +660,22 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
     torch.cuda.synchronize()
     timer = HipTimer()
     barrier(dist)
-    t_start = time.perf_counter()
-    timer.start()
-    ring.start(args.steps)
-    timer.mark_end()  # the end event completes with the launch
+    launch_ms = None
+    if args.ring_prestart:
+        # the resident kernel is launched before the window, as a serving engine's would be before
+        # requests arrive; the window holds the K batches' posts, their processing, the kernel's exit
+        # and the closing synchronize (HIP's end-of-kernel system-scope release)
+        t_l = time.perf_counter()
+        timer.start()
+        ring.start(args.steps)
+        timer.mark_end()
+        launch_ms = (time.perf_counter() - t_l) * 1e3
+        t_start = time.perf_counter()
+    else:
+        t_start = time.perf_counter()
+        timer.start()
+        ring.start(args.steps)
+        timer.mark_end()  # the end event completes with the launch
     for b in range(1, args.steps + 1):
         ring.post(b)  # one step = one batch published to the resident launch
     ring.finish()
@@ -662,8 +711,15 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
             "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, fused row plan; "
                         "one step = one 100k-row batch posted to the resident ring launch (pgm_rows_ring_*), "
                         "batches resident in HBM, batch i on buffer set i % batches",
-            "launch": "one resident launch per timed region (started inside the window), K batches posted",
+            "launch": ("one resident launch per timed region, launched just before the window (--ring-prestart), "
+                       "K batches posted inside it" if args.ring_prestart else
+                       "one resident launch per timed region (started inside the window), K batches posted"),
+            "ring_host_launch_ms": launch_ms,
             "network": "munin",
+            # what `value` measures: the fused row plan over evidence batches already resident in HBM
+            # (prepared launch: kernel + dispatch); the public DataFrame API's end-to-end rate on the same
+            # rows is `api_e2e` (host ingestion-bound)
+            "value_measures": "device-resident evidence batches through the prepared fused-plan launch",
             "missing": variables,
             "rows_per_gpu_per_step": rows,
             "global_rows_per_step": rows * world,
@@ -704,6 +760,8 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
         if world == 1 and args.cpu_pre is not None:
             result["cpu_baseline"], result["cpu_baseline_allcore"] = args.cpu_pre
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
+        if world == 1 and not args.no_api_e2e:
+            result["api_e2e"] = api_e2e_rate(model, codes_all, nodes, missing)
     del ring
     return result
 
@@ -1060,6 +1118,9 @@ def main():
                     help="c5: gather the fp64 marginals (predict_probability) or the MAP indices (predict)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
+    ap.add_argument("--ring-prestart", action="store_true",
+                    help="c3 --launch ring: launch the resident kernel just before the timed window")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     ap.add_argument("--batches", type=int, default=24,

@@ -460,7 +460,8 @@ int pgm_rows_ring_destroy(void *ring);
  * each pgm_dq_launch writes one kernel-dispatch packet (barrier bit set) and rings the doorbell — no
  * HIP runtime on the launch path.  Same kernel, same arguments, same results as pgm_rows_bound_run.
  * Ordering: pgm_dq_bind_rows waits for the device (inputs complete); dispatches on one queue run in
- * order; inputs may change only between pgm_dq_sync and the next launch (HIP writes complete); call
+ * order; inputs may change only between pgm_dq_sync and the next launch (that launch first drains the
+ * device with hipDeviceSynchronize, so HIP work issued in between is complete); call
  * pgm_dq_sync (a system-scope release barrier + wait) before HIP work reads the outputs.  The timer reports
  * the GPU span (queue profiling timestamps) from the first dispatch after pgm_dq_timer_start to the
  * last one issued.  The queue must outlive its bound launches.  Serves the same caller as
@@ -474,6 +475,9 @@ int pgm_dq_launch(void *dbound);
  * the next launch or sync waits for the whole group.  At most 128 launches, no launch repeated. */
 int pgm_dq_launch_group(void *const *dbounds, int32_t n);
 int pgm_dq_sync(void *dq);
+/* the first half of pgm_dq_sync: append the system-scope release barrier packet without waiting for
+ * it (pgm_dq_wait then waits for it with the dispatches), so several queues release in parallel */
+int pgm_dq_release(void *dq);
 /* wait until every dispatch issued on the queue has completed (no release barrier: call pgm_dq_sync
  * before HIP work reads the outputs) */
 int pgm_dq_wait(void *dq);

@@ -313,12 +313,11 @@ static int wait_tail(DirectQueue *dq) {
   return PGM_OK;
 }
 
-extern "C" int pgm_dq_sync(void *handle) {
-  DirectQueue *dq = (DirectQueue *)handle;
-  if (!dq) return fail(PGM_EINVAL, "dq_sync: null handle");
-  std::lock_guard<std::mutex> lk(dq->mu);
+// append the system-scope release barrier packet if a dispatch since the last one needs it (caller
+// holds dq->mu); the next dispatch acquires at system scope
+static int release_locked(DirectQueue *dq) {
   if (dq->issued == 0) return PGM_OK;
-  if (dq->need_release) {  // one barrier packet makes every dispatch's writes visible system-wide
+  if (dq->need_release) {
     hsa_signal_t sig;
     void *slot;
     uint64_t idx;
@@ -334,7 +333,23 @@ extern "C" int pgm_dq_sync(void *handle) {
     dq->need_release = false;
   }
   dq->fresh = true;
-  return wait_tail(dq);
+  return PGM_OK;
+}
+
+extern "C" int pgm_dq_release(void *handle) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq) return fail(PGM_EINVAL, "dq_release: null handle");
+  std::lock_guard<std::mutex> lk(dq->mu);
+  return release_locked(dq);
+}
+
+extern "C" int pgm_dq_sync(void *handle) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq) return fail(PGM_EINVAL, "dq_sync: null handle");
+  std::lock_guard<std::mutex> lk(dq->mu);
+  if (dq->issued == 0) return PGM_OK;
+  const int rc = release_locked(dq);  // one barrier packet makes every dispatch's writes visible system-wide
+  return rc != PGM_OK ? rc : wait_tail(dq);
 }
 
 int pgm_dq_wait(void *handle) {
@@ -421,6 +436,16 @@ int pgm_dq_bind_rows(void *handle, void *bound, void **out) {
 // one kernel-dispatch packet of a bound launch (caller holds dq->mu)
 static int dispatch(DirectBound *db, bool barrier) {
   DirectQueue *dq = db->dq;
+  if (dq->fresh) {
+    // the first dispatch after bind/sync: HIP work issued since (a copy or kernel writing the inputs)
+    // must be complete before the packet's system-scope acquire; the queue does not order against
+    // HIP streams, so drain the device here (once per sync, never inside a stream of dispatches)
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(PGM_EDEVICE, "dq_launch: synchronising HIP work before the first dispatch: %s", hipGetErrorString(e));
+    }
+  }
   hsa_signal_t sig;
   void *slot;
   uint64_t idx;

@@ -790,6 +790,11 @@ class DirectQueue:
     def sync(self):
         N.check(N.lib().pgm_dq_sync(self._h), "dq_sync")
 
+    def release(self):
+        """Append the system-scope release barrier without waiting (pgm_dq_release; wait() then
+        covers it): several queues release in parallel."""
+        N.check(N.lib().pgm_dq_release(self._h), "dq_release")
+
     def wait(self):
         """Every dispatch issued so far has completed (no release: sync() before HIP reads)."""
         N.check(N.lib().pgm_dq_wait(self._h), "dq_wait")
@@ -845,9 +850,17 @@ class DirectGroup:
         q = members[0].queue
         if any(m.queue is not q for m in members):
             raise ValueError("DirectGroup: launches bound to different queues")
-        outs = [t.data_ptr() for m in members for t in m.out.values()]
-        if len(set(outs)) != len(outs):
-            raise ValueError("DirectGroup: launches share an output buffer")
+        spans = []  # byte range each member's outputs cover (views of one buffer may overlap)
+        for i, m in enumerate(members):
+            for t in m.out.values():
+                if t.numel() == 0:
+                    continue
+                last = sum((int(d) - 1) * int(st) for d, st in zip(t.shape, t.stride()) if int(st) > 0)
+                spans.append((t.data_ptr(), t.data_ptr() + (last + 1) * t.element_size(), i))
+        for k, (a0, a1, i) in enumerate(spans):
+            for b0, b1, j in spans[k + 1:]:
+                if i != j and a0 < b1 and b0 < a1:
+                    raise ValueError("DirectGroup: launches write overlapping output bytes")
         self._keep = members
         self.queue = q
         self._arr = (ctypes.c_void_p * len(members))(*[m._h.value for m in members])
