@@ -215,7 +215,10 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   for (int i = 0; i < k.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)oc; (void)idx;\n";
   const int kx = k.nk - 1;  // kept outer dims 0..kx-1 (kx-1 fastest), the row dim last
-  for (int q = kx - 1; q >= 0; --q) {
+  // PGM_PM_KREV=1: dim 0 fastest instead (consecutive tiles then share the trailing dims; A/B knob)
+  static const int krev = pm_knob("PGM_PM_KREV", 0);
+  for (int qi = 0; qi < kx; ++qi) {
+    const int q = krev ? qi : kx - 1 - qi;
     const unsigned dq = k.kdiv[q].d;
     pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", dq, dq);
     if (k.ksc[q]) pgmi_appendf(o, " oc += (long long)g * %lldLL;", (long long)k.ksc[q]);
@@ -363,7 +366,9 @@ static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
   o += "  unsigned idx = ob;\n  long long m1 = 0, m2 = 0";
   for (int i = 0; i < q.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)idx;\n";
-  for (int d = q.nK - 1; d >= 0; --d) {
+  static const int krev = pm_knob("PGM_PM_KREV", 0);
+  for (int di = 0; di < q.nK; ++di) {
+    const int d = krev ? di : q.nK - 1 - di;
     pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", q.kcard[d], q.kcard[d]);
     if (q.k1[d]) pgmi_appendf(o, " m1 += (long long)g * %lldLL;", (long long)q.k1[d]);
     if (q.k2[d]) pgmi_appendf(o, " m2 += (long long)g * %lldLL;", (long long)q.k2[d]);
