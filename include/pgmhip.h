@@ -53,6 +53,10 @@ int pgm_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);  /* 
 int pgm_memcpy_d2h_async(void *dst, const void *src, size_t bytes, void *stream);
 int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
 int pgm_memset(void *dst, int value, size_t bytes, void *stream);
+/* host memory that kernels read and write directly (pinned, mapped, coherent / fine-grained; zeroed):
+ * a single query's evidence codes and result, so its captured graph needs no copy nodes */
+int pgm_host_alloc(void **ptr, size_t bytes);
+int pgm_host_free(void *ptr);
 int pgm_stream_sync(void *stream);
 /* HIP events, for timing a kernel on the stream it runs on (bench.py) */
 int pgm_event_create(void **ev);

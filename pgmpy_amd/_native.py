@@ -142,6 +142,8 @@ _SIGS = {
     "pgm_memcpy_d2h_async": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_memcpy_d2d": ([_P, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_memset": ([_P, ctypes.c_int, ctypes.c_size_t, _P], ctypes.c_int),
+    "pgm_host_alloc": ([ctypes.POINTER(_P), ctypes.c_size_t], ctypes.c_int),
+    "pgm_host_free": ([_P], ctypes.c_int),
     "pgm_stream_sync": ([_P], ctypes.c_int),
     "pgm_event_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_event_destroy": ([_P], ctypes.c_int),
@@ -300,6 +302,34 @@ def stream_handle(stream=None):
 
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+class HostBuffer:
+    """Pinned, mapped, coherent host memory that kernels read and write directly (pgm_host_alloc):
+    `array` (numpy) and `tensor` (a CPU torch view of the same bytes, for descriptor building) share
+    it; freed with the object."""
+
+    def __init__(self, shape, dtype):
+        import torch
+
+        L = lib()
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) if len(shape) else 1
+        p = ctypes.c_void_p()
+        check(L.pgm_host_alloc(ctypes.byref(p), max(1, n * dtype.itemsize)), "host_alloc")
+        self._p = p
+        raw = (ctypes.c_char * max(1, n * dtype.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(raw, dtype=dtype, count=n).reshape(shape)
+        self.tensor = torch.from_numpy(self.array)
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            try:
+                load_library().pgm_host_free(p)
+            except Exception:
+                pass
+            self._p = None
 
 
 def ptr(t):

@@ -2959,6 +2959,27 @@ int pgm_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
   return PGM_OK;
 }
 
+int pgm_host_alloc(void **ptr, size_t bytes) {
+  STALE_PROBE();
+  if (!ptr) return fail(PGM_EINVAL, "host_alloc: null pointer");
+  *ptr = nullptr;
+  if (bytes == 0) bytes = 1;
+  const hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *ptr = nullptr;
+    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "host_alloc: %s", hipGetErrorString(e));
+  }
+  memset(*ptr, 0, bytes);
+  return PGM_OK;
+}
+
+int pgm_host_free(void *ptr) {
+  STALE_PROBE();
+  if (ptr) HIP_TRY(hipHostFree(ptr));
+  return PGM_OK;
+}
+
 int pgm_memset(void *dst, int value, size_t bytes, void *stream) {
   STALE_PROBE();
   if (bytes == 0) return PGM_OK;

@@ -24,6 +24,7 @@ side keeping >= 16 states) run on FP64 MFMA instead (pgm_gemm, engine.pair_gemm)
 and executor run single queries (C2) and row batches.
 """
 import heapq
+from functools import partial
 from collections import OrderedDict
 from itertools import count
 
@@ -123,7 +124,7 @@ def greedy_path(operand_labels, out_labels, dims):
     return steps, final_id
 
 
-def elimination_path(operand_labels, out_labels, dims):
+def elimination_path(operand_labels, out_labels, dims, depth_aware=False):
     """A contraction path from a variable-elimination order (returns greedy_path's format).
 
     opt_einsum's greedy rule (greedy_path) looks one pairwise step ahead; on munin's C2 query it
@@ -132,9 +133,13 @@ def elimination_path(operand_labels, out_labels, dims):
     (pgmpy/inference/EliminationOrder.py:136-150: the product of the cardinalities of the
     variable's neighbours) measured on the current factors — multiplying the factors that hold it
     smallest-first and summing it out with the last product.  On C2 that is 18 MFLOP and 32 MB
-    with a 168 K-entry largest intermediate.  Values do not depend on the path beyond rounding."""
+    with a 168 K-entry largest intermediate.  Values do not depend on the path beyond rounding.
+    depth_aware: the factors holding the variable are multiplied shallowest-first (then smallest) —
+    a balanced product tree instead of a chain, so fewer dependency levels (one launch each in a
+    compiled program) for somewhat larger intermediates (C2: 23 levels / 49 MB against 29 / 32 MB)."""
     out_set = set(out_labels)
     ops = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    dep = {i: 0 for i in ops}
     holders = {}
     for i, ls in ops.items():
         for l in ls:
@@ -149,6 +154,7 @@ def elimination_path(operand_labels, out_labels, dims):
         nid = next(ids)
         steps.append((kind,) + tuple(olds[:1] if kind == "reduce" else olds) + (keep, nid))
         touched = set()
+        dep[nid] = 1 + max(dep[o] for o in olds)
         for o in olds:
             for l in ops[o]:
                 holders[l].discard(o)
@@ -158,6 +164,9 @@ def elimination_path(operand_labels, out_labels, dims):
             holders[l].add(nid)
         ops[nid] = keep
         return nid, touched
+
+    def order_key(i):
+        return (dep[i], _size(ops[i], dims), i) if depth_aware else (_size(ops[i], dims), i)
 
     for i in list(ops):  # 1. private labels, as in greedy_path
         keep = kept(ops[i], {i})
@@ -185,13 +194,13 @@ def elimination_path(operand_labels, out_labels, dims):
             heapq.heappush(heap, (cw, ver[v], str(v), v))
             continue
         done.add(v)
-        inv = sorted(holders[v], key=lambda i: (_size(ops[i], dims), i))
+        inv = sorted(holders[v], key=order_key)
         touched = set()
         while len(inv) > 1:
             a, b = inv[0], inv[1]
             nid, t = retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
             touched |= t
-            inv = sorted([nid] + inv[2:], key=lambda i: (_size(ops[i], dims), i))
+            inv = sorted([nid] + inv[2:], key=order_key)
         if v in ops[inv[0]]:
             _, t = retire([inv[0]], [l for l in ops[inv[0]] if l != v], "reduce")
             touched |= t
@@ -200,7 +209,7 @@ def elimination_path(operand_labels, out_labels, dims):
                 ver[l] = ver.get(l, 0) + 1
                 heapq.heappush(heap, (weight(l), ver[l], str(l), l))
     while len(ops) > 1:  # 3. what is left shares only output labels: smallest first
-        a, b = sorted(ops, key=lambda k: (_size(ops[k], dims), k))[:2]
+        a, b = sorted(ops, key=order_key)[:2]
         retire([a, b], kept(list(dict.fromkeys(ops[a] + ops[b])), {a, b}), "pair")
     (final_id,) = ops.keys() if ops else (None,)
     return steps, final_id
@@ -281,14 +290,15 @@ def path_cost(steps, operand_labels, dims):
 
 
 def choose_path(operand_labels, out_labels, dims):
-    """The cheaper of opt_einsum's greedy path and the min-weight elimination path, by an MI355X
-    estimate: bytes at 3 TB/s + flops at 15 TFLOP/s + 3 us per dependency level (one batched
-    launch per level in a compiled program)."""
+    """The cheapest of opt_einsum's greedy path and the min-weight elimination path (product chains,
+    or shallowest-first product trees), by an MI355X estimate: bytes at 3 TB/s + flops at 15 TFLOP/s
+    + 5 us per dependency level (one batched launch per level in a compiled program: ~5 us launch to
+    launch for these small steps, profiles/r03g_c2_levels.txt)."""
     best = None
-    for planner in (greedy_path, elimination_path):
+    for planner in (greedy_path, elimination_path, partial(elimination_path, depth_aware=True)):
         steps, final_id = planner(operand_labels, out_labels, dims)
         nbytes, flops, depth = path_cost(steps, operand_labels, dims)
-        est = nbytes / 3e12 + flops / 15e12 + depth * 3e-6
+        est = nbytes / 3e12 + flops / 15e12 + depth * 5e-6
         if best is None or est < best[0]:
             best = (est, steps, final_id)
     return best[1], best[2]

@@ -427,8 +427,8 @@ class PatternPlan:
     def _steps_program(self, n, outs, host_io=False):
         """The steps path for n rows compiled once: evidence gathers from the plan's own codes
         buffer, the greedy contraction (dense steps on FP64 MFMA), normalisation and the requested
-        outputs into preallocated buffers, captured as one HIP graph.  host_io: pinned host buffers for
-        QueryRunner's copies (query_one).  Returns (program, codes buffer, error flag, outputs, device column
+        outputs into preallocated buffers, captured as one HIP graph.  host_io: the codes buffer and the
+        outputs are host memory the kernels access directly (QueryRunner via query_one).  Returns (program, codes buffer, error flag, outputs, device column
         map, host buffers or None)."""
         progs = self.__dict__.setdefault("_progs", {})
         hit = progs.get((n, outs, host_io))
@@ -444,12 +444,16 @@ class PatternPlan:
         ev_set = set(self.evidence_vars)
         cols = list(self.ev_used)
         local = {v: i for i, v in enumerate(cols)}
-        codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
         perr = torch.zeros(1, dtype=torch.int32, device=dev)
         host = None
-        if host_io:  # pinned staging buffers for QueryRunner's copies (stream-ordered, outside the graph)
-            host = {"codes": torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, pin_memory=True),
-                    "err": torch.zeros(1, dtype=torch.int32, pin_memory=True)}
+        if host_io:
+            # the evidence codes and the result live in pinned, mapped, coherent host memory that the
+            # kernels read and write directly (pgm_host_alloc): a query is one graph launch + one
+            # synchronize, no copy of any size on either side
+            host = {"codes": N.HostBuffer((max(1, len(cols)), n), np.uint8)}
+            codes_buf = host["codes"].tensor
+        else:
+            codes_buf = torch.zeros((max(1, len(cols)), n), dtype=torch.uint8, device=dev)
         ops = []
         prog.begin_batch()  # every factor's evidence slice: one launch
         for t, vars_ in self._dev_factors():
@@ -468,8 +472,15 @@ class PatternPlan:
         R = contract_factors(ops, outl, prog=prog)  # [Q..., ROW] C-order
         Z = prog.contract(R, outl, None, None, [E.ROW], reduce="sum", combine="copy")
         bufs = {}
+
+        def out_buf(key, shape):
+            if host_io:
+                host[key] = N.HostBuffer(tuple(shape), np.float64)
+                return host[key].tensor
+            return E.empty(list(shape))
+
         if "marg" in outs:
-            bufs["marg"] = E.empty([self.n_acc, n])
+            bufs["marg"] = out_buf("marg", [self.n_acc, n])
             for i, v in enumerate(self.variables):
                 a = self.acc_off[i]
                 m = prog.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
@@ -479,12 +490,9 @@ class PatternPlan:
             bufs["map"] = torch.empty(n, dtype=torch.int32, device=dev)
             prog.argmax(R, n, self.P, 1, n, bufs["map"])
         if "joint" in outs:
-            bufs["joint"] = E.empty([self.P, n])
+            bufs["joint"] = out_buf("joint", [self.P, n])
             prog.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw",
                           out=bufs["joint"])
-        if host_io:
-            for k, b in bufs.items():
-                host[k] = torch.empty(tuple(b.shape), dtype=b.dtype, pin_memory=True)
         prog.capture()
         cols_dev = torch.tensor([self.col_of[v] for v in cols], dtype=torch.int32, device=dev) if cols else None
         hit = (prog, codes_buf, perr, bufs, cols_dev, host)
@@ -492,32 +500,22 @@ class PatternPlan:
         return hit
 
     def query_one(self, codes, key):
-        """One evidence row (codes[col_of[v]]: the state number of evidence variable v) through the steps
-        program: the plan's evidence columns copied from a pinned buffer, the error flag reset, one graph
-        launch, the result and the flag copied back asynchronously, ONE synchronize.
+        """One evidence row (codes[col_of[v]]: the state number of evidence variable v, already checked
+        against the state names on the host) through the steps program whose codes and result live in
+        host memory the kernels access directly: fill the codes, one graph launch, one synchronize.
         Returns a new fp64 ndarray (`key` "marg" or "joint")."""
         L = N.lib()
         with self._lock:
-            prog, cbuf, perr, bufs, _, host = self._steps_program(1, frozenset([key]), host_io=True)
+            prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
             sel = self.__dict__.get("_ev_sel")
             if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
                 sel = self._ev_sel = [self.col_of[v] for v in self.ev_used]
-            s = N.stream_handle()
-            hc = host["codes"]
             if sel:
-                hc.numpy()[:, 0] = [codes[i] for i in sel]
-                N.check(L.pgm_memcpy_h2d(N.ptr(cbuf), ctypes.c_void_p(hc.data_ptr()), hc.numel(), s), "memcpy_h2d")
-            # the flag is reset outside the graph: a captured 4-byte memset node replayed later wrote
-            # 0x02020202 after other graphs had run (r03g, tools/c1_debug.py) — never captured here
-            N.check(L.pgm_memset(N.ptr(perr), 0, 4, s), "memset")
+                host["codes"].array[:, 0] = [codes[i] for i in sel]
+            s = N.stream_handle()
             prog.run()
-            ho, he, b = host[key], host["err"], bufs[key]
-            N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(ho.data_ptr()), N.ptr(b), b.numel() * 8, s), "memcpy_d2h")
-            N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(he.data_ptr()), N.ptr(perr), 4, s), "memcpy_d2h")
             N.check(L.pgm_stream_sync(s), "stream_sync")
-            if int(he.numpy()[0]) != 0:
-                raise IndexError("evidence state code out of range")
-            return ho.numpy().reshape(-1).copy()
+            return host[key].array.reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
         """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
