@@ -175,6 +175,7 @@ struct PMSpec {  // one fused step's specialisation
   ProdMK k;
   int red = PGM_RED_SUM, XI = 1, unroll = 8;
   bool store = true, xcd = false, nt = false;
+  bool wt = false;    // write-through (sc1) 16-B product stores: no dirty lines left for the kernel's end
   bool has_m = true;  // false: the product alone (pgm_product_n_bind), no marginal
   unsigned gx = 1;
   uint64_t total = 0;  // blocks
@@ -211,6 +212,8 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   if (xcd) pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n",
                    (unsigned long long)(total / 8));
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
+  if (store && sp.wt)
+    o += "  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0x7fffffff, 0x00020000);\n";
   o += "  unsigned idx = ob;\n  long long oc = 0, om = 0";
   for (int i = 0; i < k.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)oc; (void)idx;\n";
@@ -309,10 +312,14 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     pgmi_appendf(o, "%sconst pgm_d2 w%d = {w%dx, w%dy};\n", ind.c_str(), u, u, u);
   }
   if (store) {
-    pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
+    if (!sp.wt) pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
     for (int u = 0; u < XI; ++u) {
       const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
-      if (nt)
+      if (sp.wt)  // byte offset < 2 GiB (checked at bind)
+        pgmi_appendf(o, "%s%s{ pgm_u32x4 q_; __builtin_memcpy(&q_, &w%d, 16); __builtin_amdgcn_raw_buffer_store_b128("
+                        "q_, rsC, (int)((oc + %s + 2LL * x%d) * 8LL), 0, 16); }\n",
+                     ind.c_str(), guard.c_str(), u, lin(k.rsc).c_str(), u);
+      else if (nt)
         pgmi_appendf(o, "%s%s__builtin_nontemporal_store(w%d, cj + x%d);\n", ind.c_str(), guard.c_str(), u, u);
       else
         pgmi_appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
@@ -488,6 +495,7 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
   std::string o =
       "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
       "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
+      "typedef unsigned int pgm_u32x4 __attribute__((ext_vector_type(4)));\n"
       "__device__ __forceinline__ double pgm_ratio(double a, double b) { const double r = a / b; "
       "return r != r ? 0.0 : r; }\n"
       "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
@@ -619,6 +627,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
   static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
   static const int nt = pm_knob("PGM_PM_NT", 1);
+  static const int wt = pm_knob("PGM_PM_WT", 0);  // write-through product stores (A/B knob)
   static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
   const uint64_t entries = (uint64_t)k.n_outer * (uint64_t)k.n_red * 2ull * k.NP;
   if (!on || no_jit || entries < (uint64_t)min_entries) return PGM_OK;  // *bound NULL: generic kernel
@@ -651,6 +660,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.has_m = has_m;
   sp.xcd = xcd_knob && total % 8 == 0;
   sp.nt = nt != 0;
+  sp.wt = wt != 0 && sp.store && entries * 8ull + 64ull < (1ull << 31);
   sp.gx = (unsigned)gx;
   sp.total = total;
   std::vector<uint64_t> starts;
