@@ -388,7 +388,12 @@ class BeliefPropagation(Inference):
             t, ls = cal.beliefs[c]
             f = fac[frozenset(c)]._meta_copy()
             n = t.numel()
-            f._set_d(flat[at:at + n].view(tuple(int(k) for k in f.cardinality)))
+            fv = list(f.variables)
+            card = {v: int(k) for v, k in zip(fv, f.cardinality)}
+            d = flat[at:at + n].view(tuple(card[v] for v in ls))  # the schedule's clique layout
+            if list(ls) != fv:
+                d = E.contract(d, list(ls), None, None, fv, combine="copy")
+            f._set_d(d)
             at += n
             self.clique_beliefs[c] = f
         for p, c in bjt.order:
