@@ -271,6 +271,9 @@ class BatchedJunctionTree:
         # the work between XCDs — every separator-sized operand slice is then read by one XCD only —
         # while the belief is still written in address order.  PGM_BP_LAYOUT=0: the factor's own order.
         shared = {}
+        # only the large cliques (measured: the uniform rule slowed the 8-12 K-state cliques' level,
+        # profiles/r03m_*): PGM_BP_LAYOUT_MIN states and up
+        layout_min = int(os.environ.get("PGM_BP_LAYOUT_MIN", 16384))
         if os.environ.get("PGM_BP_LAYOUT", "1") != "0":
             for a, b in jt.edges():
                 for v in set(a) & set(b):
@@ -280,7 +283,7 @@ class BatchedJunctionTree:
             f = jt.get_factors(c)
             labels = list(f.variables)
             t = f._d()
-            if shared:
+            if shared and int(np.prod([int(k) for k in f.cardinality])) >= layout_min:
                 pos = {v: i for i, v in enumerate(labels)}
                 order = sorted(labels, key=lambda v: (-shared.get((c, v), 0), pos[v]))
                 if order != labels:
