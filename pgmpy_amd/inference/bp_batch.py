@@ -269,12 +269,13 @@ class BatchedJunctionTree:
         # pathfinder's Fault in all 57 separators of the root.  A fused clique pass walks its kept states
         # in layout order and hands each XCD a contiguous range of them, so the shared variables split
         # the work between XCDs — every separator-sized operand slice is then read by one XCD only —
-        # while the belief is still written in address order.  PGM_BP_LAYOUT=0: the factor's own order.
+        # while the belief is still written in address order.  A/B knob PGM_BP_LAYOUT=1 (default: the
+        # factor's own order — the rule shortened the root levels but slowed the schedule as a whole).
         shared = {}
         # only the large cliques (measured: the uniform rule slowed the 8-12 K-state cliques' level,
         # profiles/r03m_*): PGM_BP_LAYOUT_MIN states and up
         layout_min = int(os.environ.get("PGM_BP_LAYOUT_MIN", 16384))
-        if os.environ.get("PGM_BP_LAYOUT", "1") != "0":
+        if os.environ.get("PGM_BP_LAYOUT", "0") == "1":  # measured slower overall (r03m/r03n): off
             for a, b in jt.edges():
                 for v in set(a) & set(b):
                     shared[(a, v)] = shared.get((a, v), 0) + 1
