@@ -227,12 +227,36 @@ class Launcher:
                 q.sync()
         torch.cuda.synchronize()
 
+    def steps_released(self, k):
+        """k steps (group 1) whose last launch on each queue releases at system scope on its own
+        completion (pgm_dq_launch_release), so the window needs no separate release barrier packet."""
+        nq = len(self.qs) if self.kind == "direct" else 0
+        if self.group != 1 or nq == 0 or k < nq:
+            self.steps(k)
+            self._released = False
+            return
+        last = set()
+        n = len(self.rs)
+        for j in range(k - nq, k):
+            last.add(j)
+        for j in range(k):
+            r = self.rs[self._next]
+            if j in last:
+                r.run_release()
+            else:
+                r.run()
+            self._next = (self._next + 1) % n
+        # every queue got exactly one released launch when its launches are round robin over the queues
+        self._released = len({id(self.rs[(self._next - 1 - t) % n].queue) for t in range(nq)}) == nq
+
     def release_and_wait(self):
-        """End of a timed region with the outputs released at system scope: direct queues append their
-        release barriers together, then wait; HIP: wait() (end event + device synchronize)."""
-        if self.kind == "direct":
+        """End of a timed region with the outputs released at system scope: when the window's last
+        launch per queue carried the release (steps_released) just wait; else direct queues append
+        their release barriers together, then wait; HIP: wait() (end event + device synchronize)."""
+        if self.kind == "direct" and not getattr(self, "_released", False):
             for q in self.qs:
                 q.release()
+        self._released = False
         self.wait()
 
     def wait(self):
@@ -511,10 +535,10 @@ def bench_c3(args, dist, rank, world):
     # kernel time omits
     launcher.timer_start()
     t_start = time.perf_counter()
-    launcher.steps(args.steps)
+    launcher.steps_released(args.steps)
     # the window closes on every step's dispatch complete AND its outputs visible system-wide: on the
-    # direct queues one system-scope release barrier packet per queue, all appended before any is waited
-    # for (pgm_dq_release, then pgm_dq_wait); HIP: the end event + torch.cuda.synchronize
+    # direct queues the last launch of each queue releases at system scope on its own completion
+    # (pgm_dq_launch_release), then every dispatch is waited for; HIP: the end event + torch.cuda.synchronize
     launcher.release_and_wait()
     t_end = time.perf_counter()
     kern_ms_total = launcher.timer_stop_ms()  # dispatch timestamps, read after the timed region

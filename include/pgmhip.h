@@ -478,6 +478,10 @@ int pgm_dq_launch(void *dbound);
  * the first waits for everything before it (barrier bit), the others may overlap it and each other;
  * the next launch or sync waits for the whole group.  At most 128 launches, no launch repeated. */
 int pgm_dq_launch_group(void *const *dbounds, int32_t n);
+/* one dispatch whose own completion releases at system scope (its packet's release fence): the last
+ * dispatch before the host or HIP reads the outputs, instead of a separate pgm_dq_sync barrier packet;
+ * wait for it with pgm_dq_wait.  Like pgm_dq_sync, the next dispatch acquires at system scope. */
+int pgm_dq_launch_release(void *dbound);
 int pgm_dq_sync(void *dq);
 /* the first half of pgm_dq_sync: append the system-scope release barrier packet without waiting for
  * it (pgm_dq_wait then waits for it with the dispatches), so several queues release in parallel */

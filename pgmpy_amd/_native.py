@@ -230,6 +230,7 @@ _SIGS = {
     "pgm_dq_sync": ([_P], ctypes.c_int),
     "pgm_dq_wait": ([_P], ctypes.c_int),
     "pgm_dq_release": ([_P], ctypes.c_int),
+    "pgm_dq_launch_release": ([_P], ctypes.c_int),
     "pgm_dq_timer_start": ([_P], ctypes.c_int),
     "pgm_dq_timer_stop_ms": ([_P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "pgm_dq_timer_stop_ticks": ([_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),

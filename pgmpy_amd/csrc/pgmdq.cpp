@@ -434,7 +434,7 @@ int pgm_dq_bind_rows(void *handle, void *bound, void **out) {
 }
 
 // one kernel-dispatch packet of a bound launch (caller holds dq->mu)
-static int dispatch(DirectBound *db, bool barrier) {
+static int dispatch(DirectBound *db, bool barrier, bool sys_release = false) {
   DirectQueue *dq = db->dq;
   if (dq->fresh) {
     // the first dispatch after bind/sync: HIP work issued since (a copy or kernel writing the inputs)
@@ -466,11 +466,12 @@ static int dispatch(DirectBound *db, bool barrier) {
   pkt->reserved2 = 0;
   pkt->completion_signal = sig;
   const uint16_t acq = dq->fresh ? dq->fresh_acq_scope : dq->acq_scope;
+  const uint16_t rel = sys_release ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : db->rel_scope;
   dq->fresh = false;
-  dq->need_release = dq->need_release || db->rel_scope != HSA_FENCE_SCOPE_SYSTEM;
+  dq->need_release = sys_release ? false : (dq->need_release || db->rel_scope != HSA_FENCE_SCOPE_SYSTEM);
   dq->last_kernel = dq->issued;
   if (barrier) dq->group_first = dq->issued;
-  publish(dq, slot, header_word(HSA_PACKET_TYPE_KERNEL_DISPATCH, acq, db->rel_scope,
+  publish(dq, slot, header_word(HSA_PACKET_TYPE_KERNEL_DISPATCH, acq, rel,
                                 (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS), barrier), idx);
   return PGM_OK;
 }
@@ -480,6 +481,15 @@ int pgm_dq_launch(void *dbound) {
   if (!db) return fail(PGM_EINVAL, "dq_launch: null handle");
   std::lock_guard<std::mutex> lk(db->dq->mu);
   return dispatch(db, true);
+}
+
+int pgm_dq_launch_release(void *dbound) {
+  DirectBound *db = (DirectBound *)dbound;
+  if (!db) return fail(PGM_EINVAL, "dq_launch_release: null handle");
+  std::lock_guard<std::mutex> lk(db->dq->mu);
+  const int rc = dispatch(db, true, true);
+  if (rc == PGM_OK) db->dq->fresh = true;  // as after pgm_dq_sync: the next dispatch acquires at system scope
+  return rc;
 }
 
 int pgm_dq_launch_group(void *const *dbounds, int32_t n) {

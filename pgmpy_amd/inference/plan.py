@@ -894,6 +894,12 @@ class DirectRows:
             N.check(st, "dq_launch")
         return self.out
 
+    def run_release(self):
+        """The launch with a system-scope release on its own completion (pgm_dq_launch_release): the last
+        launch before the outputs are read; wait with queue.wait()."""
+        N.check(N.lib().pgm_dq_launch_release(self._h), "dq_launch_release")
+        return self.out
+
     def sync(self):
         self.queue.sync()
 

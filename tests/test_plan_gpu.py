@@ -285,6 +285,19 @@ def test_direct_queue_launch_matches_bound(gpu, rows):
     plan.bind(d, rows, 0, rows, ref).run()
     torch.cuda.synchronize()
     assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    # HIP writes the inputs and clears the outputs with NO synchronize before the next direct launch: the
+    # first dispatch after a sync drains HIP work itself; the launch releases at system scope
+    # on its own completion (pgm_dq_launch_release), so a wait suffices before HIP reads the outputs
+    d.copy_(upload_codes(ev))
+    out["marg"].zero_()
+    out["map"].zero_()
+    direct.run_release()
+    q.wait()
+    plan.bind(d, rows, 0, rows, ref).run()
+    torch.cuda.synchronize()
+    assert torch.equal(out["marg"], ref["marg"]) and torch.equal(out["map"], ref["map"])
+    direct.run()  # the dispatch after a released launch acquires again (as after a sync)
+    q.sync()
 
 
 def test_direct_group_launch_matches_bound(gpu):
