@@ -101,11 +101,12 @@ class Evidence:
         return self.codes.index_select(1, idx).contiguous()
 
 
-def _column_raw(v, st, col):
+def _column_raw(v, st, col, fallback=None):
     """(int8 raw indices, LUT) of one column: pandas Categorical codes or Arrow dictionary indices
     and a category -> state LUT, or, for any other dtype, the state numbers themselves (one host hash
     pass) and the identity LUT.
-    None when the column does not fit int8 indices (the host encoder handles the frame)."""
+    None when the column does not fit int8 indices (the host encoder handles the frame).  `fallback`
+    (a set) receives `col` when a cell reached its state through the str() fallback."""
     import pandas as pd
 
     cats = raw = None
@@ -130,6 +131,8 @@ def _column_raw(v, st, col):
             sm = {str(x): i for i, x in enumerate(st)}
             for i in miss:
                 lut[i] = sm.get(str(cats[i]), 254)
+            if fallback is not None:
+                fallback.add(col)
         return raw, lut.astype(np.uint8)
     if len(st) > 127:
         return None
@@ -148,6 +151,8 @@ def _column_raw(v, st, col):
                 if k is None:
                     raise KeyError(f"state: {vals[i]} is an unknown for variable: {col}. It must be one of {st}")
                 c[i] = k
+            if fallback is not None:
+                fallback.add(col)
     return c.astype(np.int8), np.arange(len(st), dtype=np.uint8)
 
 
@@ -167,14 +172,16 @@ def ingest_frame(model, data, columns=None, row_hash=False):
     n = len(data)
     nc = len(columns)
     raws, luts = [], []
+    fallback = set()
     for col in columns:
         st = list(states[col])
         if len(st) >= MISSING:
             raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
-        r = _column_raw(data[col], st, col)
+        r = _column_raw(data[col], st, col, fallback)
         if r is None:
             codes = encode_frame(model, data, columns)
             ev = Evidence(upload_codes(codes), group_patterns(codes), n)
+            ev.fallback_cols = None  # unknown: the host encoder does not report it
             if row_hash:
                 ev.row_hash = _host_row_hash(codes)
             return ev
@@ -222,6 +229,7 @@ def ingest_frame(model, data, columns=None, row_hash=False):
             groups.append((hr[:, rows[0]] >= 0, rows))
         groups.sort(key=lambda gr: gr[1][0])
     ev = Evidence(d_codes, groups, n)
+    ev.fallback_cols = fallback
     if row_hash:
         ev.row_hash = download(d_hash)
     return ev
@@ -561,14 +569,17 @@ def _hash_groups_exact(ev, first, inv):
     return bool(torch.equal(ev.codes.index_select(1, idx), ev.codes))
 
 
-def _raw_values_ambiguous(model, data, columns):
+def _raw_values_ambiguous(model, data, columns, fallback_cols=None):
     """Whether two distinct raw cell values of a column map to one state (the str() fallback:
     1 and "1"; or two categories with the same state), so grouping by state codes would merge rows
-    the reference's groupby over raw values keeps apart."""
+    the reference's groupby over raw values keeps apart.  fallback_cols: the columns ingestion saw
+    use the str() fallback (only those can be ambiguous); None = check every column."""
     import pandas as pd
 
     states = model.states
     for col in columns:
+        if fallback_cols is not None and col not in fallback_cols:
+            continue
         v = data[col]
         st = list(states[col])
         if isinstance(v.dtype, pd.CategoricalDtype):
@@ -604,7 +615,8 @@ def predict_stochastic_frame(model, data, seed=None):
     ev = ingest_frame(model, data, columns, row_hash=True)
     _, first, inv = np.unique(ev.row_hash, axis=0, return_index=True, return_inverse=True)
     inv = inv.reshape(-1)
-    if not _hash_groups_exact(ev, first, inv) or _raw_values_ambiguous(model, data, columns):
+    if not _hash_groups_exact(ev, first, inv) or \
+            _raw_values_ambiguous(model, data, columns, getattr(ev, "fallback_cols", None)):
         # a hash collision, or cells whose raw values differ but reach the same state (1 and "1"
         # through the str() fallback): the reference's own grouping of the raw values (L867)
         gid = data.groupby(columns, dropna=False, sort=False).ngroup().to_numpy()
