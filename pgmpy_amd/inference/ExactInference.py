@@ -145,8 +145,10 @@ class VariableElimination(Inference):
             virt_evidence = {"__" + cpd.variables[0]: 0 for cpd in virtual_evidence}
             return self.query(variables=variables, evidence={**evidence, **virt_evidence}, virtual_evidence=None,
                               elimination_order=elimination_order, joint=joint, show_progress=show_progress)
+        node_map = getattr(self.model, "_node", None)  # networkx's node dict: a plain membership test
         if (isinstance(self.model, DiscreteBayesianNetwork) and elimination_order == "greedy"
-                and all(v in self.model for v in list(variables) + list(evidence))):
+                and all(v in (node_map if node_map is not None else self.model)
+                        for v in itertools.chain(variables, evidence))):
             return self._query_compiled(list(variables), evidence, joint)
         if isinstance(self.model, DiscreteBayesianNetwork):
             model_reduced, evidence = self._prune_bayesian_model(variables, evidence)
@@ -213,7 +215,20 @@ class VariableElimination(Inference):
             cache[key] = runner  # most recently used last
         plan = runner.plan
         model = self.model
-        codes = [model.get_cpds(v).get_state_no(v, evidence[v]) for v in ev_vars]
+        # state name -> number tables of the evidence variables, taken once per runner (a runner lives as
+        # long as its plan is current: same model structure and CPDs); a name not in a table goes through
+        # get_state_no, which raises the reference's KeyError
+        tabs = runner.__dict__.get("_code_tables")
+        if tabs is None:
+            cpds = [model.get_cpds(v) for v in ev_vars]
+            tabs = runner._code_tables = (
+                [(v, c.name_to_no[v]) for v, c in zip(ev_vars, cpds)] if all(c.state_names for c in cpds) else None)
+        try:
+            codes = [tab[evidence[v]] for v, tab in tabs] if tabs is not None else None
+        except (KeyError, TypeError):
+            codes = None
+        if codes is None:
+            codes = [model.get_cpds(v).get_state_no(v, evidence[v]) for v in ev_vars]
         vals = runner.run(codes)
         states = {v: model.get_cpds(v).state_names[v] for v in variables}
         if joint:
