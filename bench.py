@@ -535,7 +535,10 @@ def bench_c3(args, dist, rank, world):
     # kernel time omits
     launcher.timer_start()
     t_start = time.perf_counter()
-    launcher.steps_released(args.steps)
+    if args.release_mode == "launch":
+        launcher.steps_released(args.steps)
+    else:
+        launcher.steps(args.steps)
     # the window closes on every step's dispatch complete AND its outputs visible system-wide: on the
     # direct queues the last launch of each queue releases at system scope on its own completion
     # (pgm_dq_launch_release), then every dispatch is waited for; HIP: the end event + torch.cuda.synchronize
@@ -1143,6 +1146,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
+    ap.add_argument("--release-mode", default="launch", choices=["launch", "barrier"],
+                    help="c3 direct: the window's system-scope release on the last launch per queue (launch) or as "
+                         "one barrier packet per queue appended together (barrier)")
     ap.add_argument("--ring-prestart", action="store_true",
                     help="c3 --launch ring: launch the resident kernel just before the timed window")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")

@@ -38,7 +38,7 @@ def main():
     print("warm ms/query", (time.perf_counter() - t0) / 20 * 1e3, flush=True)
     runner, = ve._compiled.values()
     plan = runner.plan
-    (prog, cbuf, perr, bufs, cols_dev), = plan._progs.values()
+    (prog, cbuf, perr, bufs, cols_dev, _host), = plan._progs.values()
     L = N.lib()
     a, b = ctypes.c_void_p(), ctypes.c_void_p()
     N.check(L.pgm_event_create(ctypes.byref(a)))
