@@ -27,6 +27,9 @@ PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 18))  # C4 1,000 ro
 # Measured slower on C2 (r03f: 0.58-1.69 ms/query against 0.27 with one launch per level; a grid barrier
 # with its agent-scope write-back / invalidate costs more than a kernel boundary), so off by default.
 LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
+# n-ary products with more operands than one kernel takes: balanced tree (default) or sequential fold
+# (PGM_PRODN_TREE=0, A/B knob)
+TREE_PRODUCTS = os.environ.get("PGM_PRODN_TREE", "1") != "0"
 
 
 def _key(t):
@@ -396,6 +399,17 @@ class Program:
         ops = list(operands)
         kinds = list(kinds) if kinds is not None else [N.PRODN_MUL] * len(ops)
         L = N.lib()
+        if len(ops) > N.PRODN_MAX_OPS and all(k == N.PRODN_MUL for k in kinds) and TREE_PRODUCTS:
+            # more operands than one kernel takes: a balanced tree of products (independent groups of
+            # up to PRODN_MAX_OPS, then their partial products) instead of a sequential fold, so a
+            # levelled program runs the groups in one level — pathfinder's root folds 46 one-variable
+            # messages: 2 dependency levels instead of 7
+            m = N.PRODN_MAX_OPS
+            n_groups = -(-len(ops) // m)
+            size = -(-len(ops) // n_groups)
+            partials = [(self.product_n(ops[i:i + size], out_labels), list(out_labels))
+                        for i in range(0, len(ops), size)]
+            return self.product_n(partials, out_labels, out)
         while len(ops) > N.PRODN_MAX_OPS:  # fold the surplus (plain MUL operands) into the output first
             cut = N.PRODN_MAX_OPS if kinds[N.PRODN_MAX_OPS - 1] != N.PRODN_RATIO else N.PRODN_MAX_OPS - 1
             out = self.product_n(ops[:cut], out_labels, out, kinds[:cut])
