@@ -1146,7 +1146,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
-    ap.add_argument("--release-mode", default="launch", choices=["launch", "barrier"],
+    ap.add_argument("--release-mode", default="barrier", choices=["launch", "barrier"],
                     help="c3 direct: the window's system-scope release on the last launch per queue (launch) or as "
                          "one barrier packet per queue appended together (barrier)")
     ap.add_argument("--ring-prestart", action="store_true",
