@@ -63,9 +63,6 @@ int pgm_event_create(void **ev);
 int pgm_event_destroy(void *ev);
 int pgm_event_record(void *ev, void *stream);
 int pgm_event_elapsed_ms(void *start, void *stop, float *ms);
-/* stream waits for the event (cross-stream dependency; inside a graph capture: an edge of the graph, so a
- * compiled program is captured as a DAG over several streams) */
-int pgm_stream_wait_event(void *stream, void *ev);
 
 /* ---------------------------------------------------------------- contract
  * The one generic kernel behind DiscreteFactor.product / sum / divide /

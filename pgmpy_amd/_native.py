@@ -148,7 +148,6 @@ _SIGS = {
     "pgm_event_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_event_destroy": ([_P], ctypes.c_int),
     "pgm_event_record": ([_P, _P], ctypes.c_int),
-    "pgm_stream_wait_event": ([_P, _P], ctypes.c_int),
     "pgm_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "pgm_contract_workspace": ([ctypes.POINTER(ContractDesc), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "pgm_contract": ([ctypes.POINTER(ContractDesc), _P, _P, _P, _P, ctypes.c_size_t, _P], ctypes.c_int),

@@ -3014,13 +3014,6 @@ int pgm_event_record(void *ev, void *stream) {
   return PGM_OK;
 }
 
-int pgm_stream_wait_event(void *stream, void *ev) {
-  STALE_PROBE();
-  if (!ev) return fail(PGM_EINVAL, "stream_wait_event: null event");
-  HIP_TRY(hipStreamWaitEvent(S(stream), (hipEvent_t)ev, 0));
-  return PGM_OK;
-}
-
 int pgm_event_elapsed_ms(void *start, void *stop, float *ms) {
   STALE_PROBE();
   HIP_TRY(hipEventSynchronize((hipEvent_t)stop));

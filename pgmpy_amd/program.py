@@ -30,9 +30,7 @@ LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
 # n-ary products with more operands than one kernel takes: balanced tree (default) or sequential fold
 # (PGM_PRODN_TREE=0, A/B knob)
 TREE_PRODUCTS = os.environ.get("PGM_PRODN_TREE", "1") != "0"
-# levelled programs captured as a DAG over this many streams (1: one stream, every launch after the
-# previous one).  A/B knob PGM_GRAPH_STREAMS.
-GRAPH_STREAMS = max(1, int(os.environ.get("PGM_GRAPH_STREAMS", "1")))
+
 
 
 def _key(t):
@@ -83,7 +81,6 @@ class Program:
         self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
         self._chains = []  # levelled batch handles (several dependency levels in one launch)
-        self.step_rw = []  # levelled Program: (read keys, write keys) of each lowered step (DAG capture)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
 
     # ------------------------------------------------------------------ batching
@@ -273,7 +270,6 @@ class Program:
         self.notes.append(f"levels {chain[0][0]}-{chain[-1][0]} as one levelled batch of {n_jobs} jobs")
         self.step_bytes.append(sum(r.nbytes for _, recs in chain for r in recs))
         self.step_levels.append(chain[0][0])
-        self.step_rw.append(_rw([r for _, recs in chain for r in recs]))
 
     def _emit_level(self, lv, recs):
         """One dependency level: its unbatched launches, then one batch launch of its small jobs."""
@@ -287,7 +283,6 @@ class Program:
                 self._steps.append(r.fn)
                 self.notes.append(r.note)
                 self.step_bytes.append(r.nbytes)
-                self.step_rw.append(_rw([r]))
                 if r.pm is not None:
                     self._pm_launch.append(r.pm)
         if len(small) < 2:
@@ -300,7 +295,6 @@ class Program:
         self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
         self.notes.append(f"level batch of {len(small)}: " + "; ".join(r.note[:60] for r in small[:4]))
         self.step_bytes.append(sum(r.nbytes for r in small))
-        self.step_rw.append(_rw(small))
         self.step_levels.extend([lv] * (len(self._steps) - n0))
 
     def barrier_timed_out(self):
@@ -344,7 +338,6 @@ class Program:
             self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
             self.step_bytes.append(sum(r.nbytes for r in part))
-            self.step_rw.append(_rw(part))
             done.update(part)
         return done
 
@@ -599,79 +592,13 @@ class Program:
         torch.cuda.current_stream().synchronize()
         s = N.stream_handle(self._stream)
         g = ctypes.c_void_p()
-        dag = self._levels and GRAPH_STREAMS > 1 and len(self.step_rw) == len(self._steps) and len(self._steps) > 1
         N.check(L.pgm_graph_capture_begin(s), "graph_capture_begin")
         try:
-            if dag:
-                self._capture_dag(s)
-            else:
-                for step in self._steps:
-                    step(s)
+            for step in self._steps:
+                step(s)
         finally:
             N.check(L.pgm_graph_capture_end(s, ctypes.byref(g)), "graph_capture_end")
-            for e in getattr(self, "_dag_keep", []):  # the graph holds its own edges
-                L.pgm_event_destroy(e)
-            self._dag_keep = []
         self._graph = g
-
-    def _capture_dag(self, s0):
-        """Record the lowered steps over up to GRAPH_STREAMS streams so the captured graph is a DAG:
-        a step waits (graph edge) only for the steps whose buffers it reads or overwrites (read-after-
-        write, write-after-read, write-after-write by storage key), not for every earlier level, so a
-        chain of small dependent launches (pathfinder's Fault-separator levels) runs beside independent
-        big ones.  A step goes on the stream of its latest dependency (else the least recently used)."""
-        import torch
-
-        L = N.lib()
-        streams = [s0] + [N.stream_handle(torch.cuda.Stream()) for _ in range(GRAPH_STREAMS - 1)]
-        self._dag_keep = []
-
-        def event():
-            e = ctypes.c_void_p()
-            N.check(L.pgm_event_create(ctypes.byref(e)), "event_create")
-            self._dag_keep.append(e)
-            return e
-
-        fork = event()
-        N.check(L.pgm_event_record(fork, s0), "event_record")
-        for st in streams[1:]:
-            N.check(L.pgm_stream_wait_event(st, fork), "stream_wait_event")
-        last_w = {}   # key -> step index of its last writer
-        readers = {}  # key -> step indices reading it since its last write
-        done_ev, on = {}, {}
-        tail = [-1] * len(streams)  # last step issued on each stream
-        use = list(range(len(streams)))
-        for i, (step, (rd, wr)) in enumerate(zip(self._steps, self.step_rw)):
-            deps = set()
-            for k in rd:
-                if k in last_w:
-                    deps.add(last_w[k])
-            for k in wr:
-                if k in last_w:
-                    deps.add(last_w[k])
-                deps.update(readers.get(k, ()))
-            deps.discard(i)
-            if deps:
-                j = on[max(deps)]
-            else:
-                j = use[0]
-            for d in deps:
-                if on[d] != j and d > tail[j]:
-                    N.check(L.pgm_stream_wait_event(streams[j], done_ev[d]), "stream_wait_event")
-            step(streams[j])
-            e = event()
-            N.check(L.pgm_event_record(e, streams[j]), "event_record")
-            done_ev[i], on[i], tail[j] = e, j, i
-            use.remove(j)
-            use.append(j)
-            for k in wr:
-                last_w[k] = i
-                readers[k] = []
-            for k in rd:
-                readers.setdefault(k, []).append(i)
-        for j in range(1, len(streams)):  # join every stream back into the capturing one
-            if tail[j] >= 0:
-                N.check(L.pgm_stream_wait_event(s0, done_ev[tail[j]]), "stream_wait_event")
 
     def __len__(self):
         self._lower()
@@ -689,15 +616,6 @@ class Program:
                 L.pgm_pm_bound_destroy(h)
         except Exception:
             pass
-
-
-def _rw(recs):
-    """(read keys, write keys) of the records one lowered launch runs."""
-    rd, wr = set(), set()
-    for r in recs:
-        rd.update(r.reads)
-        wr.update(r.writes)
-    return rd, wr
 
 
 def _work(d):
