@@ -354,6 +354,17 @@ def test_direct_group_launch_matches_bound(gpu):
         DirectGroup([rs[0], rs[0]])
     with pytest.raises(ValueError):
         DirectGroup([rs[0], plan.bind(d, rows * nb, rows, rows, outs[0]).direct(q)])
+    # distinct base pointers, overlapping bytes (views of one buffer): refused too
+    m = plan.n_acc * rows
+    flat = torch.empty(3 * m, dtype=torch.float64, device=d.device)
+    va = {"marg": flat[:m].view(plan.n_acc, rows)}
+    vb = {"marg": flat[m // 2:m // 2 + m].view(plan.n_acc, rows)}
+    ra = plan.bind(d, rows * nb, 0, rows, va).direct(q)
+    rb = plan.bind(d, rows * nb, rows, rows, vb).direct(q)
+    with pytest.raises(ValueError, match="overlapping"):
+        DirectGroup([ra, rb])
+    vc = {"marg": flat[m:2 * m].view(plan.n_acc, rows)}  # adjacent, not overlapping: accepted
+    DirectGroup([ra, plan.bind(d, rows * nb, rows, rows, vc).direct(q)])
 
 
 def test_direct_queues_in_parallel(gpu):
