@@ -691,10 +691,12 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
     if args.ring_prestart:
         # the resident kernel is launched before the window, as a serving engine's would be before
         # requests arrive; the window holds the K batches' posts, their processing, the kernel's exit
-        # and the closing synchronize (HIP's end-of-kernel system-scope release)
+        # and the closing synchronize (HIP's end-of-kernel system-scope release).  start returns once
+        # every workgroup is resident with its CPT staged (pgm_rows_ring_start_ready), so the window
+        # holds no part of the launch
         t_l = time.perf_counter()
         timer.start()
-        ring.start(args.steps)
+        ring.start(args.steps, wait_ready=True)
         timer.mark_end()
         launch_ms = (time.perf_counter() - t_l) * 1e3
         t_start = time.perf_counter()
@@ -738,8 +740,8 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
             "workload": "C3 munin predict_probability template: 3 missing / 1038 observed, fused row plan; "
                         "one step = one 100k-row batch posted to the resident ring launch (pgm_rows_ring_*), "
                         "batches resident in HBM, batch i on buffer set i % batches",
-            "launch": ("one resident launch per timed region, launched just before the window (--ring-prestart), "
-                       "K batches posted inside it" if args.ring_prestart else
+            "launch": ("one resident launch per timed region, launched and resident (every workgroup running) "
+                       "before the window (--ring-prestart), K batches posted inside it" if args.ring_prestart else
                        "one resident launch per timed region (started inside the window), K batches posted"),
             "ring_host_launch_ms": launch_ms,
             "network": "munin",

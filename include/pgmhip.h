@@ -447,6 +447,10 @@ int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint
                          int64_t ld_out, int32_t *const *map, double *const *gap, int32_t *err_flag, void *stream,
                          void **ring);
 int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s);
+/* start_ready: start, then wait (up to ready_timeout_s) until every workgroup of the resident grid is
+ * running with its CPT staged, so that what follows (posts, completions) no longer includes the launch
+ * itself; PGM_EDEVICE (and the launch cancelled) if the grid does not come up in time */
+int pgm_rows_ring_start_ready(void *ring, uint32_t n_batches, double timeout_s, double ready_timeout_s);
 int pgm_rows_ring_post(void *ring, uint32_t n_posted);
 int pgm_rows_ring_finish(void *ring);
 int pgm_rows_ring_cancel(void *ring);

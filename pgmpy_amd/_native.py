@@ -212,6 +212,7 @@ _SIGS = {
                               ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P, ctypes.POINTER(ctypes.c_void_p)],
                              ctypes.c_int),
     "pgm_rows_ring_start": ([_P, ctypes.c_uint32, ctypes.c_double], ctypes.c_int),
+    "pgm_rows_ring_start_ready": ([_P, ctypes.c_uint32, ctypes.c_double, ctypes.c_double], ctypes.c_int),
     "pgm_rows_ring_post": ([_P, ctypes.c_uint32], ctypes.c_int),
     "pgm_rows_ring_finish": ([_P], ctypes.c_int),
     "pgm_rows_ring_cancel": ([_P], ctypes.c_int),

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -34,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 15  // 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 16  // 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -2467,6 +2468,18 @@ static int ring_wg() {
   return wg;
 }
 
+// the ring's waiting waves back off (knob PGM_RING_BACKOFF, default 1): the workgroup's token wave reads the
+// chip-wide poll token before trying to take it, and sleeps longer the longer it has waited (4 -> 12 -> 32
+// x 64 clocks).  768 token waves retrying one atomic every ~0.1 us while the ring idles saturate that
+// address and delay the one wave that reads the host counter
+static bool ring_backoff() {
+  static const bool on = [] {
+    const char *e = getenv("PGM_RING_BACKOFF");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 static std::vector<int> rows_cols(const pgm_rows_plan *pl);
 static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R, bool coherent = false);
 static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, const std::vector<int> &cols,
@@ -2661,16 +2674,23 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
   const int NV = pl->n_values + 1;
   const int WG = ring_wg();
   const int K = (NV + WG - 1) / WG;
+  pgmi_appendf(o, "#define BACKOFF %d\n", ring_backoff() ? 1 : 0);
   o += "struct pgm_ring_slot { const unsigned char *C; long long ldc, row0; double *M; long long ldo; int *MP; "
        "double *G; long long pad; };\n";
   pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_ring(const double *__restrict__ V, "
              "const pgm_ring_slot *__restrict__ D, unsigned n_slots, unsigned *ctl, unsigned *g, unsigned n_batches, "
-             "unsigned base, long long n, int *__restrict__ E, int mode, unsigned long long timeout) {\n", WG);
+             "unsigned base, long long n, int *__restrict__ E, int mode, unsigned long long timeout, int signal) {\n", WG);
   o += "  const int t = threadIdx.x;\n";
   pgmi_appendf(o, "  __shared__ double S[%d];\n  __shared__ unsigned seen_s, token_s, stop_s;\n", K * WG);
   for (int i = 0; i < K; ++i) pgmi_appendf(o, "  const double s%d = V[t + %d < %d ? t + %d : %d];\n", i, WG * i, NV, WG * i, NV - 1);
   for (int i = 0; i < K; ++i) pgmi_appendf(o, "  S[t + %d < %d ? t + %d : %d] = s%d;\n", WG * i, NV, WG * i, NV - 1, i);
   o += "  if (t == 0) { seen_s = base; token_s = 0u; stop_s = 0u; }\n  __syncthreads();\n#define VAL(i) S[i]\n";
+  // readiness (pgm_rows_ring_wait_ready): every workgroup counts itself in g[4..5] (64-bit, never reset:
+  // each launch adds exactly gridDim.x) once its CPT copy is staged; the last one raises ctl[3] for the host
+  o += "  if (signal && t == 0) {\n"
+       "    const unsigned long long s = atomicAdd((unsigned long long *)(g + 4), 1ull) + 1ull;\n"
+       "    if (s % gridDim.x == 0ull) __hip_atomic_store(&ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+       "  }\n";
   pgmi_appendf(o, "  const unsigned long long W = (unsigned long long)gridDim.x * %d;\n", WG / 64);
   pgmi_appendf(o, "  const unsigned long long wv0 = (unsigned long long)blockIdx.x * %d + (t >> 6);\n", WG / 64);
   o += "  const unsigned long long chunks = (unsigned long long)(n + 127) / 128;\n"
@@ -2694,12 +2714,14 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "        __builtin_amdgcn_s_sleep(2);\n"
        "        continue;\n"
        "      }\n"
+       "      unsigned nap = 0u;\n"
        "      for (;;) {  /* this wave speaks for its workgroup */\n"
        "        unsigned m = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "        if (m <= ab) {\n"
        "          if (__hip_atomic_load(&g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = true; break; }\n"
        "          unsigned poll = 0u;\n"
-       "          if (lead) poll = atomicCAS(&g[1], 0u, 1u) == 0u ? 1u : 0u;\n"
+       "          if (lead && (!BACKOFF || __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u))\n"
+       "            poll = atomicCAS(&g[1], 0u, 1u) == 0u ? 1u : 0u;\n"
        "          poll = __builtin_amdgcn_readfirstlane(poll);\n"
        "          if (poll) {  /* the one reader of the host counter */\n"
        "            const unsigned p = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n"
@@ -2726,7 +2748,9 @@ static void emit_rows_ring(std::string &o, const pgm_rows_plan *pl) {
        "          if (lead) atomicMax(&seen_s, m);\n"
        "          break;\n"
        "        }\n"
-       "        __builtin_amdgcn_s_sleep(4);\n"
+       "        if (!BACKOFF || ++nap <= 2u) __builtin_amdgcn_s_sleep(4);\n"
+       "        else if (nap <= 8u) __builtin_amdgcn_s_sleep(12);\n"
+       "        else __builtin_amdgcn_s_sleep(32);\n"
        "      }\n"
        "      if (stop && lead) atomicExch(&stop_s, 1u);\n"
        "      if (lead) atomicExch(&token_s, 0u);\n"
@@ -4306,9 +4330,33 @@ int pgm_rows_ring_create(void *handle, int32_t mode, int32_t n_slots, const uint
   return PGM_OK;
 }
 
+static int ring_start(RowsRing *rg, uint32_t n_batches, double timeout_s, int signal);
+
 int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
   STALE_PROBE();
+  return ring_start((RowsRing *)ring, n_batches, timeout_s, 0);
+}
+
+int pgm_rows_ring_start_ready(void *ring, uint32_t n_batches, double timeout_s, double ready_timeout_s) {
+  STALE_PROBE();
   RowsRing *rg = (RowsRing *)ring;
+  if (!(ready_timeout_s > 0.0) || ready_timeout_s > 600.0)
+    return fail(PGM_EINVAL, "rows_ring_start_ready: ready timeout must be in (0, 600] s");
+  if (rg) __atomic_store_n(&rg->ctl[3], 0u, __ATOMIC_SEQ_CST);
+  const int st = ring_start(rg, n_batches, timeout_s, 1);
+  if (st != PGM_OK || n_batches == 0) return st;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&rg->ctl[3], __ATOMIC_ACQUIRE) == 0u) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > ready_timeout_s) {
+      (void)pgm_rows_ring_cancel(ring);
+      return fail(PGM_EDEVICE, "rows_ring_start_ready: the resident grid did not come up within %.3g s",
+                  ready_timeout_s);
+    }
+  }
+  return PGM_OK;
+}
+
+static int ring_start(RowsRing *rg, uint32_t n_batches, double timeout_s, int signal) {
   if (!rg) return fail(PGM_EINVAL, "rows_ring_start: null ring");
   if (rg->running) return fail(PGM_EINVAL, "rows_ring_start: the ring is running (finish or cancel it first)");
   if (!(timeout_s > 0.0) || timeout_s > 600.0) return fail(PGM_EINVAL, "rows_ring_start: timeout must be in (0, 600] s");
@@ -4330,8 +4378,9 @@ int pgm_rows_ring_start(void *ring, uint32_t n_batches, double timeout_s) {
   long long n = rg->n_rows;
   int32_t *ef = rg->err;
   int32_t md = rg->mode;
-  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, (void *)&gc, &nb, &base, &n, (void *)&ef, &md, &ticks};
-  if (rg->reset_gctl) {  // mirror = base, token free, stop clear
+  int sg = signal;
+  void *args[] = {(void *)&v, (void *)&d, &ns, (void *)&ctl, (void *)&gc, &nb, &base, &n, (void *)&ef, &md, &ticks, &sg};
+  if (rg->reset_gctl) {  // mirror = base, token free, stop clear, readiness count 0
     unsigned init[16] = {base, 0u, 0u};
     HIP_TRY(hipMemcpyAsync(rg->gctl, init, sizeof init, hipMemcpyHostToDevice, rg->stream));
     HIP_TRY(hipStreamSynchronize(rg->stream));

@@ -707,9 +707,15 @@ class RowRing:
         self.outs = outs
         self.n_rows = int(n_rows)
 
-    def start(self, n_batches, timeout_s=5.0):
+    def start(self, n_batches, timeout_s=5.0, wait_ready=False):
+        """Launch for n_batches batches; wait_ready=True returns only once every workgroup of the
+        resident grid is running (pgm_rows_ring_start_ready)."""
         base = int(self._counter[0])  # the launch's base: batches posted over the ring's lifetime
-        N.check(self._start(self._h, int(n_batches), float(timeout_s)), "rows_ring_start")
+        if wait_ready:
+            N.check(N.lib().pgm_rows_ring_start_ready(self._h, int(n_batches), float(timeout_s), float(timeout_s)),
+                    "rows_ring_start_ready")
+        else:
+            N.check(self._start(self._h, int(n_batches), float(timeout_s)), "rows_ring_start")
         self._base = base
         self._n = int(n_batches)
         self._posted = 0

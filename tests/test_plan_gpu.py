@@ -196,6 +196,19 @@ def test_row_ring_matches_bound_launches(gpu, rows, n_batches):
         for s in range(3):
             slots[s][3]["marg"].fill_(-1.0)
         torch.cuda.synchronize()
+    # started resident first (every workgroup running before the first post), twice: the readiness
+    # count carries over launches without a reset
+    for _ in range(2):
+        ring.start(n_batches, wait_ready=True)
+        for b in range(1, n_batches + 1):
+            ring.post(b)
+        ring.finish()
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        for s in range(3):
+            assert torch.equal(slots[s][3]["marg"], refs[s]["marg"]), s
+            slots[s][3]["marg"].fill_(-1.0)
+        torch.cuda.synchronize()
     ring.start(2)
     ring.post(1)
     with pytest.raises(ValueError):
