@@ -13,8 +13,10 @@ from . import _native as N
 from . import engine as E
 
 
-BATCH_MAX_WORK = 1 << 22  # index-space size (outputs x reduction) up to which a step joins a batch
-BATCH_SPLIT_WORK = 1 << 16  # a step the planner would split (few outputs, long reduction) joins only this small
+# index-space size (outputs x reduction) up to which a step joins a batch (knob PGM_BATCH_MAX_WORK)
+BATCH_MAX_WORK = int(os.environ.get("PGM_BATCH_MAX_WORK", 1 << 22))
+# a step the planner would split (few outputs, long reduction) joins only this small (PGM_BATCH_SPLIT_WORK)
+BATCH_SPLIT_WORK = int(os.environ.get("PGM_BATCH_SPLIT_WORK", 1 << 16))
 # outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
 # their own row-mode launch (16-B two-rows-per-lane).  Tuning knob: PGM_PRODN_BATCH_MAX.
 PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
