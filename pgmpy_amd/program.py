@@ -17,6 +17,10 @@ from . import engine as E
 BATCH_MAX_WORK = int(os.environ.get("PGM_BATCH_MAX_WORK", 1 << 22))
 # a step the planner would split (few outputs, long reduction) joins only this small (PGM_BATCH_SPLIT_WORK)
 BATCH_SPLIT_WORK = int(os.environ.get("PGM_BATCH_SPLIT_WORK", 1 << 16))
+# the same for a plain Program's batches (the levels of a contraction path, C1 / C2): a split step costs two
+# launches (partials + final) at ~4.5 us each, more than the unsplit job takes inside the level's batch — C2
+# 0.218 -> 0.204 ms/query (profiles/r03w/)
+PLAIN_SPLIT_WORK = int(os.environ.get("PGM_PLAIN_SPLIT_WORK", 1 << 22))
 # outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
 # their own row-mode launch (16-B two-rows-per-lane).  Tuning knob: PGM_PRODN_BATCH_MAX.
 PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
@@ -369,7 +373,7 @@ class Program:
                        [A, B], [out, ws], job, pm=pm)
             return out
         w = _work(d) if self._batch is not None else 0
-        if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
+        if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else PLAIN_SPLIT_WORK):
             self._batch.jobs.append(("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)),
                                      (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)))
             return out
