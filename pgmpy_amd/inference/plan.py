@@ -470,7 +470,18 @@ class PatternPlan:
             # no evidence touches this pattern: broadcast one result over the rows
             ops.append((E.to_device(np.ones(n)), [E.ROW]))
         R = contract_factors(ops, outl, prog=prog)  # [Q..., ROW] C-order
+        # normalisation in two launches whatever the number of query variables: the row masses Z and
+        # every variable's unnormalised marginal (all read only R) as one batch, then every division as
+        # one batch (before: 1 + 2 V dependent launches of ~4.5 us each).  A single query variable's
+        # marginal is R itself (same labels, same layout), not a copy of it.
+        prog.begin_batch()
         Z = prog.contract(R, outl, None, None, [E.ROW], reduce="sum", combine="copy")
+        ms = []
+        if "marg" in outs:
+            for v in self.variables:
+                ms.append(R if len(self.variables) == 1 else
+                          prog.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy"))
+        prog.end_batch()
         bufs = {}
 
         def out_buf(key, shape):
@@ -479,20 +490,21 @@ class PatternPlan:
                 return host[key].tensor
             return E.empty(list(shape))
 
+        prog.begin_batch()
         if "marg" in outs:
             bufs["marg"] = out_buf("marg", [self.n_acc, n])
             for i, v in enumerate(self.variables):
                 a = self.acc_off[i]
-                m = prog.contract(R, outl, None, None, [v, E.ROW], reduce="sum", combine="copy")
-                prog.contract(m, [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw",
+                prog.contract(ms[i], [v, E.ROW], Z, [E.ROW], [v, E.ROW], combine="div_raw",
                               out=bufs["marg"][a:a + self.cards[i]])
-        if "map" in outs:
-            bufs["map"] = torch.empty(n, dtype=torch.int32, device=dev)
-            prog.argmax(R, n, self.P, 1, n, bufs["map"])
         if "joint" in outs:
             bufs["joint"] = out_buf("joint", [self.P, n])
             prog.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw",
                           out=bufs["joint"])
+        prog.end_batch()
+        if "map" in outs:
+            bufs["map"] = torch.empty(n, dtype=torch.int32, device=dev)
+            prog.argmax(R, n, self.P, 1, n, bufs["map"])
         prog.capture()
         cols_dev = torch.tensor([self.col_of[v] for v in cols], dtype=torch.int32, device=dev) if cols else None
         hit = (prog, codes_buf, perr, bufs, cols_dev, host)
