@@ -88,6 +88,7 @@ class Program:
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
         self._chains = []  # levelled batch handles (several dependency levels in one launch)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
+        self.merged_parts = {}  # step index -> full notes of the specialised steps merged into it
 
     # ------------------------------------------------------------------ batching
     def begin_batch(self):
@@ -341,6 +342,7 @@ class Program:
                 continue
             self._pm_bound.append(m)
             self._pm_launch.append(m)
+            self.merged_parts[len(self._steps)] = [r.note for r in part]
             self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
             self.step_bytes.append(sum(r.nbytes for r in part))
