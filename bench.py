@@ -317,6 +317,35 @@ def dispatch_floor_ms(plan, d_codes, rows, args, launcher_cls):
     return res[0], res[1]
 
 
+def ring_launch_roofline(plan, d_codes, outs, rows, err, n_batches=400):
+    """The same batches through ONE launch (the resident ring, pgm_rows_ring_*: batch b = the rows and
+    output buffers of resident batch b % len(outs)), after the timed region: the per-launch roofline of a
+    single kernel instance — its duration from HIP events on its stream around the launch (start,
+    posting of all n_batches, completion), which a rocprofv3 kernel trace of the same command reports as
+    one `pgm_rows_ring` dispatch.  achieved = n_batches x the batch's algorithmic bytes / that duration."""
+    import torch
+
+    nb = len(outs)
+    ring = plan.ring([(d_codes, rows * nb, i * rows, outs[i]) for i in range(nb)], rows, err=err)
+    kname, k_blocks, k_wg = ring.kernel()
+    ring.run(n_batches)  # warm, same size (so a rocprofv3 --stats average over both dispatches is the
+    torch.cuda.synchronize()  # timed one's duration): the kernel's first-use load, every slot touched
+    timer = HipTimer()
+    timer.start()
+    ring.run(n_batches)
+    timer.mark_end()
+    torch.cuda.synchronize()
+    ms = timer.elapsed_ms()
+    assert int(err.item()) == 0
+    del ring
+    nbytes = plan.algorithmic_bytes_per_row(marginals=True) * rows * n_batches
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": kname, "grid": {"blocks": k_blocks, "workgroup": k_wg}, "batches": n_batches,
+            "rows_per_batch": rows, "launches": 1, "kernel_ms": ms, "ms_per_batch": ms / n_batches,
+            "bytes_per_launch": nbytes, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+            "working_set_exceeds_mall": plan.algorithmic_bytes_per_row(marginals=True) * rows * nb > MALL_BYTES}
+
+
 def hbm_stream_roofline(plan, d_codes, rows, nb, args, err, qs, n_out=24, steps=200):
     """The C3 launch streamed over n_out distinct output buffers (n_out x 13.6 MB > the 256 MiB MALL, so
     the outputs of a step are evicted to HBM before the buffer comes round again) on args.queues
@@ -560,6 +589,12 @@ def bench_c3(args, dist, rank, world):
     stream = None
     if args.launch == "direct" and working_set <= MALL_BYTES:
         stream = hbm_stream_roofline(plan, d_codes, rows, nb, args, err, launcher.qs)
+    ring_roof = None
+    if not args.no_ring_roofline:
+        try:
+            ring_roof = ring_launch_roofline(plan, d_codes, outs, rows, err)
+        except Exception as e:  # reported, never silently dropped; the headline above stands on its own
+            ring_roof = {"error": f"{type(e).__name__}: {e}"}
     kname, k_blocks, k_wg = bounds[0].kernel()  # the kernel the bound launches run
     kname = kname or plan.kernel_name()
     traffic, traffic_rows = load_traffic(kname)
@@ -637,6 +672,10 @@ def bench_c3(args, dist, rank, world):
             "working_set_bytes": working_set,
             "working_set_exceeds_mall": working_set > MALL_BYTES,
             "hbm_stream": stream,
+            # per-launch roofline of ONE kernel instance over the same batches (resident ring, 400
+            # batches, after the timed region): a duration a rocprofv3 kernel trace reproduces directly
+            # (one dispatch), unlike the overlapped four-queue span above
+            "single_launch_ring": ring_roof,
         },
     }
     if rank == 0:
@@ -1148,6 +1187,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
+    ap.add_argument("--no-ring-roofline", action="store_true",
+                    help="c3: skip the single-launch (resident ring) roofline after the timed region")
     ap.add_argument("--release-mode", default="barrier", choices=["launch", "barrier"],
                     help="c3 direct: the window's system-scope release on the last launch per queue (launch) or as "
                          "one barrier packet per queue appended together (barrier)")

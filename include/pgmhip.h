@@ -417,6 +417,23 @@ int pgm_rows_bound_destroy(void *bound);
  * per thread, 16-B stores), "pgm_rows_floor" / "pgm_rows_floor2" (PGM_ROWS_FLOOR), or "" (an AOT kernel), with its grid and workgroup size */
 int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks, uint32_t *wg);
 
+/* Rows sharded over several GPUs from host buffers: the data-parallel axis of predict /
+ * predict_probability (pgmpy/models/DiscreteBayesianNetwork.py:867-910, 912-989) split into n_shards
+ * contiguous row blocks (shard i = rows [i n / S, (i + 1) n / S), as pgmpy_amd.distributed.shard_bounds),
+ * shard i run by handles[i] on the HIP device that was current when that handle was created
+ * (pgm_rows_plan_create once per device; the handles must describe the same plan).  One host thread per
+ * shard: the shard's rows of evidence columns [0, n_cols) in (host_codes column-major uint8, leading dim
+ * ld_codes, the plan's column numbering), the plan's pass, its outputs out to the caller's host arrays at
+ * the shard's columns — the gather of every shard's result is that copy.  mode: PGM_ROWS_MARGINALS
+ * (host_marg [n_marg][ld_out] f64) and / or PGM_ROWS_MAP (host_map [n_rows] int32).  *err_any is ORed
+ * with the kernels' evidence-error flag (PGM_ROWS error semantics of pgm_rows_plan_run).  Returns when
+ * every shard is done; the first failing shard's status otherwise.  Outputs equal one
+ * pgm_rows_plan_run over all rows bit for bit.  (the multi-GPU entry a non-Python
+ * FFI caller uses; the Python path shards with torch.distributed, pgmpy_amd/distributed.py.) */
+int pgm_rows_shard_run(void *const *handles, int32_t n_shards, int32_t mode, const uint8_t *host_codes,
+                       int64_t ld_codes, int64_t n_cols, int64_t n_rows, double *host_marg, int64_t ld_out,
+                       int32_t *host_map, int32_t *err_any);
+
 /* Host-side scan for evidence ingestion (no device needed): out[j] = 1 when any of the n int8 cells of
  * column cols[j] is negative (a pandas Categorical NaN code), else 0; up to `threads` host threads.
  * Finds the NaN-holding columns of a categorical frame in one native pass, so rows are grouped by

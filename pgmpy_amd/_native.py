@@ -206,6 +206,8 @@ _SIGS = {
     "pgm_rows_bound_destroy": ([_P], ctypes.c_int),
     "pgm_rows_bound_kernel": ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                                ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "pgm_rows_shard_run": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.c_int64, _P, ctypes.c_int64, _P, _P], ctypes.c_int),
     "pgm_host_any_negative_i8": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32], ctypes.c_int),
     "pgm_rows_ring_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64),
                               ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.POINTER(_P), ctypes.c_int64,

@@ -35,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 16  // 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 17  // 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -1889,6 +1889,8 @@ struct RowsHandle {
   hipFunction_t jit_fn_ring = nullptr;    // the resident ring kernel (pgm_rows_ring_*)
   std::vector<char> jit_code;         // the compiled code object (the direct AQL path loads it again)
   bool jit_write_through = false;     // its output stores are write-through (jit_store() == 2)
+  int device = 0;                     // the HIP device current at create (its buffers / module live there)
+  int n_cols = 0;                     // 1 + the largest evidence column the plan reads (0: none)
 };
 
 template <bool VL, bool AL, int MAXFC, int MAXT>
@@ -3968,6 +3970,8 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   h->all_affine = !any_table && max_nf <= 4 && max_nt <= 8;
   h->d_values = nullptr;
   h->d_desc = nullptr;
+  (void)hipGetDevice(&h->device);
+  for (int j = 0; j < pl->n_ev; ++j) h->n_cols = std::max(h->n_cols, pl->ev_col[j] + 1);
   if (!any_table) {
     h->jit_src = rows_jit_source(pl);
     h->jit_write_through = jit_store() == 2;
@@ -4227,6 +4231,112 @@ int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks,
 int pgm_rows_bound_destroy(void *bound) {
   STALE_PROBE();
   delete (RowsBound *)bound;
+  return PGM_OK;
+}
+
+// ---------------------------------------------------------------------------- rows sharded over GPUs
+// One shard of pgm_rows_shard_run on its plan's device: its rows' evidence columns in, the plan's pass,
+// its outputs out to the caller's host arrays at the shard's columns.  Runs on its own host thread.
+static int rows_shard_one(RowsHandle *h, int32_t mode, const uint8_t *host_codes, int64_t ld_codes, int64_t n_cols,
+                          int64_t r0, int64_t nr, double *host_marg, int64_t ld_out, int32_t *host_map,
+                          int32_t *err_any) {
+  HIP_TRY(hipSetDevice(h->device));
+  hipStream_t s = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  // device layout of the shard: codes [n_cols][ldc], marg [n_marg][ldc], map [ldc], err; ldc even and
+  // 16-B aligned columns so the two-rows-per-lane kernel takes the shard
+  const int64_t ldc = (nr + 15) & ~(int64_t)15;
+  const bool want_m = (mode & PGM_ROWS_MARGINALS) != 0, want_p = (mode & PGM_ROWS_MAP) != 0;
+  const size_t b_codes = (size_t)std::max<int64_t>(n_cols, 1) * ldc;
+  const size_t o_marg = (b_codes + 255) & ~(size_t)255;
+  const size_t b_marg = want_m ? (size_t)h->k.n_marg * ldc * sizeof(double) : 0;
+  const size_t o_map = o_marg + ((b_marg + 255) & ~(size_t)255);
+  const size_t b_map = want_p ? (size_t)ldc * sizeof(int32_t) : 0;
+  const size_t o_err = o_map + ((b_map + 255) & ~(size_t)255);
+  char *d = nullptr;
+  hipError_t e = hipMalloc((void **)&d, o_err + 256);
+  int st = PGM_OK;
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamDestroy(s);
+    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_shard_run: %s", hipGetErrorString(e));
+  }
+  uint8_t *d_codes = (uint8_t *)d;
+  double *d_marg = want_m ? (double *)(d + o_marg) : nullptr;
+  int32_t *d_map = want_p ? (int32_t *)(d + o_map) : nullptr;
+  int32_t *d_err = (int32_t *)(d + o_err);
+  int32_t h_err = 0;
+  e = hipMemsetAsync(d_err, 0, sizeof(int32_t), s);
+  if (e == hipSuccess && n_cols > 0)  // rows [r0, r0 + nr) of every column the plan may read
+    e = hipMemcpy2DAsync(d_codes, (size_t)ldc, host_codes + r0, (size_t)ld_codes, (size_t)nr, (size_t)n_cols,
+                         hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    st = rows_plan_run(h, mode, d_codes, ldc, 0, nr, d_marg, nullptr, ldc, d_map, nullptr, d_err, s, false);
+    if (st == PGM_OK && want_m)
+      e = hipMemcpy2DAsync(host_marg + r0, (size_t)ld_out * sizeof(double), d_marg, (size_t)ldc * sizeof(double),
+                           (size_t)nr * sizeof(double), (size_t)h->k.n_marg, hipMemcpyDeviceToHost, s);
+    if (st == PGM_OK && e == hipSuccess && want_p)
+      e = hipMemcpyAsync(host_map + r0, d_map, (size_t)nr * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (st == PGM_OK && e == hipSuccess)
+      e = hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+  }
+  const hipError_t es = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = es;
+  (void)hipFree(d);
+  (void)hipStreamDestroy(s);
+  if (st != PGM_OK) return st;
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(PGM_EDEVICE, "rows_shard_run: %s", hipGetErrorString(e));
+  }
+  if (h_err && err_any) __atomic_fetch_or(err_any, h_err, __ATOMIC_RELAXED);
+  return PGM_OK;
+}
+
+int pgm_rows_shard_run(void *const *handles, int32_t n_shards, int32_t mode, const uint8_t *host_codes,
+                       int64_t ld_codes, int64_t n_cols, int64_t n_rows, double *host_marg, int64_t ld_out,
+                       int32_t *host_map, int32_t *err_any) {
+  STALE_PROBE();
+  if (!handles || n_shards < 1) return fail(PGM_EINVAL, "rows_shard_run: no plan handles");
+  if (n_rows < 0 || ld_codes < n_rows || n_cols < 0) return fail(PGM_EINVAL, "rows_shard_run: bad shape");
+  if (mode & ~(PGM_ROWS_MARGINALS | PGM_ROWS_MAP))
+    return fail(PGM_EINVAL, "rows_shard_run: mode takes PGM_ROWS_MARGINALS | PGM_ROWS_MAP only");
+  if (!(mode & (PGM_ROWS_MARGINALS | PGM_ROWS_MAP))) return fail(PGM_EINVAL, "rows_shard_run: no output requested");
+  if ((mode & PGM_ROWS_MARGINALS) && (!host_marg || ld_out < n_rows))
+    return fail(PGM_EINVAL, "rows_shard_run: marginals need host_marg with ld_out >= n_rows");
+  if ((mode & PGM_ROWS_MAP) && !host_map) return fail(PGM_EINVAL, "rows_shard_run: MAP needs host_map");
+  int32_t n_marg = -1;
+  for (int32_t i = 0; i < n_shards; ++i) {
+    const RowsHandle *h = (const RowsHandle *)handles[i];
+    if (!h) return fail(PGM_EINVAL, "rows_shard_run: null handle %d", i);
+    if (h->n_cols > n_cols) return fail(PGM_EINVAL, "rows_shard_run: plan %d reads column %d of %lld", i, h->n_cols - 1,
+                                        (long long)n_cols);
+    if (n_marg >= 0 && h->k.n_marg != n_marg) return fail(PGM_EINVAL, "rows_shard_run: plans differ (marginal rows)");
+    n_marg = h->k.n_marg;
+  }
+  if (n_rows == 0) return PGM_OK;
+  if (n_cols > 0 && !host_codes) return fail(PGM_EINVAL, "rows_shard_run: null codes");
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  // contiguous shards (distributed.shard_bounds): shard i = rows [i n / S, (i + 1) n / S)
+  std::vector<int> st(n_shards, PGM_OK);
+  std::vector<std::string> msg(n_shards);
+  std::vector<std::thread> th;
+  th.reserve(n_shards);
+  for (int32_t i = 0; i < n_shards; ++i) {
+    const int64_t a = n_rows * i / n_shards, b = n_rows * (i + 1) / n_shards;
+    th.emplace_back([&, i, a, b] {
+      if (b > a) {
+        st[i] = rows_shard_one((RowsHandle *)handles[i], mode, host_codes, ld_codes, n_cols, a, b - a, host_marg,
+                               ld_out, host_map, err_any);
+        if (st[i] != PGM_OK) msg[i] = g_err;  // the worker's thread-local message
+      }
+    });
+  }
+  for (auto &t : th) t.join();
+  (void)hipSetDevice(prev);
+  for (int32_t i = 0; i < n_shards; ++i)
+    if (st[i] != PGM_OK) return fail(st[i], "rows_shard_run: shard %d: %s", i, msg[i].c_str());
   return PGM_OK;
 }
 

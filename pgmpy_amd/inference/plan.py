@@ -252,6 +252,42 @@ class PatternPlan:
                         self._handle_joint = h
                     self._handle = h
 
+    def shard_run(self, codes, devices, marginals=True, map_=False):
+        """This fused plan over host rows sharded across GPUs through the C-ABI (pgm_rows_shard_run):
+        codes = host uint8 [columns, n_rows] in this plan's column numbering (col_of), devices = the
+        HIP device of each shard (contiguous row blocks, shard i on devices[i]; one plan handle per
+        shard, created on its device and cached).  Returns {"marg": [n_acc, n_rows] f64, "map": [n_rows]
+        int32} as numpy arrays, equal to run() over all rows.  The native path a non-Python caller uses
+        (include/pgmhip.h); pgmpy_amd.distributed shards over processes instead."""
+        if self.kind != "fused":
+            raise ValueError("shard_run(): fused plans only")
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        n_cols, n_rows = codes.shape
+        L = N.lib()
+        cache = self.__dict__.setdefault("_shard_handles", {})
+        handles = []
+        for i, d in enumerate(devices):
+            key = (i, int(d))
+            if key not in cache:
+                N.check(L.pgm_set_device(int(d)), "set_device")
+                try:
+                    cache[key] = self._make_rows_plan(split=True)[0]
+                finally:
+                    N.check(L.pgm_set_device(E.device().index or 0), "set_device")
+            handles.append(cache[key])
+        mode = (N.ROWS_MARGINALS if marginals else 0) | (N.ROWS_MAP if map_ else 0)
+        marg = np.empty((self.n_acc, n_rows), dtype=np.float64) if marginals else None
+        mp = np.empty(n_rows, dtype=np.int32) if map_ else None
+        err = np.zeros(1, dtype=np.int32)
+        arr = (ctypes.c_void_p * len(handles))(*[h.value for h in handles])
+        N.check(L.pgm_rows_shard_run(arr, len(handles), mode, codes.ctypes.data_as(ctypes.c_void_p), n_rows, n_cols,
+                                     n_rows, None if marg is None else marg.ctypes.data_as(ctypes.c_void_p), n_rows,
+                                     None if mp is None else mp.ctypes.data_as(ctypes.c_void_p),
+                                     err.ctypes.data_as(ctypes.c_void_p)), "rows_shard_run")
+        if err[0]:
+            raise IndexError("evidence state code out of range")
+        return {"marg": marg, "map": mp}
+
     def _joint_handle(self):
         if self._handle_joint is None:
             with self._lock:
@@ -260,7 +296,8 @@ class PatternPlan:
         return self._handle_joint
 
     def __del__(self):
-        hs = {id(h): h for h in (getattr(self, "_handle", None), getattr(self, "_handle_joint", None))
+        hs = {id(h): h for h in (getattr(self, "_handle", None), getattr(self, "_handle_joint", None),
+                                 *self.__dict__.get("_shard_handles", {}).values())
               if h is not None and h.value}
         for h in hs.values():
             try:

@@ -219,6 +219,34 @@ def test_row_ring_matches_bound_launches(gpu, rows, n_batches):
     ring.finish()
 
 
+@pytest.mark.parametrize("rows,n_shards", [(10_001, 3), (100_000, 2), (7, 4), (1, 1)])
+def test_rows_shard_run_matches_run(gpu, rows, n_shards):
+    """pgm_rows_shard_run (the C-ABI multi-GPU entry: host rows split into contiguous shards, one
+    plan handle + host thread per shard, outputs copied back into the caller's arrays) equals one
+    pgm_rows_plan_run over all rows bit for bit — marginals and MAP indices — with the shards on the
+    box's GPUs (round robin; several shards share a GPU on a one-GPU box); more shards than rows leave
+    empty shards; an out-of-range evidence code raises like run()."""
+    import torch
+
+    from pgmpy_amd.inference.batch import download, upload_codes
+
+    plan, ev = _munin_template(rows, seed=23)
+    ref = plan.alloc_outputs(rows, marginals=True, map_=True)
+    plan.run(upload_codes(ev), rows, 0, rows, ref)
+    torch.cuda.synchronize()
+    n_dev = torch.cuda.device_count()
+    got = plan.shard_run(ev, [i % n_dev for i in range(n_shards)], marginals=True, map_=True)
+    assert np.array_equal(got["marg"], download(ref["marg"]), equal_nan=True)
+    assert np.array_equal(got["map"], download(ref["map"]))
+    only = plan.shard_run(ev, [i % n_dev for i in range(n_shards)], marginals=False, map_=True)
+    assert only["marg"] is None and np.array_equal(only["map"], got["map"])
+    col = plan.col_of[plan.ev_used[0]]
+    bad = ev.copy()
+    bad[col, rows // 2] = 200  # not a state of that variable, not the 255 "unobserved" code
+    with pytest.raises(IndexError):
+        plan.shard_run(bad, [i % n_dev for i in range(n_shards)])
+
+
 def test_row_ring_exits_without_posts(gpu):
     """Every exit path of the resident kernel ends the launch: cancel() with batches never posted,
     and the timeout (the waves give up waiting; finish() then reports the timeout)."""
