@@ -318,6 +318,18 @@ int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, 
  * that waits > 2 s (residency violated by another persistent kernel) gives up; pgm_batch_info then
  * reports timed_out = 1 (and resets the barrier).  One handle must not run on two streams at once. */
 int pgm_batch_add_level(void *handle);
+/* Single-workgroup levelled batch (set before finalize): run launches ONE workgroup that executes every
+ * level's blocks in order, one block after another, with a workgroup barrier between them (no grid
+ * barrier, no cache maintenance: producer and consumer are the same workgroup) — for chains of tiny
+ * dependent levels (the last levels of a contraction path down to the query marginal and its
+ * normalisation, ExactInference.py:404-421), whose one-launch-per-level cost is all launch latency.
+ * mode: PGM_BATCH_GRID (default: the persistent grid above) or PGM_BATCH_ONE_WORKGROUP, set before the
+ * first job (its contraction jobs are then planned to occupy as few blocks as their outputs allow). */
+enum { PGM_BATCH_GRID = 0, PGM_BATCH_ONE_WORKGROUP = 1 };
+int pgm_batch_set_mode(void *handle, int32_t mode);
+/* blocks (256-thread workgroups) the jobs added so far occupy; the levelled single-workgroup kernel
+ * runs them one after another, so callers keep it to levels of a few blocks */
+int pgm_batch_blocks(void *handle, int64_t *blocks);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
 /* levels, persistent grid (0: one launch per level), and (synchronising) whether a barrier timed out */

@@ -35,6 +35,7 @@ ROWS_MAX_EV = 48
 ROWS_MAX_COMP = 12
 ROWS_MAX_MARG = 192
 ROWS_MARGINALS, ROWS_JOINT, ROWS_MAP, ROWS_MAPGAP, ROWS_VALUES_GLOBAL = 1, 2, 4, 8, 16
+BATCH_GRID, BATCH_ONE_WORKGROUP = 0, 1  # pgm_batch_set_mode
 ROWS_ONE_GROUP, ROWS_GENERIC, ROWS_NO_JIT, ROWS_FLOOR = 32, 64, 128, 256
 
 
@@ -178,6 +179,8 @@ _SIGS = {
     "pgm_batch_add_product_n": ([_P, ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P], ctypes.c_int),
     "pgm_batch_add_indicator": ([_P, _P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P],
                                 ctypes.c_int),
+    "pgm_batch_set_mode": ([_P, ctypes.c_int32], ctypes.c_int),
+    "pgm_batch_blocks": ([_P, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "pgm_batch_add_level": ([_P], ctypes.c_int),
     "pgm_batch_finalize": ([_P], ctypes.c_int),
     "pgm_batch_run": ([_P, _P], ctypes.c_int),

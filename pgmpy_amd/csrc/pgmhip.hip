@@ -35,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 17  // 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 18  // 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -1374,6 +1374,22 @@ __global__ __launch_bounds__(256) void k_batch_levels(const BatchJob *__restrict
     const uint32_t e = level_off[l + 1];
     for (uint32_t b = level_off[l] + blockIdx.x; b < e; b += G) batch_block(jobs, block_job, b);
     if (l + 1 < n_levels && !grid_barrier(bar, G, deadline)) return;
+  }
+}
+
+// Several tiny dependent levels in ONE workgroup: each level's blocks run one after another on the same
+// 256 threads, a workgroup barrier after each (the block bodies may use LDS; the next level reads what
+// this workgroup wrote, which a workgroup-scope release/acquire makes visible).  Replaces one launch per
+// level for the last levels of a contraction path (C1 / C2), where every launch is latency only.
+__global__ __launch_bounds__(256) void k_batch_wg(const BatchJob *__restrict__ jobs,
+                                                  const uint32_t *__restrict__ block_job,
+                                                  const uint32_t *__restrict__ level_off, uint32_t n_levels) {
+  for (uint32_t l = 0; l < n_levels; ++l) {
+    const uint32_t e = level_off[l + 1];
+    for (uint32_t b = level_off[l]; b < e; ++b) {
+      batch_block(jobs, block_job, b);
+      __syncthreads();
+    }
   }
 }
 
@@ -3334,6 +3350,7 @@ struct BatchHandle {
   unsigned *d_bar = nullptr;  // grid barrier: arrivals, generation, timeout status
   unsigned grid = 0;          // persistent grid (levelled batch)
   unsigned long long timeout_ticks = 0;
+  int32_t mode = PGM_BATCH_GRID;  // PGM_BATCH_ONE_WORKGROUP: k_batch_wg
 };
 
 // workgroups of k_batch_levels that are resident at once (the grid barrier needs all of them),
@@ -3416,9 +3433,12 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   k.row_mode = 0;
   k.n_split = 1;
   k.red_chunk = k.n_ro;
+  // (a single-workgroup levelled batch runs its blocks one after another: spread a job over at most
+  // one block's lanes there)
+  const uint64_t lanes_cap = h->mode == PGM_BATCH_ONE_WORKGROUP ? 256 : 4096;
   int g = 0;
   if (d->reduce != PGM_RED_NONE && (uint64_t)k.n_ro * k.ri_card > 1)
-    while (g < 6 && ((uint64_t)k.n_out << g) < 4096 && (1u << (g + 1)) <= k.ri_card) ++g;
+    while (g < 6 && ((uint64_t)k.n_out << g) < lanes_cap && (1u << (g + 1)) <= k.ri_card) ++g;
   k.g_log2 = g;
   // output pairs with 16-B accesses when one lane per output is the choice anyway and every access
   // along the innermost kept dim is aligned and unit-stride (or broadcast)
@@ -3500,6 +3520,23 @@ int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, 
   return batch_append(h, J, (uint64_t)(n_rows * card));
 }
 
+int pgm_batch_set_mode(void *handle, int32_t mode) {
+  STALE_PROBE();
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h) return fail(PGM_EINVAL, "batch_set_mode: null handle");
+  if (h->d_jobs || !h->jobs.empty()) return fail(PGM_EINVAL, "batch_set_mode: set before the first job");
+  if (mode != PGM_BATCH_GRID && mode != PGM_BATCH_ONE_WORKGROUP) return fail(PGM_EINVAL, "batch_set_mode: mode %d", mode);
+  h->mode = mode;
+  return PGM_OK;
+}
+
+int pgm_batch_blocks(void *handle, int64_t *blocks) {
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !blocks) return fail(PGM_EINVAL, "batch_blocks: null argument");
+  *blocks = (int64_t)h->block_job.size();
+  return PGM_OK;
+}
+
 int pgm_batch_add_level(void *handle) {
   STALE_PROBE();
   BatchHandle *h = (BatchHandle *)handle;
@@ -3533,7 +3570,12 @@ int pgm_batch_finalize(void *handle) {
     e = hipMemcpy(h->d_jobs, h->jobs.data(), sizeof(BatchJob) * h->jobs.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipMemcpy(h->d_map, h->block_job.data(), sizeof(uint32_t) * h->block_job.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess && n_levels > 1) {
+  if (e == hipSuccess && h->mode == PGM_BATCH_ONE_WORKGROUP) {  // level table only, no grid barrier
+    e = hipMalloc((void **)&h->d_level, sizeof(uint32_t) * h->level_off.size());
+    if (e == hipSuccess)
+      e = hipMemcpy(h->d_level, h->level_off.data(), sizeof(uint32_t) * h->level_off.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  } else if (e == hipSuccess && n_levels > 1) {
     uint32_t widest = 0;
     for (size_t l = 0; l < n_levels; ++l) widest = std::max(widest, h->level_off[l + 1] - h->level_off[l]);
     h->grid = std::min(widest, batch_levels_cap());
@@ -3563,7 +3605,9 @@ int pgm_batch_run(void *handle, void *stream) {
   if (h->jobs.empty()) return PGM_OK;
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
   const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
-  if (n_levels > 1 && h->grid > 0) {
+  if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
+    hipLaunchKernelGGL(k_batch_wg, dim3(1), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level, n_levels);
+  } else if (n_levels > 1 && h->grid > 0) {
     hipLaunchKernelGGL(k_batch_levels, dim3(h->grid), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level,
                        n_levels, h->d_bar, h->timeout_ticks);
   } else if (n_levels > 1) {  // no occupancy figure: one launch per level, in order on the stream

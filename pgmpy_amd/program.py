@@ -33,6 +33,14 @@ PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 18))  # C4 1,000 ro
 # Measured slower on C2 (r03f: 0.58-1.69 ms/query against 0.27 with one launch per level; a grid barrier
 # with its agent-scope write-back / invalidate costs more than a kernel boundary), so off by default.
 LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
+# plain programs: consecutive dependency levels of at most this many 256-thread blocks each run in ONE
+# single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP: the levels' blocks one after another with a
+# workgroup barrier between them) instead of one launch each — the tail of a contraction path (C1 / C2:
+# the last levels down to the query marginal, then its normalisation).  Measured no faster (r03aa: C2
+# 0.215-0.221 ms/query with chains of <= 4-block levels against 0.208-0.210 without; C1 0.082-0.095 vs
+# 0.082-0.084): a tiny level's cost is its dependent load chain, not the launch, so it stays an A/B knob
+# (0 = off, the default; the test sets it).
+WG_CHAIN_BLOCKS = int(os.environ.get("PGM_WG_CHAIN_BLOCKS", 0))
 # n-ary products with more operands than one kernel takes: balanced tree (default) or sequential fold
 # (PGM_PRODN_TREE=0, A/B knob)
 TREE_PRODUCTS = os.environ.get("PGM_PRODN_TREE", "1") != "0"
@@ -125,6 +133,21 @@ class Program:
             else:
                 N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
 
+    def _batch_blocks(self, b):
+        """256-thread blocks the jobs of batch b occupy inside a single-workgroup levelled batch (planned
+        on a scratch handle in that mode)."""
+        L = N.lib()
+        h = ctypes.c_void_p()
+        N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
+        try:
+            N.check(L.pgm_batch_set_mode(h, N.BATCH_ONE_WORKGROUP), "batch_set_mode")
+            self._add_batch_jobs(h, b.jobs)
+            n = ctypes.c_int64()
+            N.check(L.pgm_batch_blocks(h, ctypes.byref(n)), "batch_blocks")
+            return int(n.value)
+        finally:
+            L.pgm_batch_destroy(h)
+
     def _batch_step(self, b):
         L = N.lib()
         if len(b.jobs) == 1:  # a batch of one is just the job (with its own planner's launch)
@@ -154,7 +177,33 @@ class Program:
             while j < n and isinstance(self._steps[j], _Batch):
                 j += 1
             group = self._steps[i:j]
-            if LEVEL_CHAIN and len(group) >= 2:
+            if WG_CHAIN_BLOCKS > 0 and not LEVEL_CHAIN and len(group) >= 2:
+                # runs of consecutive tiny levels (each at most WG_CHAIN_BLOCKS blocks) -> one
+                # single-workgroup launch; the other levels keep one launch each
+                blocks = [self._batch_blocks(b) for b in group]
+                k = 0
+                while k < len(group):
+                    e = k
+                    while e < len(group) and blocks[e] <= WG_CHAIN_BLOCKS:
+                        e += 1
+                    if e - k >= 2:
+                        h = self._new_batch()
+                        N.check(L.pgm_batch_set_mode(h, N.BATCH_ONE_WORKGROUP), "batch_set_mode")
+                        for m, b in enumerate(group[k:e]):
+                            if m:
+                                N.check(L.pgm_batch_add_level(h), "batch_add_level")
+                            self._add_batch_jobs(h, b.jobs)
+                        N.check(L.pgm_batch_finalize(h), "batch_finalize")
+                        steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+                        notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
+                                     f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
+                        k = e
+                        continue
+                    fn, note = self._batch_step(group[k])
+                    steps.append(fn)
+                    notes.append(note)
+                    k += 1
+            elif LEVEL_CHAIN and len(group) >= 2:
                 h = self._new_batch()
                 for k, b in enumerate(group):
                     if k:

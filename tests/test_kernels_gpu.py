@@ -696,6 +696,72 @@ def test_levelled_batch_chain_matches_numpy(gpu, monkeypatch):
     check()
 
 
+def test_single_workgroup_level_chain_matches_numpy(gpu, monkeypatch):
+    """A plain Program's consecutive tiny levels (batches of at most PGM_WG_CHAIN_BLOCKS blocks) run as
+    ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP / k_batch_wg): two interleaved chains
+    of dependent contractions, a wide level in the middle that keeps its own launch, a chain after it;
+    every level equals numpy, on repeated runs and through a captured HIP graph."""
+    import torch
+
+    import pgmpy_amd.program as P
+    from pgmpy_amd.program import Program
+
+    monkeypatch.setattr(P, "WG_CHAIN_BLOCKS", 4)  # off by default (no faster on C1 / C2), tested here
+    E = _e()
+    rng = np.random.default_rng(11)
+    n_a, n_b = 6, 5  # tiny levels before / after the wide one
+    xs = [rng.random((16, 8)) for _ in range(2)]
+    Ws = [[rng.random((16, 16)) / 8 for _ in range(n_a + 1 + n_b)] for _ in range(2)]
+    wide = rng.random((16, 4096)) / 16  # the wide level: [16, 8] x [16, 4096] -> 32 K outputs
+    prog = Program()
+    cur = [E.to_device(x) for x in xs]
+    outs, want = [], []
+    h = [x.copy() for x in xs]
+    for lv in range(n_a + 1 + n_b):
+        prog.begin_batch()
+        if lv == n_a:
+            nxt = [prog.contract(cur[c], ["a", "r"], E.to_device(wide), ["a", "w"], ["r", "w"], reduce="sum")
+                   for c in range(2)]
+            hn = [hh.T @ wide for hh in h]
+        else:
+            W = [E.to_device(Ws[c][lv]) for c in range(2)]
+            if lv == n_a + 1:  # back to [16, 8]: fold the wide axis
+                nxt = [prog.contract(cur[c], ["r", "w"], E.to_device(wide), ["a", "w"], ["a", "r"], reduce="sum")
+                       for c in range(2)]
+                hn = [wide @ hh.T for hh in h]
+            else:
+                nxt = [prog.contract(W[c], ["b", "a"], cur[c], ["a", "r"], ["b", "r"], reduce="sum") for c in range(2)]
+                hn = [Ws[c][lv] @ h[c] for c in range(2)]
+        prog.end_batch()
+        cur, h = nxt, hn
+        outs.append(cur)
+        want.append(h)
+    prog.run()
+    notes = list(prog.notes)
+    assert any("in one workgroup" in n for n in notes), notes
+    assert len(prog) < n_a + 1 + n_b, notes
+
+    def check():
+        torch.cuda.synchronize()
+        for lv in range(len(outs)):
+            for c in range(2):
+                np.testing.assert_allclose(E.to_host(outs[lv][c]), want[lv][c], rtol=1e-12)
+
+    check()
+    for o in outs:
+        for t in o:
+            t.zero_()
+    prog.run()
+    prog.run()
+    check()
+    prog.capture()
+    for o in outs:
+        for t in o:
+            t.zero_()
+    prog.run()
+    check()
+
+
 @pytest.mark.parametrize("operation", ["marginalize", "maximize"])
 def test_bp_levelled_schedule_matches_sequential(gpu, operation):
     """The levelled batched-BP schedule (one launch per dependency level for the small cliques)
