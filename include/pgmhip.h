@@ -58,6 +58,9 @@ int pgm_memset(void *dst, int value, size_t bytes, void *stream);
 int pgm_host_alloc(void **ptr, size_t bytes);
 int pgm_host_free(void *ptr);
 int pgm_stream_sync(void *stream);
+/* the same wait by polling (no blocking wait's wake-up latency; a host core spins meanwhile): the single
+ * query path (VariableElimination.query, ExactInference.py:246-440) waits for its one graph launch this way */
+int pgm_stream_sync_spin(void *stream);
 /* HIP events, for timing a kernel on the stream it runs on (bench.py) */
 int pgm_event_create(void **ev);
 int pgm_event_destroy(void *ev);

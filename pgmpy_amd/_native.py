@@ -145,6 +145,7 @@ _SIGS = {
     "pgm_memset": ([_P, ctypes.c_int, ctypes.c_size_t, _P], ctypes.c_int),
     "pgm_host_alloc": ([ctypes.POINTER(_P), ctypes.c_size_t], ctypes.c_int),
     "pgm_host_free": ([_P], ctypes.c_int),
+    "pgm_stream_sync_spin": ([_P], ctypes.c_int),
     "pgm_stream_sync": ([_P], ctypes.c_int),
     "pgm_event_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_event_destroy": ([_P], ctypes.c_int),

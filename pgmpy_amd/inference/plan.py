@@ -563,7 +563,7 @@ class PatternPlan:
                 host["codes"].array[:, 0] = [codes[i] for i in sel]
             s = N.stream_handle()
             prog.run()
-            N.check(L.pgm_stream_sync(s), "stream_sync")
+            N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
             return host[key].array.reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
