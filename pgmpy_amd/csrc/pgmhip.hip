@@ -168,18 +168,53 @@ __device__ __forceinline__ void contract_flat(const ContractK &p, const double *
       idx = q;
     }
     double acc = red_init<RED>();
-    for (uint32_t ro = r0; ro < r1; ++ro) {
-      int64_t ra, rb;
-      decode_ro(p, ro, ra, rb);
-      const double *a = A + oa + ra;
-      const double *b = B + ob + rb;
-      for (uint32_t ri = lane_g; ri < p.ri_card; ri += G) {
-        double v;
-        if constexpr (CMB == PGM_COMBINE_COPY)
-          v = a[(int64_t)ri * p.ri_sa];
-        else
-          v = combine<CMB>(a[(int64_t)ri * p.ri_sa], b[(int64_t)ri * p.ri_sb]);
-        acc = red_op<RED>(acc, v);
+    if (G == 1) {
+      // one lane per output: the reduction entries (reduction-outer major, innermost minor — the
+      // summation order of the loop below) UNR at a time, every operand load of a group issued before
+      // the group is summed, so a long reduction is not one memory round trip per entry (the entry
+      // walk is wave-uniform: scalar offsets and branches)
+      constexpr int UNR = 8;
+      const uint32_t total = (r1 > r0 ? r1 - r0 : 0u) * p.ri_card;
+      uint32_t ro = r0, ri = 0;
+      int64_t ra = 0, rb = 0;
+      if (total) decode_ro(p, ro, ra, rb);
+      for (uint32_t e = 0; e < total; e += UNR) {
+        double xa[UNR], xb[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (e + u < total) {
+            xa[u] = A[oa + ra + (int64_t)ri * p.ri_sa];
+            if constexpr (CMB != PGM_COMBINE_COPY) xb[u] = B[ob + rb + (int64_t)ri * p.ri_sb];
+            if (++ri == p.ri_card) {
+              ri = 0;
+              if (++ro < r1) decode_ro(p, ro, ra, rb);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (e + u < total) {
+            if constexpr (CMB == PGM_COMBINE_COPY)
+              acc = red_op<RED>(acc, xa[u]);
+            else
+              acc = red_op<RED>(acc, combine<CMB>(xa[u], xb[u]));
+          }
+        }
+      }
+    } else {
+      for (uint32_t ro = r0; ro < r1; ++ro) {
+        int64_t ra, rb;
+        decode_ro(p, ro, ra, rb);
+        const double *a = A + oa + ra;
+        const double *b = B + ob + rb;
+        for (uint32_t ri = lane_g; ri < p.ri_card; ri += G) {
+          double v;
+          if constexpr (CMB == PGM_COMBINE_COPY)
+            v = a[(int64_t)ri * p.ri_sa];
+          else
+            v = combine<CMB>(a[(int64_t)ri * p.ri_sa], b[(int64_t)ri * p.ri_sb]);
+          acc = red_op<RED>(acc, v);
+        }
       }
     }
     if constexpr (RED != PGM_RED_NONE) {
@@ -217,34 +252,49 @@ __device__ __forceinline__ void contract_flat2(const ContractK &p, const double 
       idx = qq;
     }
     double lo = red_init<RED>(), hi = red_init<RED>();
-    for (uint32_t ro = 0; ro < p.n_ro; ++ro) {
-      int64_t ra, rb;
-      decode_ro(p, ro, ra, rb);
-      const double *a = A + oa + ra;
-      const double *b = B + ob + rb;
-      for (uint32_t ri = 0; ri < p.ri_card; ++ri) {
-        double xl, xh;
-        if (va) {
-          const double2 w = *(const double2 *)(a + (int64_t)ri * p.ri_sa);
-          xl = w.x;
-          xh = w.y;
-        } else {
-          xl = xh = a[(int64_t)ri * p.ri_sa];
-        }
-        if constexpr (CMB != PGM_COMBINE_COPY) {
-          double yl, yh;
-          if (vb) {
-            const double2 w = *(const double2 *)(b + (int64_t)ri * p.ri_sb);
-            yl = w.x;
-            yh = w.y;
+    // the reduction entries in order (reduction-outer major), UNR at a time with every load of a group
+    // issued before it is summed (see contract_flat)
+    constexpr int UNR = 4;
+    const uint32_t total = p.n_ro * p.ri_card;
+    uint32_t ro = 0, ri = 0;
+    int64_t ra = 0, rb = 0;
+    if (total) decode_ro(p, ro, ra, rb);
+    for (uint32_t e = 0; e < total; e += UNR) {
+      double2 xa[UNR], xb[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (e + u < total) {
+          const double *a = A + oa + ra + (int64_t)ri * p.ri_sa;
+          if (va) {
+            xa[u] = *(const double2 *)a;
           } else {
-            yl = yh = b[(int64_t)ri * p.ri_sb];
+            xa[u].x = xa[u].y = *a;
           }
-          xl = combine<CMB>(xl, yl);
-          xh = combine<CMB>(xh, yh);
+          if constexpr (CMB != PGM_COMBINE_COPY) {
+            const double *b = B + ob + rb + (int64_t)ri * p.ri_sb;
+            if (vb) {
+              xb[u] = *(const double2 *)b;
+            } else {
+              xb[u].x = xb[u].y = *b;
+            }
+          }
+          if (++ri == p.ri_card) {
+            ri = 0;
+            if (++ro < p.n_ro) decode_ro(p, ro, ra, rb);
+          }
         }
-        lo = red_op<RED>(lo, xl);
-        hi = red_op<RED>(hi, xh);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (e + u < total) {
+          double xl = xa[u].x, xh = xa[u].y;
+          if constexpr (CMB != PGM_COMBINE_COPY) {
+            xl = combine<CMB>(xl, xb[u].x);
+            xh = combine<CMB>(xh, xb[u].y);
+          }
+          lo = red_op<RED>(lo, xl);
+          hi = red_op<RED>(hi, xh);
+        }
       }
     }
     *(double2 *)(C + oc) = make_double2(lo, hi);

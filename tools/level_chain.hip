@@ -126,6 +126,21 @@ static double run(int n_levels, int blocks, int reps) {
   CK(hipStreamSynchronize(s));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, a, b));
+  {  // host time of one hipGraphLaunch call on an idle stream, and launch -> completion
+    double h = 0, w = 0;
+    for (int i = 0; i < 20; ++i) {
+      auto t0 = std::chrono::steady_clock::now();
+      CK(hipGraphLaunch(ge, s));
+      auto t1 = std::chrono::steady_clock::now();
+      CK(hipStreamSynchronize(s));
+      auto t2 = std::chrono::steady_clock::now();
+      h += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      w += std::chrono::duration<double, std::micro>(t2 - t0).count();
+    }
+    if (DEPTH == 1 && blocks == 1)
+      printf("  one %d-node graph: hipGraphLaunch host %.1f us, launch -> synchronized %.1f us\n", n_levels, h / 20,
+             w / 20);
+  }
   CK(hipGraphExecDestroy(ge));
   CK(hipGraphDestroy(g));
   CK(hipStreamDestroy(s));
