@@ -1270,7 +1270,12 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   // target block count (tuning knob PGM_MARG_BLOCKS)
   static const uint64_t target = getenv("PGM_MARG_BLOCKS") ? strtoull(getenv("PGM_MARG_BLOCKS"), nullptr, 10) : 2048;
   const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, target / gy));
-  if (gx * gy < 512) return 0;  // too few blocks to fill the chip: the two-kernel path is faster
+  // too few blocks to fill the chip: the two-kernel path (product_n + contract) was faster for a lone
+  // launch below 512 blocks; inside a levelled schedule it costs a second dependency level, so the
+  // floor is a knob (PGM_MARG_MIN_BLOCKS)
+  static const uint64_t min_blocks = getenv("PGM_MARG_MIN_BLOCKS") ? strtoull(getenv("PGM_MARG_MIN_BLOCKS"), nullptr, 10)
+                                                                   : 512;
+  if (gx * gy < min_blocks) return 0;
   grid = dim3((unsigned)gx, (unsigned)gy, 1);
   return 1;
 }

@@ -56,6 +56,9 @@ class BatchedCalibration:
         return dict(self._marg)
 
 
+DIRECT_OPS = os.environ.get("PGM_BP_DIRECT_OPS", "1") != "0"
+
+
 def _aggregate(prog, small, clique_labels, scope_size):
     """Multiply the findings / messages entering a clique bottom-up over their scopes.
 
@@ -149,7 +152,13 @@ class BPSchedule:
             operands[c] = ops
             if c in parent:
                 sep = [v for v in ls if v in parent[c]]
-                bt, m, _ = prog.product_n_marginal(ops, ls + [R], sep + [R], reduce=red, store=False)
+                # the message from the findings / child messages themselves when the fused pass takes
+                # them all: the aggregates (distribute's operands) are then off collect's critical path
+                # (one dependency level less per clique whose inputs share a scope; PGM_BP_DIRECT_OPS=0: A/B)
+                mops = ops
+                if DIRECT_OPS and len(ops) - 1 < len(small) and 1 + len(small) <= 4:
+                    mops = [(t, ls)] + list(small)
+                bt, m, _ = prog.product_n_marginal(mops, ls + [R], sep + [R], reduce=red, store=False)
                 beliefs[c] = (bt, ls)  # the buffer distribute writes (the fallback path filled it already)
                 msgs[c] = (m, sep + [R])
             elif c in kids:
