@@ -1271,10 +1271,12 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   static const uint64_t target = getenv("PGM_MARG_BLOCKS") ? strtoull(getenv("PGM_MARG_BLOCKS"), nullptr, 10) : 2048;
   const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, target / gy));
   // too few blocks to fill the chip: the two-kernel path (product_n + contract) was faster for a lone
-  // launch below 512 blocks; inside a levelled schedule it costs a second dependency level, so the
-  // floor is a knob (PGM_MARG_MIN_BLOCKS)
+  // launch below 512 blocks, but inside a levelled schedule it costs a second dependency level.  C4
+  // (r03ae, two runs each): floor 512 / 256 / 128 / 64 -> 0.87-0.88 / 0.92 / 0.95 / 0.85 M
+  // calibrations/s at 1,000 rows, 1.20-1.21 / 1.25 / 1.24-1.25 / 1.24-1.25 M at 4,000.  Knob
+  // PGM_MARG_MIN_BLOCKS.
   static const uint64_t min_blocks = getenv("PGM_MARG_MIN_BLOCKS") ? strtoull(getenv("PGM_MARG_MIN_BLOCKS"), nullptr, 10)
-                                                                   : 512;
+                                                                   : 128;
   if (gx * gy < min_blocks) return 0;
   grid = dim3((unsigned)gx, (unsigned)gy, 1);
   return 1;
