@@ -618,7 +618,10 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // defaults measured on MI355X, pathfinder C4 (4,000 / 1,000 rows: generic 781K / 515K calibrations/s;
   // specialised above 2M entries 911K / 601K; + one row pair per lane, nontemporal belief stores and
   // XCD-grouped blocks 933K; threshold 256K entries 648K at 1,000 rows)
-  static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 18);
+  // r03ag, after the schedule changes (direct collect operands, 128-block fused floor): 2^18 / 2^16 / 2^14
+  // -> 0.96-0.97 / 1.024-1.026 / 1.026-1.028 M calibrations/s at 1,000 rows, 1.27-1.28 / 1.28-1.29 /
+  // 1.29 M at 4,000 (small steps specialised join their level's merged launch instead of launching alone)
+  static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 14);
   static const int xi_knob = pm_knob("PGM_PM_XI", 0);  // 0: per step (below); 1 / 2 / 4 / 8: forced
   // per step, at least this many row pairs per lane (1 / 2 / 4) when the rows fill them: 2 measured
   // (MI355X, C4 4,000 rows: 1.146 -> 1.18 M calibrations/s; 1,000 rows unchanged, too few rows;

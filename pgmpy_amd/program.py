@@ -27,7 +27,7 @@ PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
 # levelled programs: n-ary products / separator marginals at least this large (entries) become
 # specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
 # take or that are below the engine's own threshold, PGM_PM_JIT_MIN)
-PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 18))  # C4 1,000 rows: 745K -> 856K
+PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 14))  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
 # consecutive dependency levels made only of batch jobs run as ONE persistent launch with a grid barrier
 # between levels (pgm_batch_add_level) instead of one launch each.  A/B knob: PGM_BATCH_LEVELS=1.
 # Measured slower on C2 (r03f: 0.58-1.69 ms/query against 0.27 with one launch per level; a grid barrier
