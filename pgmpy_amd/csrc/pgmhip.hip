@@ -1276,9 +1276,10 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   // calibrations/s at 1,000 rows, 1.20-1.21 / 1.25 / 1.24-1.25 / 1.24-1.25 M at 4,000.  Knob
   // PGM_MARG_MIN_BLOCKS.  Once small steps are specialised and merged into their level's launch
   // (PGM_PM_JIT_MIN 2^14, r03ag) a small fused pass costs no launch of its own: floor 128 -> 32 gives
-  // 1.03 -> 1.09 M at 1,000 rows, 4,000 rows unchanged at 1.29-1.30 M (r03ah).
+  // 1.03 -> 1.09 M at 1,000 rows, 4,000 rows unchanged at 1.29-1.30 M (r03ah); 32 / 8 / 2 -> 1.08 / 1.08
+  // / 1.09-1.10 M (r03ai): no floor by default.
   static const uint64_t min_blocks = getenv("PGM_MARG_MIN_BLOCKS") ? strtoull(getenv("PGM_MARG_MIN_BLOCKS"), nullptr, 10)
-                                                                   : 32;
+                                                                   : 1;
   // (also accepting short reductions on 16+ blocks was slower at 1,000 rows, 0.95 -> 0.87 M: each such
   // pass is a launch of its own, where the two-kernel path's jobs join the level's batch launch; r03af)
   if (gx * gy < min_blocks) return 0;

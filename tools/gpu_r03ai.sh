@@ -1,7 +1,7 @@
 # round 3: C4 fused-pass block floor x specialised-step threshold, after r03ag
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-TAG=${1:-r03ah}
+TAG=${1:-r03ai}
 for R in 1 2; do
 for MB in 32 8 2; do
 for T in 16384; do
