@@ -43,6 +43,38 @@ def test_struct_layouts_match_header():
                                              + N.ROWS_MAX_FAC * (3 + N.ROWS_MAX_LOOP) + 3 * N.ROWS_MAX_EV)
 
 
+def test_argument_checks_before_any_device_call():
+    """Entry points of r03 reject bad arguments on the host, before any HIP call (no device here):
+    pgm_rows_shard_run (no handles, a null handle, a mode it does not take, no output),
+    pgm_batch_set_mode (an unknown mode) and pgm_batch_blocks (a null handle)."""
+    import ctypes
+
+    from pgmpy_amd import _native as N
+
+    lib = N.load_library()
+    h = (ctypes.c_void_p * 1)(None)
+    codes = np.zeros((1, 4), dtype=np.uint8)
+    marg = np.zeros((2, 4))
+    args = (codes.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(4), ctypes.c_int64(1), ctypes.c_int64(4),
+            marg.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(4), None, None)
+    shard = lib.pgm_rows_shard_run
+    shard.restype = ctypes.c_int
+    assert shard(h, ctypes.c_int32(0), ctypes.c_int32(N.ROWS_MARGINALS), *args) == N.PGM_EINVAL  # no handles
+    assert shard(h, ctypes.c_int32(1), ctypes.c_int32(N.ROWS_MARGINALS), *args) == N.PGM_EINVAL  # null handle
+    assert shard(h, ctypes.c_int32(1), ctypes.c_int32(N.ROWS_JOINT), *args) == N.PGM_EINVAL  # mode
+    assert shard(h, ctypes.c_int32(1), ctypes.c_int32(0), *args) == N.PGM_EINVAL  # no output
+    b = ctypes.c_void_p()
+    assert lib.pgm_batch_create(ctypes.byref(b)) == 0
+    try:
+        assert lib.pgm_batch_set_mode(b, ctypes.c_int32(7)) == N.PGM_EINVAL
+        assert lib.pgm_batch_set_mode(b, ctypes.c_int32(N.BATCH_ONE_WORKGROUP)) == 0
+        n = ctypes.c_int64(-1)
+        assert lib.pgm_batch_blocks(b, ctypes.byref(n)) == 0 and n.value == 0
+        assert lib.pgm_batch_blocks(None, ctypes.byref(n)) == N.PGM_EINVAL
+    finally:
+        lib.pgm_batch_destroy(b)
+
+
 def test_no_compute_without_gpu():
     import torch
 
