@@ -343,6 +343,8 @@ def ring_launch_roofline(plan, d_codes, outs, rows, err, n_batches=400):
     return {"kernel": kname, "grid": {"blocks": k_blocks, "workgroup": k_wg}, "batches": n_batches,
             "rows_per_batch": rows, "launches": 1, "kernel_ms": ms, "ms_per_batch": ms / n_batches,
             "bytes_per_launch": nbytes, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+            "slots": nb, "working_set_bytes": plan.algorithmic_bytes_per_row(marginals=True) * rows * nb,
+            "working_set_over_mall": plan.algorithmic_bytes_per_row(marginals=True) * rows * nb / MALL_BYTES,
             "working_set_exceeds_mall": plan.algorithmic_bytes_per_row(marginals=True) * rows * nb > MALL_BYTES}
 
 
@@ -530,7 +532,12 @@ def bench_c3(args, dist, rank, world):
     # outputs per batch without re-running the sampler)
     prng = np.random.default_rng(1000 + rank)
     perms = [np.arange(rows)] + [prng.permutation(rows) for _ in range(nb - 1)]
-    codes_ev = np.concatenate([codes_one[:, p] for p in perms], axis=1) if nb > 1 else codes_one  # [1038, rows * nb]
+    if nb > 1:  # [1038, rows * nb], filled in place (no list of copies: 96 batches are 10 GB)
+        codes_ev = np.empty((codes_one.shape[0], rows * nb), dtype=np.uint8)
+        for i, p in enumerate(perms):
+            codes_ev[:, i * rows:(i + 1) * rows] = codes_one[:, p]
+    else:
+        codes_ev = codes_one
     del codes_one
     col_of = {v: i for i, v in enumerate(observed)}
     log(f"[rank {rank}] sampled {rows} rows, {nb} batch(es), in {time.perf_counter() - t0:.1f}s")
@@ -670,6 +677,7 @@ def bench_c3(args, dist, rank, world):
             # before its buffer comes round again and the achieved rate is an HBM rate; with a set
             # that fits (--batches <= 17) hbm_stream repeats the measurement over 24 output buffers
             "working_set_bytes": working_set,
+            "working_set_over_mall": working_set / MALL_BYTES,
             "working_set_exceeds_mall": working_set > MALL_BYTES,
             "hbm_stream": stream,
             # per-launch roofline of ONE kernel instance over the same batches (resident ring, 400
@@ -815,6 +823,7 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
             "bytes_per_launch": bpr * rows * args.steps,
             "bytes_per_step": bpr * rows,
             "working_set_bytes": working_set,
+            "working_set_over_mall": working_set / MALL_BYTES,
             "working_set_exceeds_mall": working_set > MALL_BYTES,
         },
     }
@@ -1196,9 +1205,10 @@ def main():
                     help="c3 --launch ring: launch the resident kernel just before the timed window")
     ap.add_argument("--gather", action="store_true", help="c3: after timing, gather marginals to rank 0 (RCCL)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
-    ap.add_argument("--batches", type=int, default=24,
+    ap.add_argument("--batches", type=int, default=96,
                     help="c3: distinct resident row batches (each its own evidence columns and output), "
-                         "stepped round robin")
+                         "stepped round robin; 96 x 14.3 MB = 1.37 GB = 5.1x the 256 MiB Infinity Cache, so "
+                         "a batch's output lines are evicted to HBM long before its buffer comes round again")
     ap.add_argument("--group", type=int, default=1,
                     help="c3 direct launch: dispatch this many consecutive steps (distinct batches) as one "
                          "pgm_dq_launch_group (<= --batches)")

@@ -437,9 +437,14 @@ int pgm_rows_bound_kernel(void *bound, char *name, size_t cap, uint32_t *blocks,
  * contiguous row blocks (shard i = rows [i n / S, (i + 1) n / S), as pgmpy_amd.distributed.shard_bounds),
  * shard i run by handles[i] on the HIP device that was current when that handle was created
  * (pgm_rows_plan_create once per device; the handles must describe the same plan).  One host thread per
- * shard: the shard's rows of evidence columns [0, n_cols) in (host_codes column-major uint8, leading dim
- * ld_codes, the plan's column numbering), the plan's pass, its outputs out to the caller's host arrays at
- * the shard's columns — the gather of every shard's result is that copy.  mode: PGM_ROWS_MARGINALS
+ * shard: the shard's rows of the evidence columns the plan reads in (host_codes column-major uint8 with
+ * columns [0, n_cols), leading dim ld_codes, the plan's column numbering), the plan's pass, its outputs
+ * out to the caller's host arrays at the shard's columns — the gather of every shard's result is that
+ * copy, each GPU's over its own host link.  A shard runs in chunks of 256 K rows (PGM_SHARD_CHUNK)
+ * alternating between two streams and device buffers the handle keeps from its first call (no
+ * allocation after it), so a chunk's copy-in and pass overlap the previous chunk's copy-out when the host
+ * arrays are pinned (pgm_host_alloc); pageable arrays work and are staged by HIP.  One call at a time
+ * per handle.  mode: PGM_ROWS_MARGINALS
  * (host_marg [n_marg][ld_out] f64) and / or PGM_ROWS_MAP (host_map [n_rows] int32).  *err_any is ORed
  * with the kernels' evidence-error flag (PGM_ROWS error semantics of pgm_rows_plan_run).  Returns when
  * every shard is done; the first failing shard's status otherwise.  Outputs equal one

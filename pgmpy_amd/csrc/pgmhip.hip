@@ -1969,6 +1969,19 @@ struct RowsHandle {
   bool jit_write_through = false;     // its output stores are write-through (jit_store() == 2)
   int device = 0;                     // the HIP device current at create (its buffers / module live there)
   int n_cols = 0;                     // 1 + the largest evidence column the plan reads (0: none)
+  std::vector<int> cols;              // the evidence columns the plan reads, ascending
+  // pgm_rows_shard_run's resources on this handle's device, created on first use and kept until the
+  // handle is destroyed: two streams, each with its own grow-only device chunk buffer (codes of the
+  // columns the plan reads, outputs, error flag) and a pinned error word, so consecutive chunks
+  // alternate between them (chunk c + 1's copy-in and pass overlap chunk c's copy-out)
+  struct ShardSide {
+    hipStream_t s = nullptr;
+    char *buf = nullptr;
+    size_t cap = 0;
+    int32_t *h_err = nullptr;
+  };
+  ShardSide shard[2];
+  std::mutex shard_mu;  // one pgm_rows_shard_run shard at a time per handle
 };
 
 template <bool VL, bool AL, int MAXFC, int MAXT>
@@ -4089,6 +4102,9 @@ int pgm_rows_plan_create(const pgm_rows_plan *pl, const double *host_values, voi
   h->d_desc = nullptr;
   (void)hipGetDevice(&h->device);
   for (int j = 0; j < pl->n_ev; ++j) h->n_cols = std::max(h->n_cols, pl->ev_col[j] + 1);
+  for (int j = 0; j < pl->n_ev; ++j) h->cols.push_back(pl->ev_col[j]);
+  std::sort(h->cols.begin(), h->cols.end());
+  h->cols.erase(std::unique(h->cols.begin(), h->cols.end()), h->cols.end());
   if (!any_table) {
     h->jit_src = rows_jit_source(pl);
     h->jit_write_through = jit_store() == 2;
@@ -4138,6 +4154,16 @@ int pgm_rows_plan_destroy(void *handle) {
   STALE_PROBE();
   RowsHandle *h = (RowsHandle *)handle;
   if (!h) return PGM_OK;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (h->shard[0].s || h->shard[1].s) (void)hipSetDevice(h->device);
+  for (auto &sd : h->shard) {
+    if (sd.s) (void)hipStreamSynchronize(sd.s);
+    if (sd.buf) (void)hipFree(sd.buf);
+    if (sd.h_err) (void)hipHostFree(sd.h_err);
+    if (sd.s) (void)hipStreamDestroy(sd.s);
+  }
+  (void)hipSetDevice(prev);
   if (h->d_values) (void)hipFree(h->d_values);
   if (h->d_desc) (void)hipFree(h->d_desc);
   if (h->jit_mod) (void)hipModuleUnload(h->jit_mod);
@@ -4352,55 +4378,96 @@ int pgm_rows_bound_destroy(void *bound) {
 }
 
 // ---------------------------------------------------------------------------- rows sharded over GPUs
-// One shard of pgm_rows_shard_run on its plan's device: its rows' evidence columns in, the plan's pass,
-// its outputs out to the caller's host arrays at the shard's columns.  Runs on its own host thread.
-static int rows_shard_one(RowsHandle *h, int32_t mode, const uint8_t *host_codes, int64_t ld_codes, int64_t n_cols,
-                          int64_t r0, int64_t nr, double *host_marg, int64_t ld_out, int32_t *host_map,
-                          int32_t *err_any) {
+// One shard of pgm_rows_shard_run on its plan's device, on its own host thread: its rows in chunks of
+// at most shard_chunk_rows(), chunk c on side c % 2 of the handle's kept resources (stream + device
+// buffer): the chunk's rows of the columns the plan reads in (one copy per run of adjacent columns),
+// the plan's pass, its outputs out to the caller's host arrays at the chunk's columns.  Each side's
+// stream orders its own chunks, so chunk c + 2 reuses the buffer only after chunk c's copy-out; with
+// pinned host arrays (pgm_host_alloc / hipHostRegister) the two sides' DMA and kernels overlap.
+static int64_t shard_chunk_rows() {
+  static const int64_t v = [] {
+    const char *e = getenv("PGM_SHARD_CHUNK");
+    const long long x = e ? atoll(e) : 0;
+    return (int64_t)(x >= 16 ? x & ~15LL : 262144);  // 256 K rows: 36 MB of marginals per chunk
+  }();
+  return v;
+}
+
+static int shard_side_ready(RowsHandle::ShardSide &sd, size_t need) {
+  if (!sd.s) HIP_TRY(hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking));
+  if (!sd.h_err) HIP_TRY(hipHostMalloc((void **)&sd.h_err, 64, hipHostMallocDefault));
+  if (sd.cap < need) {
+    if (sd.buf) {
+      HIP_TRY(hipStreamSynchronize(sd.s));
+      (void)hipFree(sd.buf);
+      sd.buf = nullptr;
+      sd.cap = 0;
+    }
+    HIP_TRY(hipMalloc((void **)&sd.buf, need));
+    sd.cap = need;
+  }
+  return PGM_OK;
+}
+
+static int rows_shard_one(RowsHandle *h, int32_t mode, const uint8_t *host_codes, int64_t ld_codes, int64_t r0,
+                          int64_t nr, double *host_marg, int64_t ld_out, int32_t *host_map, int32_t *err_any) {
+  std::lock_guard<std::mutex> lk(h->shard_mu);
   HIP_TRY(hipSetDevice(h->device));
-  hipStream_t s = nullptr;
-  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  // device layout of the shard: codes [n_cols][ldc], marg [n_marg][ldc], map [ldc], err; ldc even and
-  // 16-B aligned columns so the two-rows-per-lane kernel takes the shard
-  const int64_t ldc = (nr + 15) & ~(int64_t)15;
+  const int64_t chunk = std::min<int64_t>(nr, shard_chunk_rows());
+  // device layout of a chunk: codes [h->n_cols][ldc] (only the plan's columns are written), marg
+  // [n_marg][ldc], map [ldc], err; ldc a multiple of 16 so the two-rows-per-lane kernel takes full chunks
+  const int64_t ldc = (chunk + 15) & ~(int64_t)15;
   const bool want_m = (mode & PGM_ROWS_MARGINALS) != 0, want_p = (mode & PGM_ROWS_MAP) != 0;
-  const size_t b_codes = (size_t)std::max<int64_t>(n_cols, 1) * ldc;
+  const size_t b_codes = (size_t)std::max(h->n_cols, 1) * ldc;
   const size_t o_marg = (b_codes + 255) & ~(size_t)255;
   const size_t b_marg = want_m ? (size_t)h->k.n_marg * ldc * sizeof(double) : 0;
   const size_t o_map = o_marg + ((b_marg + 255) & ~(size_t)255);
   const size_t b_map = want_p ? (size_t)ldc * sizeof(int32_t) : 0;
   const size_t o_err = o_map + ((b_map + 255) & ~(size_t)255);
-  char *d = nullptr;
-  hipError_t e = hipMalloc((void **)&d, o_err + 256);
+  const int n_sides = nr > chunk ? 2 : 1;
+  for (int i = 0; i < n_sides; ++i) {
+    const int st = shard_side_ready(h->shard[i], o_err + 256);
+    if (st != PGM_OK) return st;
+    h->shard[i].h_err[0] = 0;
+    HIP_TRY(hipMemsetAsync(h->shard[i].buf + o_err, 0, sizeof(int32_t), h->shard[i].s));
+  }
+  // runs of adjacent plan columns: one 2-D copy each
+  std::vector<std::pair<int, int>> runs;
+  for (int c : h->cols) {
+    if (!runs.empty() && runs.back().first + runs.back().second == c) ++runs.back().second;
+    else runs.push_back({c, 1});
+  }
   int st = PGM_OK;
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipStreamDestroy(s);
-    return fail(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "rows_shard_run: %s", hipGetErrorString(e));
-  }
-  uint8_t *d_codes = (uint8_t *)d;
-  double *d_marg = want_m ? (double *)(d + o_marg) : nullptr;
-  int32_t *d_map = want_p ? (int32_t *)(d + o_map) : nullptr;
-  int32_t *d_err = (int32_t *)(d + o_err);
-  int32_t h_err = 0;
-  e = hipMemsetAsync(d_err, 0, sizeof(int32_t), s);
-  if (e == hipSuccess && n_cols > 0)  // rows [r0, r0 + nr) of every column the plan may read
-    e = hipMemcpy2DAsync(d_codes, (size_t)ldc, host_codes + r0, (size_t)ld_codes, (size_t)nr, (size_t)n_cols,
-                         hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) {
-    st = rows_plan_run(h, mode, d_codes, ldc, 0, nr, d_marg, nullptr, ldc, d_map, nullptr, d_err, s, false);
+  hipError_t e = hipSuccess;
+  int64_t c = 0;
+  for (int64_t a = r0; a < r0 + nr && st == PGM_OK && e == hipSuccess; a += chunk, ++c) {
+    RowsHandle::ShardSide &sd = h->shard[c % n_sides];
+    const int64_t m = std::min(chunk, r0 + nr - a);
+    uint8_t *d_codes = (uint8_t *)sd.buf;
+    double *d_marg = want_m ? (double *)(sd.buf + o_marg) : nullptr;
+    int32_t *d_map = want_p ? (int32_t *)(sd.buf + o_map) : nullptr;
+    int32_t *d_err = (int32_t *)(sd.buf + o_err);
+    for (size_t k = 0; k < runs.size() && e == hipSuccess; ++k)
+      e = hipMemcpy2DAsync(d_codes + (size_t)runs[k].first * ldc, (size_t)ldc,
+                           host_codes + (size_t)runs[k].first * ld_codes + a, (size_t)ld_codes, (size_t)m,
+                           (size_t)runs[k].second, hipMemcpyHostToDevice, sd.s);
+    if (e != hipSuccess) break;
+    st = rows_plan_run(h, mode, d_codes, ldc, 0, m, d_marg, nullptr, ldc, d_map, nullptr, d_err, sd.s, false);
     if (st == PGM_OK && want_m)
-      e = hipMemcpy2DAsync(host_marg + r0, (size_t)ld_out * sizeof(double), d_marg, (size_t)ldc * sizeof(double),
-                           (size_t)nr * sizeof(double), (size_t)h->k.n_marg, hipMemcpyDeviceToHost, s);
+      e = hipMemcpy2DAsync(host_marg + a, (size_t)ld_out * sizeof(double), d_marg, (size_t)ldc * sizeof(double),
+                           (size_t)m * sizeof(double), (size_t)h->k.n_marg, hipMemcpyDeviceToHost, sd.s);
     if (st == PGM_OK && e == hipSuccess && want_p)
-      e = hipMemcpyAsync(host_map + r0, d_map, (size_t)nr * sizeof(int32_t), hipMemcpyDeviceToHost, s);
-    if (st == PGM_OK && e == hipSuccess)
-      e = hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+      e = hipMemcpyAsync(host_map + a, d_map, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, sd.s);
   }
-  const hipError_t es = hipStreamSynchronize(s);
-  if (e == hipSuccess) e = es;
-  (void)hipFree(d);
-  (void)hipStreamDestroy(s);
+  int32_t h_err = 0;
+  for (int i = 0; i < n_sides; ++i) {
+    RowsHandle::ShardSide &sd = h->shard[i];
+    if (e == hipSuccess && st == PGM_OK)
+      e = hipMemcpyAsync(sd.h_err, sd.buf + o_err, sizeof(int32_t), hipMemcpyDeviceToHost, sd.s);
+    const hipError_t es = hipStreamSynchronize(sd.s);
+    if (e == hipSuccess) e = es;
+    h_err |= sd.h_err[0];
+  }
   if (st != PGM_OK) return st;
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -4444,8 +4511,8 @@ int pgm_rows_shard_run(void *const *handles, int32_t n_shards, int32_t mode, con
     const int64_t a = n_rows * i / n_shards, b = n_rows * (i + 1) / n_shards;
     th.emplace_back([&, i, a, b] {
       if (b > a) {
-        st[i] = rows_shard_one((RowsHandle *)handles[i], mode, host_codes, ld_codes, n_cols, a, b - a, host_marg,
-                               ld_out, host_map, err_any);
+        st[i] = rows_shard_one((RowsHandle *)handles[i], mode, host_codes, ld_codes, a, b - a, host_marg, ld_out,
+                               host_map, err_any);
         if (st[i] != PGM_OK) msg[i] = g_err;  // the worker's thread-local message
       }
     });

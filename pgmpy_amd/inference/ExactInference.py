@@ -5,8 +5,11 @@ factor operation runs in libpgmhip kernels:
   * query(elimination_order="greedy") — the reference's one opt_einsum call
     (L349-406) becomes a host-planned greedy path of fused product+marginalize
     kernels over evidence-sliced CPTs (pgmpy_amd.inference.contraction);
-  * classic VE (map_query, any named/explicit order; L141-244) — product and
-    marginalize per eliminated variable, each one kernel;
+  * classic VE (map_query, any named/explicit order; L141-244) — ONE planned
+    contraction whose path is the elimination order itself (each step multiplies
+    the factors holding the next variable and sums it out, the reference's
+    working-set update), compiled and cached per (operand shapes, order)
+    (contraction.order_path, _variable_elimination below);
   * BeliefPropagation.calibrate — a two-pass (collect/distribute)
     Lauritzen-Spiegelhalter belief-update schedule on the device.  The
     reference repeats message passes until _is_converged (L807-895); belief

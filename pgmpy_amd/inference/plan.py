@@ -252,16 +252,19 @@ class PatternPlan:
                         self._handle_joint = h
                     self._handle = h
 
-    def shard_run(self, codes, devices, marginals=True, map_=False):
+    def shard_run(self, codes, devices, marginals=True, map_=False, out=None):
         """This fused plan over host rows sharded across GPUs through the C-ABI (pgm_rows_shard_run):
         codes = host uint8 [columns, n_rows] in this plan's column numbering (col_of), devices = the
         HIP device of each shard (contiguous row blocks, shard i on devices[i]; one plan handle per
         shard, created on its device and cached).  Returns {"marg": [n_acc, n_rows] f64, "map": [n_rows]
-        int32} as numpy arrays, equal to run() over all rows.  The native path a non-Python caller uses
-        (include/pgmhip.h); pgmpy_amd.distributed shards over processes instead."""
+        int32} as numpy arrays, equal to run() over all rows.  out: the caller's arrays to write instead
+        (same keys; pinned ones, e.g. pgmpy_amd._native.HostBuffer arrays, take the overlapped DMA path).
+        The native path a non-Python caller uses (include/pgmhip.h); pgmpy_amd.distributed shards over
+        processes instead."""
         if self.kind != "fused":
             raise ValueError("shard_run(): fused plans only")
-        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        if not (isinstance(codes, np.ndarray) and codes.dtype == np.uint8 and codes.flags.c_contiguous):
+            codes = np.ascontiguousarray(codes, dtype=np.uint8)
         n_cols, n_rows = codes.shape
         L = N.lib()
         cache = self.__dict__.setdefault("_shard_handles", {})
@@ -276,8 +279,18 @@ class PatternPlan:
                     N.check(L.pgm_set_device(E.device().index or 0), "set_device")
             handles.append(cache[key])
         mode = (N.ROWS_MARGINALS if marginals else 0) | (N.ROWS_MAP if map_ else 0)
-        marg = np.empty((self.n_acc, n_rows), dtype=np.float64) if marginals else None
-        mp = np.empty(n_rows, dtype=np.int32) if map_ else None
+        out = out or {}
+        marg = out.get("marg") if marginals else None
+        mp = out.get("map") if map_ else None
+        if marg is None and marginals:
+            marg = np.empty((self.n_acc, n_rows), dtype=np.float64)
+        if mp is None and map_:
+            mp = np.empty(n_rows, dtype=np.int32)
+        if marg is not None and (marg.dtype != np.float64 or marg.shape != (self.n_acc, n_rows)
+                                 or not marg.flags.c_contiguous):
+            raise ValueError(f"out['marg'] must be a C-contiguous float64 [{self.n_acc}, {n_rows}] array")
+        if mp is not None and (mp.dtype != np.int32 or mp.shape != (n_rows,)):
+            raise ValueError(f"out['map'] must be an int32 [{n_rows}] array")
         err = np.zeros(1, dtype=np.int32)
         arr = (ctypes.c_void_p * len(handles))(*[h.value for h in handles])
         N.check(L.pgm_rows_shard_run(arr, len(handles), mode, codes.ctypes.data_as(ctypes.c_void_p), n_rows, n_cols,

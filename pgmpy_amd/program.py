@@ -11,6 +11,7 @@ import os
 
 from . import _native as N
 from . import engine as E
+from . import hazard as H
 
 
 # index-space size (outputs x reduction) up to which a step joins a batch (knob PGM_BATCH_MAX_WORK)
@@ -56,14 +57,16 @@ class _Rec:
     """One recorded launch of a levelled Program: plain launch, optional batch job, buffers it
     reads / writes (storage keys)."""
 
-    __slots__ = ("fn", "note", "job", "reads", "writes", "level", "pm", "nbytes")
+    __slots__ = ("fn", "note", "job", "reads", "writes", "level", "pm", "nbytes", "foot", "step")
 
-    def __init__(self, fn, note, job, reads, writes, pm=None, nbytes=0):
+    def __init__(self, fn, note, job, reads, writes, pm=None, nbytes=0, foot=None, step=0):
         self.fn, self.note, self.job = fn, note, job
         self.reads, self.writes = reads, writes
         self.level = 0
         self.pm = pm  # bound specialised product+marginal step (mergeable with its level's others)
         self.nbytes = nbytes  # algorithmic bytes: every distinct tensor read or written once
+        self.foot = foot  # byte ranges the launch touches, from its descriptor (hazard.py)
+        self.step = step  # plain Program: the launch this record runs in (a batch's jobs share one)
 
 
 class _Batch:
@@ -97,6 +100,8 @@ class Program:
         self._chains = []  # levelled batch handles (several dependency levels in one launch)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
         self.merged_parts = {}  # step index -> full notes of the specialised steps merged into it
+        self._plain_recs = []  # plain Program: one record per launch / batch job (check_hazards only)
+        self._unit = 0  # plain Program: launch counter behind _Rec.step
 
     # ------------------------------------------------------------------ batching
     def begin_batch(self):
@@ -105,6 +110,7 @@ class Program:
         if self._batch is not None:
             raise RuntimeError("batch already open")
         self._batch = _Batch()
+        self._unit += 1  # every job of the batch runs in the same launch
 
     def end_batch(self):
         """Close the batch.  It becomes a step when the program is lowered (first run / capture):
@@ -121,6 +127,7 @@ class Program:
         captured graph then holds as a memcpy node)."""
         if self._levels:
             raise RuntimeError("raw_step: plain Program only")
+        self._unit += 1
         self._steps.append(fn)
         self.notes.append(note)
 
@@ -222,22 +229,46 @@ class Program:
         self._steps, self.notes = steps, notes
 
     # ------------------------------------------------------------------ levelled recording
-    def _emit(self, fn, note, reads, writes, job=None, pm=None):
-        """Append one launch (plain `fn(stream)`), or record it for levelling."""
+    @staticmethod
+    def _rec(fn, note, reads, writes, job=None, pm=None, foot=None, step=0):
+        rk = [k for k in (_key(t) for t in reads if t is not None) if k]
+        wk = [k for k in (_key(t) for t in writes if t is not None) if k]
+        seen, nb = set(), 0
+        for t in list(reads) + list(writes):
+            if t is not None and hasattr(t, "numel") and id(t) not in seen:
+                seen.add(id(t))
+                nb += t.numel() * t.element_size()
+        return _Rec(fn, note, job, rk, wk, pm, nb, foot, step)
+
+    def _emit(self, fn, note, reads, writes, job=None, pm=None, foot=None):
+        """Append one launch (plain `fn(stream)`), or record it for levelling.  reads / writes: the
+        buffers the launch declares (its hazards); foot: the byte ranges its descriptor touches
+        (hazard.py), checked against the declarations by check_hazards()."""
         if self._levels:
             if self._lowered:
                 raise RuntimeError("levelled Program: no recording after the first run / capture")
-            rk = [k for k in (_key(t) for t in reads if t is not None) if k]
-            wk = [k for k in (_key(t) for t in writes if t is not None) if k]
-            seen, nb = set(), 0
-            for t in list(reads) + list(writes):
-                if t is not None and hasattr(t, "numel") and id(t) not in seen:
-                    seen.add(id(t))
-                    nb += t.numel() * t.element_size()
-            self._recs.append(_Rec(fn, note, job, rk, wk, pm, nb))
+            self._recs.append(self._rec(fn, note, reads, writes, job, pm, foot))
         else:
+            self._unit += 1
+            self._plain_recs.append(self._rec(fn, note, reads, writes, foot=foot, step=self._unit))
             self._steps.append(fn)
             self.notes.append(note)
+
+    def _batch_job(self, note, reads, writes, foot):
+        """Plain Program: record a job of the open batch for check_hazards()."""
+        self._plain_recs.append(self._rec(None, note, reads, writes, foot=foot, step=self._unit))
+
+    def check_hazards(self):
+        """Recompute every recorded launch's byte ranges from its descriptor and check them against
+        the declared reads / writes and the launch order the program runs (hazard.check): [] when
+        every overlap is ordered.  Host only (no launch)."""
+        self._lower()
+        recs = self._recs if self._levels else self._plain_recs
+        units = [(r.note, r.foot or [], r.reads, r.writes, None) for r in recs]
+        tensors = [t for t in self._keep if hasattr(t, "untyped_storage")]
+        if self._levels:
+            return H.check(units, tensors, lambda a, b: recs[b].level > recs[a].level)
+        return H.check(units, tensors, lambda a, b: recs[a].step != recs[b].step)
 
     def _ready(self):
         """Lower, then compile every specialised kernel the steps launch (in parallel, before any
@@ -408,6 +439,7 @@ class Program:
         d, out, ws, wsb = E.prepare_contract(A, la, B, lb, out_labels, reduce, combine, out)
         self._keep.extend([d, A, B, out, ws])
         L = N.lib()
+        note = f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}"
         if self._levels:
             w = _work(d)
             args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
@@ -415,27 +447,30 @@ class Program:
             if w <= (BATCH_MAX_WORK if wsb == 0 else BATCH_SPLIT_WORK):
                 job = ("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)))
             fn, pm = (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), None
+            foot = H.contract_foot(d, N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
             if (job is None or A.numel() >= PM_PREFER_MIN) and B is None and combine == "copy" and \
                     reduce in ("sum", "max"):
-                pm = self._bind_marginal(A, la, out_labels, out, reduce)
-                if pm is not None:
+                bm = self._bind_marginal(A, la, out_labels, out, reduce)
+                if bm is not None:
+                    pm, foot = bm
                     fn, job = (lambda s, b=pm: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), None
-            self._emit(fn, f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}",
-                       [A, B], [out, ws], job, pm=pm)
+            self._emit(fn, note, [A, B], [out, ws], job, pm=pm, foot=foot)
             return out
         w = _work(d) if self._batch is not None else 0
         if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else PLAIN_SPLIT_WORK):
             self._batch.jobs.append(("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)),
                                      (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)))
+            self._batch_job(note, [A, B], [out], H.contract_foot(d, N.ptr(A), N.ptr(B), N.ptr(out)))
             return out
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
-        self._steps.append(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"))
-        self.notes.append(f"contract {combine}/{reduce} {list(la)}{tuple(A.shape)} x {lb} -> {list(out_labels)}")
+        self._emit(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"), note, [A, B], [out, ws],
+                   foot=H.contract_foot(d, N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb))
         return out
 
     def _bind_marginal(self, A, la, out_labels, out, reduce):
-        """out = reduce of A onto out_labels as a specialised marginal-only step (one operand), or
-        None when the fused kernel does not take the shape (rows not innermost, too few blocks)."""
+        """(bound, footprint): out = reduce of A onto out_labels as a specialised marginal-only step (one
+        operand), or None when the fused kernel does not take the shape (rows not innermost, too few
+        blocks)."""
         la, out_labels = list(la), list(out_labels)
         if not out_labels or out_labels[-1] != la[-1] or any(l not in la for l in out_labels):
             return None
@@ -451,7 +486,7 @@ class Program:
             return None
         self._keep.extend([d, ptrs, ms])
         self._pm_bound.append(bound)
-        return bound
+        return bound, H.product_n_foot(d, ptrs, None, store=False, marg=[(ms, N.ptr(out))])
 
     def product_n(self, operands, out_labels, out=None, kinds=None):
         ops = list(operands)
@@ -486,7 +521,8 @@ class Program:
                 self._pm_bound.append(bound)
                 fn, pm, job = (lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), bound, None
         self._emit(fn, f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
-                       f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job, pm=pm)
+                       f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job, pm=pm,
+                   foot=H.product_n_foot(d, ptrs, N.ptr(out)))
         return out
 
     def product_n_marginal(self, operands, out_labels, marg_labels, out=None, kinds=None, reduce="sum",
@@ -515,7 +551,8 @@ class Program:
                            f"product_n_marginal{'' if store else ' (marginal only)'} "
                            f"{[(list(ls), tuple(t.shape)) for t, ls in ops]} "
                            f"-> {list(out_labels)}{tuple(out2.shape)} + {list(marg_labels)}{tuple(M.shape)}",
-                           [t for t, _ in ops], [out2, M] if store else [M], pm=pm)
+                           [t for t, _ in ops], [out2, M] if store else [M], pm=pm,
+                           foot=H.product_n_foot(d, ptrs, N.ptr(out2), store, [(ms, N.ptr(M))]))
                 return out2, M, store
         C = self.product_n(ops, out_labels, out, kinds)
         M = self.contract(C, list(out_labels), None, None, list(marg_labels), reduce=reduce, combine="copy")
@@ -547,7 +584,9 @@ class Program:
         self._pm_bound.append(bound)
         self._emit(lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"),
                    f"product_n_marginals {[(list(ls), tuple(t.shape)) for t, ls in ops]} -> {list(marg1)} + "
-                   f"{list(marg2)}", [t for t, _ in ops], Ms, pm=bound)
+                   f"{list(marg2)}", [t for t, _ in ops], Ms, pm=bound,
+                   foot=H.product_n_foot(d, ptrs, None, store=False,
+                                         marg=[(strides[0], N.ptr(Ms[0])), (strides[1], N.ptr(Ms[1]))]))
         return Ms[0], Ms[1]
 
     def indicator(self, codes_col, card, n_rows, err=None):
@@ -558,7 +597,9 @@ class Program:
         self._keep.extend([codes_col, out, err])
         # err is an atomic OR flag: not a hazard; a levelled program batches all findings into one launch
         self._emit(lambda s, a=args: N.check(L.pgm_indicator(*a, s), "indicator"), f"indicator card {card}",
-                   [codes_col], [out], ("indicator", args))
+                   [codes_col], [out], ("indicator", args),
+                   foot=H.indicator_foot(N.ptr(codes_col), n_rows, card, N.ptr(out), int(out.stride(0)),
+                                         int(out.stride(1)), N.ptr(err)))
         return out
 
     def gather(self, A, la, evidence, out_labels, codes, ld, row0, n_rows, err=None):
@@ -566,15 +607,17 @@ class Program:
         L = N.lib()
         args = (ctypes.byref(d), Aptr, N.ptr(codes), N.ptr(out), N.ptr(err))
         self._keep.extend([d, A, codes, out, err])
+        note = f"gather {list(la)} -> {list(out_labels)}"
+        foot = H.gather_foot(d, Aptr, N.ptr(codes), N.ptr(out), N.ptr(err))
         if self._levels:
-            self._emit(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"), f"gather {list(la)} -> {list(out_labels)}",
-                       [A, codes], [out], ("gather", args) if out.numel() <= BATCH_MAX_WORK else None)
+            self._emit(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"), note,
+                       [A, codes], [out], ("gather", args) if out.numel() <= BATCH_MAX_WORK else None, foot=foot)
             return out
         if self._batch is not None and out.numel() <= BATCH_MAX_WORK:
             self._batch.jobs.append(("gather", args, args))
+            self._batch_job(note, [A, codes], [out], foot)
             return out
-        self._steps.append(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"))
-        self.notes.append(f"gather {list(la)} -> {list(out_labels)}")
+        self._emit(lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather"), note, [A, codes], [out], foot=foot)
         return out
 
     def pair_gemm(self, A, la, B, lb, keep, shape):
@@ -593,14 +636,17 @@ class Program:
 
         self._emit(lambda s, a=args: N.check(L.pgm_gemm(*a, s), "gemm"),
                    f"gemm b{d.batch} m{d.m} n{d.n} k{d.k} unit A:{unit_group(A, la)} B:{unit_group(B, lb)} "
-                   f"lane_order {d.lane_order} strides(ab,bb,cb,am,cm,ak,bk,bn,cn)={list(d.stride)}", [A, B], [C])
+                   f"lane_order {d.lane_order} strides(ab,bb,cb,am,cm,ak,bk,bn,cn)={list(d.stride)}", [A, B, table], [C],
+                   foot=H.view_foot(A, H.READ) + H.view_foot(B, H.READ) + H.view_foot(table, H.READ) +
+                   H.view_foot(C, H.WRITE))
         return C
 
     def argmax(self, X, n_rows, row_len, s_row, s_elem, out32):
         L = N.lib()
         args = (N.ptr(X), int(n_rows), int(row_len), int(s_row), int(s_elem), None, N.ptr(out32))
         self._keep.extend([X, out32])
-        self._emit(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"), "argmax", [X], [out32])
+        self._emit(lambda s, a=args: N.check(L.pgm_argmax(*a, s), "argmax"), "argmax", [X], [out32],
+                   foot=H.argmax_foot(N.ptr(X), n_rows, row_len, s_row, s_elem, N.ptr(out32)))
 
     def time_steps(self, reps=3):
         """[(us, note)] per recorded step, each replayed alone (profiling aid; not graph-replayed)."""

@@ -358,6 +358,65 @@ def test_program_dependency_levels():
     assert ran == ["w_a", "w_b", "r_ab_w_c", "w_d", "inplace_c", "w_a_view"]
 
 
+def test_program_hazard_check_catches_undeclared_and_unordered_access():
+    """Program.check_hazards (pgmpy_amd/hazard.py): byte ranges recomputed from each launch's own
+    descriptor must lie in buffers the launch declares, and overlapping launches (one writing) must
+    be in different dependency levels.  Host only: CPU tensors stand in for device buffers, the
+    launches are never run."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as N
+    from pgmpy_amd import hazard as H
+    from pgmpy_amd.program import Program
+
+    a, b, c, scratch = (torch.zeros(16, dtype=torch.float64) for _ in range(4))
+
+    def whole(t, mode):
+        return H.view_foot(t, mode)
+
+    def build(declare_b_write=True, stray=False):
+        prog = Program(levels=True)
+        prog._keep.extend([a, b, c, scratch])
+        nop = lambda s: None  # noqa: E731
+        prog._emit(nop, "a -> b", [a], [b] if declare_b_write else [],
+                   foot=whole(a, H.READ) + whole(b, H.WRITE))
+        prog._emit(nop, "b -> c", [b], [c], foot=whole(b, H.READ) + whole(c, H.WRITE))
+        prog._emit(nop, "c[0:8] -> a[8:]", [c], [a], foot=whole(c[:8], H.READ) + whole(a[8:], H.WRITE))
+        if stray:  # a launch that touches bytes outside every buffer the program holds
+            prog._emit(nop, "stray", [], [], foot=[(8, 16, H.WRITE)])
+        return prog
+
+    good = build()
+    assert good.check_hazards() == []
+    assert [r.level for r in good._recs] == [0, 1, 2]
+    # the first launch writes b without declaring it: the reader of b lands in the same level
+    bad = build(declare_b_write=False).check_hazards()
+    assert any("does not declare written" in m for m in bad), bad
+    assert any("without an ordering" in m for m in bad), bad
+    assert any("no buffer the program holds" in m for m in build(stray=True).check_hazards())
+
+    # descriptor footprints: a contraction's operand spans follow its strides (a transposed view of
+    # a [4, 4] buffer reads all 16 entries; its output row 1 is entries 4..7)
+    d = N.ContractDesc()
+    d.n_keep, d.n_red = 1, 1
+    d.keep_card[0], d.red_card[0] = 4, 4
+    d.keep_sa[0], d.red_sa[0] = 1, 4  # A^T
+    d.keep_sc[0] = 1
+    pa, pc = a.data_ptr(), c.data_ptr() + 4 * 8
+    foot = H.contract_foot(d, ctypes.c_void_p(pa), None, ctypes.c_void_p(pc))
+    assert foot == [(pa, pa + 16 * 8, H.READ), (pc, pc + 4 * 8, H.WRITE)]
+    # plain programs: jobs of one batch launch must be independent
+    prog = Program()
+    prog._keep.extend([a, b])
+    prog.begin_batch()
+    prog._batch_job("w a", [], [a], whole(a, H.WRITE))
+    prog._batch_job("r a", [a], [b], whole(a, H.READ) + whole(b, H.WRITE))
+    prog._batch = None
+    assert any("without an ordering" in m for m in prog.check_hazards())
+
+
 def test_hip_backend_config_mirrors_pgmpy_config():
     """pgmpy_amd.compat.Config: pgmpy's set_backend validation (global_vars.py:82-122) plus "hip";
     without a device the hip backend fails loudly (no CPU fallback)."""

@@ -247,6 +247,45 @@ def test_rows_shard_run_matches_run(gpu, rows, n_shards):
         plan.shard_run(bad, [i % n_dev for i in range(n_shards)])
 
 
+@pytest.mark.parametrize("n_shards", [1, 3])
+def test_rows_shard_run_pinned_chunks_against_golden(gpu, n_shards):
+    """The persistent, chunk-pipelined pgm_rows_shard_run (r04: per-handle streams and device buffers
+    kept from the first call, 256 K-row chunks alternating between two streams, outputs DMA'd into
+    pinned host arrays) on the 2,000 reference munin rows tiled to 600,002 rows (so a shard spans
+    several chunks and ends on an odd row count): marginals (1e-6 relative) and MAP (exact) against the
+    reference fixture, twice in a row through the same handles (the kept buffers are reused)."""
+    from pgmpy_amd import _native as N
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from tests.goldens import munin_predict, prob_var_order
+
+    g = munin_predict()
+    m = get_example_model("munin")
+    observed = list(g["columns"])
+    variables = prob_var_order(g["prob_columns"], g["missing"], m.states)
+    plan = PatternPlan(m, variables, observed, {v: i for i, v in enumerate(observed)})
+    rows = 600_002
+    n_ref = g["codes"].shape[1]
+    reps = rows // n_ref + 1
+    codes = N.HostBuffer((len(observed), rows), np.uint8)
+    codes.array[:] = np.tile(g["codes"], (1, reps))[:, :rows]
+    out = {"marg": N.HostBuffer((plan.n_acc, rows), np.float64).array,
+           "map": N.HostBuffer((rows,), np.int32).array}
+    exp = np.tile(g["prob"], (reps, 1))[:rows]
+    want = np.tile(g["map_codes"], (reps, 1))[:rows]
+    for _ in range(2):
+        out["marg"][:] = -1.0
+        got = plan.shard_run(codes.array, [0] * n_shards, marginals=True, map_=True, out=out)
+        assert got["marg"] is out["marg"]
+        np.testing.assert_allclose(got["marg"].T, exp, rtol=1e-6, atol=1e-300)
+        idx = got["map"].astype(np.int64)
+        digits = {}
+        for v, c in reversed(list(zip(variables, plan.cards))):
+            digits[v] = idx % c
+            idx //= c
+        np.testing.assert_array_equal(np.stack([digits[v] for v in g["missing"]], axis=1), want)
+
+
 def test_row_ring_exits_without_posts(gpu):
     """Every exit path of the resident kernel ends the launch: cancel() with batches never posted,
     and the timeout (the waves give up waiting; finish() then reports the timeout)."""

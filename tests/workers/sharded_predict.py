@@ -2,7 +2,7 @@
 
 Launched as `python -m torch.distributed.run --nproc-per-node N tests/workers/sharded_predict.py OUT`.
 Every rank runs the HIP fused row plan (bound launch, as bench.py --workload c5) on its contiguous
-block of the 1,000 reference munin template rows (tests/golden/munin_predict.npz), the marginals and
+block of the 2,000 reference munin template rows (tests/golden/munin_predict.npz), the marginals and
 MAP indices are gathered to rank 0 (nccl = RCCL when every rank has its own GPU, else gloo through
 host memory), and rank 0 also runs all rows in one launch and saves both for the test to compare.
 """
@@ -43,7 +43,7 @@ def main(out_path):
     variables = prob_var_order(g["prob_columns"], g["missing"], model.states)
     plan = PatternPlan(model, variables, observed, {v: i for i, v in enumerate(observed)})
     assert plan.kind == "fused", plan.describe()
-    codes = np.ascontiguousarray(g["codes"], dtype=np.uint8)  # [1038, 1000]
+    codes = np.ascontiguousarray(g["codes"], dtype=np.uint8)  # [1038, 2000]
     n = codes.shape[1]
     lo, hi = shard_bounds(n, world, rank)
 
