@@ -328,11 +328,14 @@ def ring_launch_roofline(plan, d_codes, outs, rows, err, n_batches=400):
     nb = len(outs)
     ring = plan.ring([(d_codes, rows * nb, i * rows, outs[i]) for i in range(nb)], rows, err=err)
     kname, k_blocks, k_wg = ring.kernel()
-    ring.run(n_batches)  # warm, same size (so a rocprofv3 --stats average over both dispatches is the
-    torch.cuda.synchronize()  # timed one's duration): the kernel's first-use load, every slot touched
+    # warm, same size (so a rocprofv3 --stats average over both dispatches is the timed one's duration):
+    # the kernel's first-use load, every slot touched.  replay: 400 batches over the resident slots, whose
+    # inputs never change (each repeat writes the same outputs)
+    ring.run(n_batches, replay=True)
+    torch.cuda.synchronize()
     timer = HipTimer()
     timer.start()
-    ring.run(n_batches)
+    ring.run(n_batches, replay=True)
     timer.mark_end()
     torch.cuda.synchronize()
     ms = timer.elapsed_ms()
@@ -843,6 +846,134 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
     return result
 
 
+def bench_c5_host(args, dist, rank, world):
+    """C5 delivered to host memory (the default, --c5-delivery host): every rank writes its block's
+    results into pinned host memory of its node over its OWN host link, with no collective — the
+    result of predict_probability / predict is a host DataFrame, and a funnel into one GPU (the RCCL
+    gather, --c5-delivery rccl) moves every row's 136 B through rank 0's links.  One step = each
+    rank's fused-plan launch over its block (device-resident evidence) into device buffer k % 2 +
+    the DMA of that buffer into pinned host buffer k % 2 on a copy stream; launch k + 1 overlaps
+    copy k (launch k + 2 waits for copy k, which frees its buffer)."""
+    import torch
+
+    from pgmpy_amd.distributed import HostDelivery, shard_bounds
+    from pgmpy_amd.inference.batch import upload_codes
+    from pgmpy_amd.inference.plan import PatternPlan
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import forward_sample_codes
+
+    model = get_example_model("munin")
+    missing_list = random.Random(0).sample(sorted(model.nodes()), 3)
+    variables = list(set(missing_list))
+    total = args.rows
+    lo, hi = shard_bounds(total, world, rank)
+    rows = hi - lo
+    codes_all, nodes = forward_sample_codes(model, rows, seed=(42, lo))
+    observed = [v for v in nodes if v not in set(variables)]
+    pos = {v: i for i, v in enumerate(nodes)}
+    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])
+    del codes_all
+    plan = PatternPlan(model, variables, observed, {v: i for i, v in enumerate(observed)})
+    assert plan.kind == "fused", plan.describe()
+    d_codes = upload_codes(codes_ev)
+    dev = d_codes.device
+    want_map = args.c5_output == "map"
+    key = "map" if want_map else "marg"
+    outs = [plan.alloc_outputs(rows, marginals=not want_map, map_=want_map) for _ in range(2)]
+    delivery = HostDelivery(tuple(outs[0][key].shape), outs[0][key].dtype, depth=2, device=dev)
+    hosts, cs = delivery.hosts, delivery.stream
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    ls = torch.cuda.Stream(device=dev)
+    bounds = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=ls) for i in range(2)]
+    kname, k_blocks, k_wg = bounds[0].kernel()
+
+    def step(k):
+        delivery.acquire(k, ls)  # device buffer k % 2 and host slot k % 2 are free
+        bounds[k % 2].run()
+        delivery.deliver(k, outs[k % 2][key], ls)
+
+    for k in range(max(args.warmup, 2)):
+        step(k)
+    torch.cuda.synchronize()
+    barrier(dist)
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    cs.synchronize()
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t_end - t_start)
+    assert int(err.item()) == 0
+    # the parts alone, outside the window: the launch, and the copy-out (each back to back, one stream)
+    timer = HipTimer()
+    with torch.cuda.stream(ls):
+        timer.start()
+        for k in range(args.steps):
+            bounds[k % 2].run()
+        kernel_ms = timer.stop_ms() / args.steps
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(cs):
+        for k in range(args.steps):
+            hosts[k % 2].copy_(outs[k % 2][key], non_blocking=True)
+    cs.synchronize()
+    copy_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    copy_bytes = hosts[0].numel() * hosts[0].element_size()
+    parity = None
+    if rank == 0:
+        from oracle import ve as OVE  # checker only: first rows of rank 0's block, from the HOST copy
+        from oracle.network import load_network
+
+        net = load_network("munin")
+        got = hosts[(args.steps - 1) % 2].numpy()
+        worst, wrong, checked = 0.0, 0, 0
+        for r in range(min(rows, 16)):
+            ev = {v: net.states[v][codes_ev[j, r]] for j, v in enumerate(observed)}
+            if want_map:
+                mp, gap = OVE.map_query(net, list(plan.variables), ev)
+                if gap <= 1e-9:
+                    continue
+                flat = 0
+                for v in plan.variables:
+                    flat = flat * len(net.states[v]) + net.states[v].index(mp[v])
+                wrong += int(got[r] != flat)
+            else:
+                m = OVE.query(net, variables, ev, joint_out=False)
+                exp = np.concatenate([m[v] for v in plan.variables])
+                worst = max(worst, float(np.max(np.abs(got[:, r] - exp) / np.maximum(np.abs(exp), 1e-300))))
+            checked += 1
+        parity = ({"rows_checked": checked, "map_mismatches": wrong, "ok": wrong == 0} if want_map else
+                  {"rows_checked": checked, "max_rel_err": worst, "ok": worst <= 1e-6, "checked_on": "host copy"})
+    ms_per_step = elapsed * 1e3 / args.steps
+    bpr = plan.algorithmic_bytes_per_row(marginals=not want_map, map_=want_map)
+    achieved = bpr * rows / (kernel_ms * 1e-3) / 1e9
+    return {
+        "metric": METRIC, "value": total * args.steps / elapsed, "unit": "queries/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))",
+        "config": {"workload": ("C5 munin predict (MAP) template, 1M rows per step sharded over the ranks, "
+                                "int32 MAP indices delivered to pinned host memory per rank") if want_map else
+                               ("C5 munin predict_probability template, 1M rows per step sharded over the ranks, "
+                                "marginals delivered to pinned host memory per rank"),
+                   "network": "munin", "missing": variables, "global_rows_per_step": total,
+                   "rows_per_gpu_per_step": rows, "delivery": "host",
+                   "launch": "bound fused-plan launch on a launch stream into device buffer k % 2, DMA to pinned "
+                             "host buffer k % 2 on a copy stream (launch k + 1 overlaps copy k)",
+                   "parallelism": f"rows sharded over {world} rank(s), no collective: each rank's own host link"},
+        "kernel_ms": kernel_ms, "copy_ms": copy_ms, "copy_bytes_per_rank": copy_bytes,
+        "copy_GBps": copy_bytes / (copy_ms * 1e-3) / 1e9,
+        "pipelined_step_over_copy": ms_per_step / copy_ms if copy_ms else None,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
+                     "grid": {"blocks": k_blocks, "workgroup": k_wg}, "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows,
+                     "step_bound": "host link (PCIe D2H of the block's results)"},
+        "parity": parity,
+    }
+
+
 def bench_c5(args, dist, rank, world):
     """C5 (BASELINE.json configs[4]): ROWS (1,000,000) munin template rows per step over all ranks,
     contiguous blocks per rank (distributed.shard_bounds), strong scaling.  One step = every rank's
@@ -1193,6 +1324,9 @@ def main():
     ap.add_argument("--workload", default="c3", choices=["c3", "c5", "c1", "c2", "c4"])
     ap.add_argument("--c5-output", default="marginals", choices=["marginals", "map"],
                     help="c5: gather the fp64 marginals (predict_probability) or the MAP indices (predict)")
+    ap.add_argument("--c5-delivery", default="host", choices=["host", "rccl"],
+                    help="c5: each rank DMAs its block's results into pinned host memory (host, no collective) "
+                         "or gathers them into rank 0's GPU over RCCL (rccl)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
@@ -1236,7 +1370,7 @@ def main():
     if args.workload == "c3":
         res = bench_c3(args, dist, rank, world)
     elif args.workload == "c5":
-        res = bench_c5(args, dist, rank, world)
+        res = (bench_c5_host if args.c5_delivery == "host" else bench_c5)(args, dist, rank, world)
     elif args.workload == "c2":
         res = bench_c2(args)
     elif args.workload == "c1":

@@ -1,11 +1,17 @@
 """Multi-GPU evidence sharding: one process per GPU, rows split in contiguous blocks.
 
 Rows are independent given a compiled plan, so the data path has no
-collective: every rank runs the same plan on its own block of rows.  The only
-exchange is the optional final gather of per-row results to rank 0
-(torch.distributed `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo"
-on CPU for the tests).  CPTs are replicated: each rank compiles its own plan
-(munin's CPTs are 787 KB).
+collective: every rank runs the same plan on its own block of rows.  Results
+leave a rank one of two ways:
+
+* HostDelivery (default for C5): each rank DMAs its block's results into pinned
+  host memory over its own host link, double-buffered so step k's copy overlaps
+  step k + 1's launch — no collective, every GPU's link carries only its share;
+* gather_rows: one gather of per-row results to rank 0 (torch.distributed
+  `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo" on CPU for the
+  tests) — every row's bytes funnel into rank 0's links.
+
+CPTs are replicated: each rank compiles its own plan (munin's CPTs are 787 KB).
 """
 import numpy as np
 
@@ -23,15 +29,18 @@ def gather_rows(local, n_rows, dist, dst=0):
 
     Returns the concatenated tensor [..., n_rows] on dst and None elsewhere.
     Uses one collective (torch.distributed.gather); rows are padded to the
-    largest shard so every rank sends the same shape."""
+    largest shard so every rank sends the same shape (a block already of that
+    size is sent as it is, without a padded copy)."""
     import torch
 
     world, rank = dist.get_world_size(), dist.get_rank()
     bounds = [shard_bounds(n_rows, world, r) for r in range(world)]
     max_rows = max(hi - lo for lo, hi in bounds)
-    pad_shape = list(local.shape[:-1]) + [max_rows]
-    send = torch.zeros(pad_shape, dtype=local.dtype, device=local.device)
-    send[..., :local.shape[-1]] = local
+    if local.shape[-1] == max_rows and local.is_contiguous():
+        send = local
+    else:
+        send = torch.zeros(list(local.shape[:-1]) + [max_rows], dtype=local.dtype, device=local.device)
+        send[..., :local.shape[-1]] = local
     recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     dist.gather(send, gather_list=recv, dst=dst)
     if rank != dst:
@@ -49,3 +58,50 @@ def run_sharded(executor, codes_host, n_rows, dist, gather=True):
     if not gather:
         return local
     return gather_rows(local, n_rows, dist)
+
+
+class HostDelivery:
+    """Results of consecutive launches delivered into pinned host buffers of this rank's node, with no
+    collective (SURVEY.md §8(e)'s alternative to the gather): `depth` pinned buffers and one copy
+    stream.  Step k: acquire(k, stream) before the launch that writes the step's device buffer (the
+    launch stream then waits until slot k % depth's previous copy-out is done, so that device buffer
+    and that host buffer are free), then deliver(k, device_tensor, stream) after it: a DMA on the copy
+    stream, ordered after the launch, so the copy of step k overlaps the launch of step k + 1.
+    Each GPU's copies use its own host link."""
+
+    def __init__(self, shape, dtype, depth=2, device=None):
+        import torch
+
+        self.depth = int(depth)
+        self.hosts = [torch.empty(tuple(shape), dtype=dtype, pin_memory=True) for _ in range(self.depth)]
+        self.stream = torch.cuda.Stream(device=device)
+        self._copied = [torch.cuda.Event() for _ in range(self.depth)]
+        self._ready = [torch.cuda.Event() for _ in range(self.depth)]
+        self._used = [False] * self.depth
+
+    def acquire(self, k, stream):
+        i = k % self.depth
+        if self._used[i]:
+            stream.wait_event(self._copied[i])
+
+    def deliver(self, k, src, stream):
+        """Queue the copy of `src` (written by work already queued on `stream`) into host slot k %
+        depth; returns that pinned host tensor (complete after wait(k))."""
+        import torch
+
+        i = k % self.depth
+        self._ready[i].record(stream)
+        self.stream.wait_event(self._ready[i])
+        with torch.cuda.stream(self.stream):
+            self.hosts[i].copy_(src, non_blocking=True)
+        self._copied[i].record(self.stream)
+        self._used[i] = True
+        return self.hosts[i]
+
+    def wait(self, k=None):
+        """Every queued copy (k None) or step k's copy has completed."""
+        if k is None:
+            self.stream.synchronize()
+        else:
+            self._copied[k % self.depth].synchronize()
+        return None if k is None else self.hosts[k % self.depth]

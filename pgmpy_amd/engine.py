@@ -22,17 +22,126 @@ ROW = "__row__"  # label of the evidence-row (batch) axis
 # SURVEY.md §8(b) threading: the reference calls map_query from joblib threads on one shared
 # object (DiscreteBayesianNetwork.py:871) and ctypes releases the GIL.  A first query of a pattern
 # captures a HIP graph, and HIP rejects work on the legacy stream from another thread while a
-# stream is capturing.  So the public inference entry points (and every capture) run under one
-# process-wide re-entrant lock: the Python side takes a lock, as §8(b) allows.
-device_lock = threading.RLock()
+# stream is capturing.  So the Python side takes a readers-writer lock, as §8(b) allows: the public
+# inference entry points hold it SHARED (replays of compiled plans run concurrently; each compiled
+# runner serialises only its own buffers), every HIP graph capture holds it EXCLUSIVELY.
+
+
+class DeviceLock:
+    """Re-entrant readers-writer lock with writer preference.
+
+    A thread may nest shared holds, nest exclusive holds, and take shared inside exclusive.  A thread
+    that holds it shared and asks for it exclusively gives its shared hold up while it waits (and gets
+    it back when it releases the exclusive hold): so a capture inside a public call needs no upgrade,
+    and the rule that avoids deadlock is that no other lock is held while waiting for the exclusive
+    one (capture sites take it before any per-plan lock, PatternPlan.prepare_steps).
+    `peak_readers` records the most threads ever inside at once (a test's evidence of overlap)."""
+
+    def __init__(self):
+        self._cv = threading.Condition(threading.Lock())
+        self._readers = 0
+        self._writer = None
+        self._wdepth = 0
+        self._waiting_writers = 0
+        self._tls = threading.local()
+        self.peak_readers = 0
+
+    def _t(self):
+        t = self._tls
+        if not hasattr(t, "n"):
+            t.n, t.counted = 0, False
+        return t
+
+    def acquire_shared(self):
+        me, t = threading.get_ident(), self._t()
+        with self._cv:
+            if t.n > 0 or self._writer == me:
+                t.n += 1
+                return
+            while self._writer is not None or self._waiting_writers:
+                self._cv.wait()
+            self._readers += 1
+            self.peak_readers = max(self.peak_readers, self._readers)
+            t.n, t.counted = 1, True
+
+    def release_shared(self):
+        t = self._t()
+        with self._cv:
+            t.n -= 1
+            if t.n == 0 and t.counted:
+                t.counted = False
+                self._readers -= 1
+                self._cv.notify_all()
+
+    def acquire_exclusive(self):
+        me, t = threading.get_ident(), self._t()
+        with self._cv:
+            if self._writer == me:
+                self._wdepth += 1
+                return
+            if t.counted:  # give the shared hold up while waiting (no upgrade deadlock)
+                t.counted = False
+                self._readers -= 1
+                self._cv.notify_all()
+            self._waiting_writers += 1
+            while self._writer is not None or self._readers > 0:
+                self._cv.wait()
+            self._waiting_writers -= 1
+            self._writer, self._wdepth = me, 1
+
+    def release_exclusive(self):
+        t = self._t()
+        with self._cv:
+            self._wdepth -= 1
+            if self._wdepth == 0:
+                self._writer = None
+                if t.n > 0:  # back to the shared hold it had before
+                    t.counted = True
+                    self._readers += 1
+                self._cv.notify_all()
+
+    def shared(self):
+        return _Held(self.acquire_shared, self.release_shared)
+
+    def exclusive(self):
+        return _Held(self.acquire_exclusive, self.release_exclusive)
+
+
+class _Held:
+    __slots__ = ("_a", "_r")
+
+    def __init__(self, a, r):
+        self._a, self._r = a, r
+
+    def __enter__(self):
+        self._a()
+        return self
+
+    def __exit__(self, *exc):
+        self._r()
+        return False
+
+
+device_lock = DeviceLock()
 
 
 def serialized(fn):
-    """Run `fn` holding device_lock (re-entrant: nested public calls are free)."""
+    """Run `fn` holding device_lock shared (public entry points; re-entrant)."""
 
     @functools.wraps(fn)
     def wrapper(*args, **kwargs):
-        with device_lock:
+        with device_lock.shared():
+            return fn(*args, **kwargs)
+
+    return wrapper
+
+
+def exclusive(fn):
+    """Run `fn` holding device_lock exclusively (HIP graph captures)."""
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        with device_lock.exclusive():
             return fn(*args, **kwargs)
 
     return wrapper

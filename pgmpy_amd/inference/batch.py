@@ -8,6 +8,7 @@ grouped by evidence pattern, and each pattern runs as one compiled device plan
 (pgmpy_amd.inference.plan.PatternPlan).
 """
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -345,7 +346,10 @@ def ingest_columnar(model, data, columns):
     raws, luts, addrs = [], [], []
     i8 = np.dtype(np.int8)
     for col, arr in zip(columns, cats):
-        raw = arr._codes
+        try:
+            raw = arr.codes  # public, a read-only view of the codes (no copy)
+        except (AttributeError, TypeError):  # pragma: no cover - pandas API moved: the general encoder
+            return None
         if raw.dtype is not i8 or not raw.flags.c_contiguous:
             return None
         addrs.append(raw.__array_interface__["data"][0])
@@ -470,13 +474,83 @@ def get_plan(model, variables, evidence_vars, col_of):
     return plan
 
 
-def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars):
-    """Yield (plan, rows, outputs-on-host) per evidence pattern."""
+def _ingest(model, data):
+    """(columns, col_of, evidence) of a frame: the zero-copy Categorical path when every column is
+    one, else the general encoder."""
     columns = list(data.columns)
     col_of = {c: i for i, c in enumerate(columns)}
     ev = ingest_columnar(model, data, columns)
     if ev is None:
         ev = ingest_frame(model, data, columns)
+    return columns, col_of, ev
+
+
+# frames of at least this many rows that are one evidence pattern of a fused plan take the direct path
+# (_fused_to_host: pinned staging both ways, outputs handed to the result frame without a copy)
+FAST_MIN_ROWS = int(os.environ.get("PGM_API_FAST_MIN_ROWS", 50_000))
+
+
+def _single_fused_plan(model, data, columns, col_of, ev, variables):
+    """The fused plan when the whole frame is ONE evidence pattern with no NaN column (so the query
+    variables are exactly `variables`, in order) and at least FAST_MIN_ROWS rows; else None."""
+    if len(ev.groups) != 1 or len(data) < FAST_MIN_ROWS:
+        return None
+    mask, _ = ev.groups[0]
+    if not mask.all():
+        return None
+    plan = get_plan(model, list(variables), columns, col_of)
+    if plan.kind != "fused" or list(plan.variables) != list(variables):
+        return None
+    return plan
+
+
+def _pinned(shape, dtype):
+    """A page-locked host array from torch's caching host allocator: DMA reads / writes it directly,
+    and its memory returns to the allocator's cache when the last array viewing it is freed (a
+    result frame built on it owns it)."""
+    import torch
+
+    t = torch.empty(shape, dtype=dtype, pin_memory=True)
+    return t.numpy()
+
+
+def _fused_to_host(plan, ev, columns, col_of, n, marginals):
+    """The direct path of a one-pattern frame: the plan's evidence columns (LUT-mapped straight into a
+    pinned staging buffer when the frame is categorical) uploaded, one launch of the fused pass, the
+    outputs DMA'd into pinned host memory that the caller keeps (no further copy), one synchronize.
+    Returns the marginals [n_acc, n] f64 or the MAP flat index [n] int32 (numpy, pinned)."""
+    import torch
+
+    L = N.lib()
+    s = N.stream_handle()
+    if isinstance(ev, ColumnarEvidence):
+        used = [col_of[v] for v in plan.ev_used]
+        stage = _pinned((max(1, len(used)), n), torch.uint8)
+        for i, j in enumerate(used):
+            np.take(ev.luts[j], ev.raws[j].view(np.uint8), out=stage[i])
+        dcodes = torch.empty(stage.shape, dtype=torch.uint8, device=E.device())
+        N.check(L.pgm_memcpy_h2d(N.ptr(dcodes), stage.ctypes.data_as(ctypes.c_void_p), stage.nbytes, s), "memcpy_h2d")
+        run_plan = plan.compact()
+    else:
+        dcodes = ev.rows_codes(ev.groups[0][1])
+        run_plan = plan
+    out = run_plan.alloc_outputs(n, marginals=marginals, map_=not marginals)
+    err = torch.zeros(1, dtype=torch.int32, device=dcodes.device)
+    run_plan.run(dcodes, n, 0, n, out, err=err)
+    key = "marg" if marginals else "map"
+    dev = out[key]
+    host = _pinned(tuple(dev.shape), dev.dtype)
+    herr = _pinned((1,), torch.int32)
+    N.check(L.pgm_memcpy_d2h_async(herr.ctypes.data_as(ctypes.c_void_p), N.ptr(err), 4, s), "memcpy_d2h")
+    N.check(L.pgm_memcpy_d2h(host.ctypes.data_as(ctypes.c_void_p), N.ptr(dev), host.nbytes, s), "memcpy_d2h")
+    if herr[0] != 0:
+        raise IndexError("evidence state code out of range")
+    return host
+
+
+def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars, ingested=None):
+    """Yield (plan, rows, outputs-on-host) per evidence pattern."""
+    columns, col_of, ev = ingested if ingested is not None else _ingest(model, data)
     for mask, rows in ev.groups:
         observed = [columns[j] for j in range(len(columns)) if mask[j]]
         nan_cols = [columns[j] for j in range(len(columns)) if not mask[j]]
@@ -509,16 +583,43 @@ def predict_probability_frame(model, data):
     n = len(data)
     if n == 0:  # the reference builds its frame from empty per-column lists: no columns at all
         return pd.DataFrame({}, index=data.index)
+    ingested = _ingest(model, data)
+    plan = _single_fused_plan(model, data, *ingested, order)
+    if plan is not None:
+        # one pattern: the marginals' rows ARE the result's columns (plan.variables == order, each
+        # variable's states consecutive), so the frame is built on the pinned output block, no copy
+        marg = _fused_to_host(plan, ingested[2], ingested[0], ingested[1], n, True)
+        names = [var + "_" + str(s) for var in order for s in model.get_cpds(var).state_names[var]]
+        assert len(names) == marg.shape[0]
+        return pd.DataFrame(marg.T, columns=names, index=data.index, copy=False)
     cols = {}
     for var in order:
         for s in model.get_cpds(var).state_names[var]:
             cols[var + "_" + str(s)] = np.empty(n)
-    for plan, rows, host in _run_groups(model, data, order, True, False, False):
+    for plan, rows, host in _run_groups(model, data, order, True, False, False, ingested):
         for i, var in enumerate(plan.variables[:len(order)]):
             a = plan.acc_off[i]
             for k, s in enumerate(plan.states[var]):
                 cols[var + "_" + str(s)][rows] = host["marg"][a + k]
     return pd.DataFrame(cols, index=data.index)
+
+
+def _append_columns(base, vals, order):
+    """base's columns then vals[c] for c in order, as a new frame.  PGM_API_APPEND=concat (A/B):
+    pd.concat of the two frames; default: a shallow copy of base (its column blocks shared, not
+    copied) with the new columns set on it."""
+    import warnings
+
+    import pandas as pd
+
+    if os.environ.get("PGM_API_APPEND", "shallow") == "concat":
+        return pd.concat([base, pd.DataFrame(vals, index=base.index, columns=order)], axis=1)
+    out = base.copy(deep=False)
+    with warnings.catch_warnings():  # a frame of ~1,000 categorical blocks is "fragmented" by design
+        warnings.simplefilter("ignore", pd.errors.PerformanceWarning)
+        for c in order:
+            out[c] = vals[c]
+    return out
 
 
 def predict_frame(model, data):
@@ -529,12 +630,23 @@ def predict_frame(model, data):
     order = list(missing_variables)
     if len(data) == 0:  # the reference indexes the first group of an empty groupby
         raise IndexError("list index out of range (predict on an empty DataFrame)")
+    ingested = _ingest(model, data)
+    plan = _single_fused_plan(model, data, *ingested, order)
+    if plan is not None:  # one pattern, no NaN cell: the MAP columns straight from the pinned index
+        idx = _fused_to_host(plan, ingested[2], ingested[0], ingested[1], len(data), False).astype(np.int64)
+        vals = {}
+        for i in reversed(range(len(plan.variables))):
+            var, c = plan.variables[i], plan.cards[i]
+            vals[var] = np.array(plan.states[var], dtype=object)[idx % c]
+            idx //= c
+        out = _append_columns(data, vals, order)
+        return out if out.index.is_monotonic_increasing else out.sort_index()
     vals = {c: np.full(len(data), np.nan, dtype=object) for c in order}
     # the observed columns keep their dtype (object frames stay object, as the reference's merge
     # leaves them; a categorical frame is not expanded to 10^8 Python objects)
     base = data
     filled = {}  # observed columns whose NaN cells receive MAP states, as in the reference
-    for plan, rows, host in _run_groups(model, data, order, False, True, True):
+    for plan, rows, host in _run_groups(model, data, order, False, True, True, ingested):
         idx = host["map"].astype(np.int64)
         # decode the flat index (C-order over plan.variables, last fastest)
         for i in reversed(range(len(plan.variables))):
@@ -552,7 +664,7 @@ def predict_frame(model, data):
         base = base.assign(**filled)  # a new frame: the caller's data is not modified
     # the observed columns (object, as the reference's merge leaves them), then the MAP columns in the
     # reference's set order, rows sorted by index (DiscreteBayesianNetwork.py:895-910)
-    out = pd.concat([base, pd.DataFrame(vals, index=data.index, columns=order)], axis=1)
+    out = _append_columns(base, vals, order)
     if out.index.is_monotonic_increasing:
         return out
     return out.sort_index()

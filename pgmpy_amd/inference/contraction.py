@@ -24,8 +24,9 @@ side keeping >= 16 states) run on FP64 MFMA instead (pgm_gemm, engine.pair_gemm)
 and executor run single queries (C2) and row batches.
 """
 import heapq
-from functools import partial
+import threading
 from collections import OrderedDict
+from functools import partial
 from itertools import count
 
 import numpy as np
@@ -329,6 +330,7 @@ def plan_stats(operand_labels, out_labels, dims):
 
 
 _PATHS = OrderedDict()  # compiled paths, keyed on the operands' (label, cardinality) structure
+_PATHS_LOCK = threading.Lock()
 PACK_MAX_OUT = 4096       # pack the operands of non-GEMM steps with at most this many outputs ...
 PACK_MIN_WORK = 1 << 20   # ... and at least this large an index space
 PATH_CACHE_SIZE = 256
@@ -341,10 +343,11 @@ def compiled_path(operand_labels, out_labels, dims, order=None):
     nothing."""
     key = (tuple(tuple((l, int(dims[l])) for l in ls) for ls in operand_labels), tuple(out_labels),
            None if order is None else tuple(order))
-    hit = _PATHS.get(key)
-    if hit is not None:
-        _PATHS.move_to_end(key)
-        return hit
+    with _PATHS_LOCK:  # concurrent queries (engine.device_lock is shared) share this cache
+        hit = _PATHS.get(key)
+        if hit is not None:
+            _PATHS.move_to_end(key)
+            return hit
     if order is None:
         steps, final_id = choose_path(operand_labels, out_labels, dims)
     else:
@@ -380,9 +383,10 @@ def compiled_path(operand_labels, out_labels, dims, order=None):
             levels.append([])
         levels[d - 1].append(k)
     hit = (plan, final_id, levels)
-    _PATHS[key] = hit
-    if len(_PATHS) > PATH_CACHE_SIZE:
-        _PATHS.popitem(last=False)
+    with _PATHS_LOCK:
+        _PATHS[key] = hit
+        if len(_PATHS) > PATH_CACHE_SIZE:
+            _PATHS.popitem(last=False)
     return hit
 
 

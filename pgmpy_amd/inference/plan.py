@@ -561,6 +561,31 @@ class PatternPlan:
         progs[(n, outs, host_io)] = hit
         return hit
 
+    def prepare_steps(self, n, outs, host_io=False):
+        """Build (and capture) the steps program for (n, outs, host_io) unless it exists.  The capture
+        holds engine.device_lock exclusively, taken BEFORE this plan's own lock: a thread inside a
+        public call gives its shared hold up while it waits, and holds no per-plan lock then, so no
+        thread holding the device lock shared can be waiting for a lock this one holds."""
+        progs = self.__dict__.get("_progs")
+        if progs is not None and (n, outs, host_io) in progs:
+            return
+        with E.device_lock.exclusive():
+            with self._lock:
+                self._steps_program(n, outs, host_io)
+
+    def prepare_run(self, n_rows, keys):
+        """Every captured program run(n_rows rows, outputs `keys`) will replay, built now (see
+        prepare_steps): callers that take a lock of their own around run() call this first."""
+        keys = set(keys)
+        if self.kind == "fused":
+            if "joint" not in keys or self.joint_fused_ok:
+                return
+            keys = {"joint"}
+        outs = frozenset(k for k in ("marg", "joint", "map") if k in keys)
+        chunk = self._steps_chunk(n_rows)
+        for n in {min(chunk, n_rows - c0) for c0 in range(0, n_rows, chunk)}:
+            self.prepare_steps(n, outs)
+
     def query_one(self, codes, key):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v, already checked
         against the state names on the host) through the steps program whose codes and result live in
@@ -582,6 +607,10 @@ class PatternPlan:
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
         """Batched greedy contraction with an evidence-row axis: rows in chunks, each chunk one
         replay of a compiled program (_steps_program)."""
+        outs = frozenset(k for k in ("marg", "joint", "map") if k in out)
+        chunk = self._steps_chunk(n_rows)
+        for n in {min(chunk, n_rows - c0) for c0 in range(0, n_rows, chunk)}:
+            self.prepare_steps(n, outs)  # captures first, before this plan's lock
         with self._lock:  # the compiled programs own their scratch buffers: one caller at a time
             return self._run_steps_locked(codes, ld, row0, n_rows, out, err)
 
@@ -655,6 +684,11 @@ class QueryRunner:
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
         the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
         L = N.lib()
+        # any program the query replays is captured before this runner's lock is taken (engine.DeviceLock)
+        if self.plan.kind != "fused":
+            self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
+        else:
+            self.plan.prepare_run(1, [self.key])
         with self.lock:
             if self.plan.kind != "fused":  # host copies inside the captured graph: one launch + one sync
                 return self.plan.query_one(codes, self.key)
@@ -768,6 +802,7 @@ class RowRing:
         self._base = base.value
         self.outs = outs
         self.n_rows = int(n_rows)
+        self.n_slots = n
 
     def start(self, n_batches, timeout_s=5.0, wait_ready=False):
         """Launch for n_batches batches; wait_ready=True returns only once every workgroup of the
@@ -784,7 +819,9 @@ class RowRing:
 
     def post(self, n_posted):
         """Publish batches [0, n_posted) of the running launch: one store into the pinned counter
-        (pgm_rows_ring_counter; the same as pgm_rows_ring_post without a library call)."""
+        (pgm_rows_ring_counter; the same as pgm_rows_ring_post without a library call).  Batch b runs on
+        slot b % n_slots: a caller refilling a slot for batch b + n_slots must know batch b is done
+        (finish() of the launch that ran it); within one launch, repeats of a slot read the same inputs."""
         if not self._posted <= n_posted <= self._n:
             st = self._post(self._h, int(n_posted))  # the library reports the misuse
             N.check(st, "rows_ring_post")
@@ -807,8 +844,15 @@ class RowRing:
                 "rows_ring_kernel")
         return name.value.decode(), nb.value, wg.value
 
-    def run(self, n_batches, timeout_s=5.0):
-        """start + post every batch + finish (one resident launch over n_batches batches)."""
+    def run(self, n_batches, timeout_s=5.0, replay=False):
+        """start + post every batch + finish (one resident launch over n_batches batches).  Batches are
+        posted at once, so batch b and batch b + n_slots may run concurrently on the same slot:
+        n_batches > n_slots is refused unless replay=True, the caller's statement that every slot's
+        inputs stay unchanged for the whole launch (the repeats then write identical outputs — a
+        bandwidth measurement, bench.py's single-launch roofline)."""
+        if int(n_batches) > self.n_slots and not replay:
+            raise ValueError(f"RowRing.run: {n_batches} batches over {self.n_slots} slots would run a slot's "
+                             f"repeats concurrently; refill slots between launches or pass replay=True")
         self.start(n_batches, timeout_s)
         try:
             for b in range(1, int(n_batches) + 1):

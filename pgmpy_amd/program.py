@@ -678,13 +678,20 @@ class Program:
         s = N.stream_handle(stream)
         if self._graph is not None:
             N.check(N.lib().pgm_graph_launch(self._graph, s), "graph_launch")
-            return
-        for step in self._steps:
-            step(s)
+        else:
+            for step in self._steps:
+                step(s)
+        if self._chains and self.barrier_timed_out():
+            # a levelled batch's grid barrier (A/B knob PGM_BATCH_LEVELS=1) needs every workgroup of its
+            # persistent grid resident at once; when other work held CUs it gave up after its deadline and
+            # the later levels did not run (barrier_timed_out has reset its words for the next replay)
+            raise RuntimeError("levelled batch: the grid barrier timed out (workgroups not co-resident); "
+                               "the outputs of this run are incomplete")
 
-    @E.serialized
+    @E.exclusive
     def capture(self):
-        """Record the steps into one HIP graph (captured on a private stream, under engine.device_lock)."""
+        """Record the steps into one HIP graph (captured on a private stream, holding engine.device_lock
+        exclusively: no other thread launches while the stream captures)."""
         import torch
 
         if self._graph is not None:

@@ -88,7 +88,7 @@ def test_two_rank_gather_matches_single_rank(tmp_path):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_hip_predict_matches_golden(tmp_path, world):
     """The sharded HIP path of C5 (BASELINE.json configs[4]) at world 2 and 3 (uneven blocks):
-    each rank runs the bound fused row plan on its block of the 1,000 reference munin rows, the
+    each rank runs the bound fused row plan on its block of the 2,000 reference munin rows, the
     [17, rows] marginals and MAP indices are gathered to rank 0; the gathered result must equal
     the single-launch run bit for bit and the reference fixture (marginals 1e-6 relative, MAP
     exact).  With a GPU per rank the gather is RCCL (world 1 on the one-GPU box: a one-rank RCCL
@@ -122,3 +122,38 @@ def test_sharded_hip_predict_matches_golden(tmp_path, world):
         idx //= c
     got = np.stack([digits[v] for v in g["missing"]], axis=1)
     np.testing.assert_array_equal(got, g["map_codes"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_host_delivery_matches_golden(tmp_path, world):
+    """C5's default delivery (bench.py --c5-delivery host): no gather — every rank DMAs its block's
+    marginals and MAP indices into pinned host memory through pgmpy_amd.distributed.HostDelivery
+    (double-buffered, copies overlapping the next launch); the blocks, reassembled in rank order, equal
+    the reference fixture's 2,000 rows (marginals 1e-6 relative, MAP exact).  World 2 on the one-GPU box:
+    two ranks sharing the card (gloo process group, no collective on the data path)."""
+    import subprocess
+    import sys
+
+    from tests.goldens import munin_predict
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "host")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(root, "tests", "workers", "sharded_predict.py"), out, "host"]
+    r = subprocess.run(cmd, cwd=root, timeout=240, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    parts = [np.load(f"{out}.rank{k}.npz") for k in range(world)]
+    assert [int(p["lo"]) for p in parts] == sorted(int(p["lo"]) for p in parts)
+    assert int(parts[0]["lo"]) == 0 and all(int(a["hi"]) == int(b["lo"]) for a, b in zip(parts, parts[1:]))
+    marg = np.concatenate([p["marg"] for p in parts], axis=1)
+    mp = np.concatenate([p["map"] for p in parts])
+    g = munin_predict()
+    assert marg.shape[1] == g["codes"].shape[1] == int(parts[-1]["hi"])
+    np.testing.assert_allclose(marg.T, g["prob"], rtol=1e-6, atol=1e-300)
+    digits = {}
+    for v, c in reversed(list(zip(parts[0]["variables"], [int(c) for c in parts[0]["cards"]]))):
+        digits[str(v)] = mp % c
+        mp = mp // c
+    np.testing.assert_array_equal(np.stack([digits[v] for v in g["missing"]], axis=1), g["map_codes"])

@@ -417,6 +417,67 @@ def test_program_hazard_check_catches_undeclared_and_unordered_access():
     assert any("without an ordering" in m for m in prog.check_hazards())
 
 
+def test_device_lock_readers_writer_semantics():
+    """engine.DeviceLock (SURVEY §8(b) threading): shared holds overlap across threads, an exclusive
+    hold excludes everyone, holds nest, and two threads that each hold it shared and then ask for it
+    exclusively (a capture inside a public call) both get it in turn instead of deadlocking."""
+    import threading
+    import time
+
+    from pgmpy_amd.engine import DeviceLock
+
+    lk = DeviceLock()
+    inside, peak, errors = [0], [0], []
+    gate = threading.Barrier(4)
+
+    def reader():
+        with lk.shared():
+            with lk.shared():  # re-entrant
+                gate.wait(timeout=5)  # all four readers inside at once
+                inside[0] += 1
+                peak[0] = max(peak[0], inside[0])
+                time.sleep(0.01)
+                inside[0] -= 1
+
+    ts = [threading.Thread(target=reader) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(10)
+    assert lk.peak_readers == 4 and peak[0] >= 2
+
+    order = []
+
+    def upgrader(tag):
+        try:
+            with lk.shared():
+                time.sleep(0.02)
+                with lk.exclusive():  # gives the shared hold up while waiting
+                    order.append((tag, "in"))
+                    with lk.shared():  # shared inside exclusive: free
+                        pass
+                    with lk.exclusive():  # nested exclusive
+                        pass
+                    time.sleep(0.01)
+                    order.append((tag, "out"))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=upgrader, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(10)
+    assert not any(t.is_alive() for t in ts), "deadlock"
+    assert not errors
+    # exclusive sections did not interleave
+    assert [o[1] for o in order] == ["in", "out", "in", "out"] and order[0][0] == order[1][0]
+    # after everything: free for a new exclusive holder at once
+    done = threading.Event()
+    threading.Thread(target=lambda: (lk.acquire_exclusive(), lk.release_exclusive(), done.set())).start()
+    assert done.wait(5)
+
+
 def test_hip_backend_config_mirrors_pgmpy_config():
     """pgmpy_amd.compat.Config: pgmpy's set_backend validation (global_vars.py:82-122) plus "hip";
     without a device the hip backend fails loudly (no CPU fallback)."""

@@ -5,6 +5,9 @@ Every rank runs the HIP fused row plan (bound launch, as bench.py --workload c5)
 block of the 2,000 reference munin template rows (tests/golden/munin_predict.npz), the marginals and
 MAP indices are gathered to rank 0 (nccl = RCCL when every rank has its own GPU, else gloo through
 host memory), and rank 0 also runs all rows in one launch and saves both for the test to compare.
+With a third argument "host" no result is gathered: every rank delivers its block's marginals and MAP
+indices into pinned host memory (pgmpy_amd.distributed.HostDelivery, the C5 default of bench.py) and
+saves them to OUT.rank<r>.npz with its row bounds; the test reassembles the blocks.
 """
 import os
 import sys
@@ -16,7 +19,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def main(out_path):
+def main(out_path, mode="gather"):
     import torch
     import torch.distributed as dist
 
@@ -57,6 +60,32 @@ def main(out_path):
         assert int(err.item()) == 0
         return out
 
+    if mode == "host":
+        from pgmpy_amd.distributed import HostDelivery
+
+        block = np.ascontiguousarray(codes[:, lo:hi])
+        m = block.shape[1]
+        d = upload_codes(block)
+        outs = [plan.alloc_outputs(m, marginals=True, map_=True) for _ in range(2)]
+        err = torch.zeros(1, dtype=torch.int32, device=d.device)
+        ls = torch.cuda.Stream()
+        bounds = [plan.bind(d, m, 0, m, o, err=err, stream=ls) for o in outs]
+        dm = HostDelivery(tuple(outs[0]["marg"].shape), torch.float64, device=d.device)
+        dp = HostDelivery(tuple(outs[0]["map"].shape), torch.int32, device=d.device)
+        for k in range(5):  # consecutive steps through the double buffers, copies overlapping launches
+            dm.acquire(k, ls)
+            dp.acquire(k, ls)
+            bounds[k % 2].run()
+            dm.deliver(k, outs[k % 2]["marg"], ls)
+            dp.deliver(k, outs[k % 2]["map"], ls)
+        hm, hp = dm.wait(4), dp.wait(4)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        np.savez(f"{out_path}.rank{rank}.npz", lo=lo, hi=hi, marg=hm.numpy(), map=hp.numpy().astype(np.int64),
+                 backend="nccl" if nccl else "gloo", variables=np.array(variables), cards=np.array(plan.cards))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     mine = run(np.ascontiguousarray(codes[:, lo:hi]))
     marg = mine["marg"] if nccl else mine["marg"].cpu()
     mp = mine["map"].to(torch.int64)
@@ -74,4 +103,4 @@ def main(out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])

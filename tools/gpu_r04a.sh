@@ -7,8 +7,8 @@ TAG=${1:-r04a}
 line() {  # file label
   python -c "import json,sys; d=json.load(open('$1')); r=d['roofline']; s=r.get('single_launch_ring') or {}; print('$2', round(d['value']/1e9,2), 'G', 'frac', round(r['frac'],3), 'wall', round(r['frac_wall'],3), 'ws/mall', round(r['working_set_over_mall'],2), 'ring', round(s.get('frac',0),3), round(s.get('kernel_ms',0),4), 'ring ws/mall', round(s.get('working_set_over_mall',0),2))"
 }
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_hazards_gpu.py > gpurun_out/${TAG}_hazards0.log 2>&1 || { echo hazard tests failed; tail -60 gpurun_out/${TAG}_hazards0.log; }
-tail -3 gpurun_out/${TAG}_hazards0.log
+
+
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench96_full.json 2> gpurun_out/${TAG}_bench96_full.err || { tail -30 gpurun_out/${TAG}_bench96_full.err; exit 1; }
 line gpurun_out/${TAG}_bench96_full.json b96_full
 for B in 24 48 96; do
