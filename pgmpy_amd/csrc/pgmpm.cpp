@@ -197,6 +197,50 @@ static int pm_knob(const char *name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// Decode order of a step's kept outer dims, fastest first (the last one is the slowest: with the XCD
+// grouping each XCD takes a contiguous range of it).  Default: the belief's own order (its fastest
+// dim fastest, so a block's neighbours write neighbouring addresses).  PGM_PM_KREV=1: reversed.
+// PGM_PM_XPART=1: the kept dim carried by the most row-operand bytes becomes the slowest, so each XCD
+// reads a disjoint slice of every operand that carries it (instead of all 8 re-reading an operand that
+// lacks the belief's slowest dim); =2: in addition the other dims vary fastest in order of the bytes
+// that carry them (least first), so consecutive blocks re-read the same operand entries while they are
+// in the XCD's L2.  cards[q], bytes_of(q) = row-operand bytes that vary along kept dim q.
+template <class BytesOf>
+static std::vector<int> pm_kept_order(int kx, const unsigned *cards, BytesOf bytes_of) {
+  static const int krev = pm_knob("PGM_PM_KREV", 0);
+  static const int xpart = pm_knob("PGM_PM_XPART", 0);
+  std::vector<int> ord;
+  for (int qi = 0; qi < kx; ++qi) ord.push_back(krev ? qi : kx - 1 - qi);
+  if (!xpart || kx < 2) return ord;
+  int p = -1;
+  double best = -1.0;
+  for (int q = 0; q < kx; ++q) {
+    if (cards[q] < 2) continue;
+    const double b = bytes_of(q);
+    if (b > best || (b == best && p >= 0 && cards[q] > cards[p])) best = b, p = q;
+  }
+  if (p < 0) return ord;
+  ord.erase(std::find(ord.begin(), ord.end(), p));
+  if (xpart == 2)
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return bytes_of(a) < bytes_of(b); });
+  ord.push_back(p);
+  return ord;
+}
+
+// blocks that share an XCD (b % 8, the dispatcher's round robin) take consecutive tiles: XCD label x
+// gets tiles [x q + min(x, r), ...) with q = total / 8, r = total % 8 — a bijection for any total
+// (the plain (b % 8) q + b / 8 only when 8 divides total)
+static std::string pm_xcd_remap(uint64_t total) {
+  const unsigned long long q = total / 8, r = total % 8;
+  std::string o;
+  if (r == 0)
+    pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n", q);
+  else
+    pgmi_appendf(o, "  { const unsigned x = b %% 8u, y = b / 8u; b = (x < %lluu ? x * %lluu : %lluu + (x - %lluu) * %lluu) + y; }"
+                    "  // blocks of one XCD are consecutive tiles\n", r, q + 1, r * (q + 1), r, q);
+  return o;
+}
+
 // body `name` of one step: a device function of its block index within the step
 static std::string pm_body(const PMSpec &sp, const std::string &name) {
   const ProdMK &k = sp.k;
@@ -209,8 +253,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
              "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
              "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
   o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
-  if (xcd) pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;  // blocks of one XCD are consecutive tiles\n",
-                   (unsigned long long)(total / 8));
+  if (xcd) o += pm_xcd_remap(total);
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
   if (store && sp.wt)
     o += "  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0x7fffffff, 0x00020000);\n";
@@ -218,10 +261,23 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   for (int i = 0; i < k.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)oc; (void)idx;\n";
   const int kx = k.nk - 1;  // kept outer dims 0..kx-1 (kx-1 fastest), the row dim last
-  // PGM_PM_KREV=1: dim 0 fastest instead (consecutive tiles then share the trailing dims; A/B knob)
-  static const int krev = pm_knob("PGM_PM_KREV", 0);
-  for (int qi = 0; qi < kx; ++qi) {
-    const int q = krev ? qi : kx - 1 - qi;
+  unsigned kc[KMAX] = {};
+  for (int q = 0; q < kx; ++q) kc[q] = k.kdiv[q].d;
+  auto op_bytes = [&](int i) {  // entries of operand i over the step's index space (rows included)
+    double b = k.vec[i] ? 16.0 * k.NP : 8.0;
+    for (int q = 0; q < kx; ++q)
+      if (k.ks[i][q]) b *= kc[q];
+    for (int r = 0; r < k.nr; ++r)
+      if (k.rs[i][r]) b *= k.rdiv[r].d;
+    return b;
+  };
+  const std::vector<int> kord = pm_kept_order(kx, kc, [&](int q) {
+    double t = 0.0;
+    for (int i = 0; i < k.n_ops; ++i)
+      if (k.vec[i] && k.ks[i][q]) t += op_bytes(i);
+    return t;
+  });
+  for (int q : kord) {
     const unsigned dq = k.kdiv[q].d;
     pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", dq, dq);
     if (k.ksc[q]) pgmi_appendf(o, " oc += (long long)g * %lldLL;", (long long)k.ksc[q]);
@@ -368,14 +424,28 @@ static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
              "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
              "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
   o += "  (void)o1; (void)o2; (void)o3;\n";
-  if (sp.xcd) pgmi_appendf(o, "  b = (b %% 8u) * %lluu + b / 8u;\n", (unsigned long long)(sp.total / 8));
+  if (sp.xcd) o += pm_xcd_remap(sp.total);
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", sp.gx, sp.gx);
   o += "  unsigned idx = ob;\n  long long m1 = 0, m2 = 0";
   for (int i = 0; i < q.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)idx;\n";
-  static const int krev = pm_knob("PGM_PM_KREV", 0);
-  for (int di = 0; di < q.nK; ++di) {
-    const int d = krev ? di : q.nK - 1 - di;
+  auto op_bytes = [&](int i) {
+    double b = q.vec[i] ? 16.0 * q.NP : 8.0;
+    for (int d = 0; d < q.nK; ++d)
+      if (q.ks[i][d]) b *= q.kcard[d];
+    for (int d = 0; d < q.nU; ++d)
+      if (q.us[i][d]) b *= q.ucard[d];
+    for (int d = 0; d < q.nZ; ++d)
+      if (q.zs[i][d]) b *= q.zcard[d];
+    return b;
+  };
+  const std::vector<int> kord = pm_kept_order(q.nK, q.kcard, [&](int d) {
+    double t = 0.0;
+    for (int i = 0; i < q.n_ops; ++i)
+      if (q.vec[i] && q.ks[i][d]) t += op_bytes(i);
+    return t;
+  });
+  for (int d : kord) {
     pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", q.kcard[d], q.kcard[d]);
     if (q.k1[d]) pgmi_appendf(o, " m1 += (long long)g * %lldLL;", (long long)q.k1[d]);
     if (q.k2[d]) pgmi_appendf(o, " m2 += (long long)g * %lldLL;", (long long)q.k2[d]);
@@ -661,7 +731,8 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.unroll = unroll;
   sp.store = C != nullptr;
   sp.has_m = has_m;
-  sp.xcd = xcd_knob && total % 8 == 0;
+  // PGM_PM_XCD: 1 = XCD grouping when the block count is a multiple of 8, 2 = always (bijective remap)
+  sp.xcd = xcd_knob >= 2 || (xcd_knob == 1 && total % 8 == 0);
   sp.nt = nt != 0;
   sp.wt = wt != 0 && sp.store && entries * 8ull + 64ull < (1ull << 31);
   sp.gx = (unsigned)gx;
@@ -788,7 +859,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
   sp.store = false;
   sp.gx = (sp.mm.NP + 255) / 256;
   sp.total = (uint64_t)sp.gx * sp.mm.n_outer;
-  sp.xcd = pm_knob("PGM_PM_XCD", 1) && sp.total % 8 == 0;
+  sp.xcd = pm_knob("PGM_PM_XCD", 1) >= 2 || (pm_knob("PGM_PM_XCD", 1) == 1 && sp.total % 8 == 0);
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;
   const std::string src = pm_source({sp}, starts, &blocks);

@@ -42,6 +42,10 @@ LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
 # 0.082-0.084): a tiny level's cost is its dependent load chain, not the launch, so it stays an A/B knob
 # (0 = off, the default; the test sets it).
 WG_CHAIN_BLOCKS = int(os.environ.get("PGM_WG_CHAIN_BLOCKS", 0))
+# a plain Program's batch of ONE job: the job's own launch (pgm_contract / pgm_gather: the planner may
+# split a long reduction; the descriptor travels by value in the kernel arguments) or, with
+# PGM_ONE_JOB_AS_BATCH=1 (A/B knob), a one-job pgm_batch launch (descriptor in device memory)
+ONE_JOB_AS_BATCH = os.environ.get("PGM_ONE_JOB_AS_BATCH", "0") == "1"
 # n-ary products with more operands than one kernel takes: balanced tree (default) or sequential fold
 # (PGM_PRODN_TREE=0, A/B knob)
 TREE_PRODUCTS = os.environ.get("PGM_PRODN_TREE", "1") != "0"
@@ -157,7 +161,7 @@ class Program:
 
     def _batch_step(self, b):
         L = N.lib()
-        if len(b.jobs) == 1:  # a batch of one is just the job (with its own planner's launch)
+        if len(b.jobs) == 1 and not ONE_JOB_AS_BATCH:  # a batch of one is just the job (its own planner's launch)
             kind, _, args = b.jobs[0]
             if kind == "contract":
                 return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), f"{kind} (batch of one)"

@@ -5,6 +5,8 @@ Each kernel is checked against the numpy arithmetic the reference itself runs
 771-777; compat_fns.py:53-74).  Tolerance: 1e-12 relative for sums (fp64,
 different summation order), exact for copies, max and argmax.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -938,3 +940,28 @@ def test_two_marginals_one_pass(gpu, rows, red, ratio):
     f = np.sum if red == "sum" else np.max
     np.testing.assert_allclose(E.to_host(Ms[0]), f(full, axis=(2, 3)), rtol=1e-13)
     np.testing.assert_allclose(E.to_host(Ms[1]), f(full, axis=(0, 1)), rtol=1e-13)
+
+
+@pytest.mark.parametrize("env", [{"PGM_PM_XCD": "2"}, {"PGM_PM_XPART": "1"}, {"PGM_PM_XPART": "2", "PGM_PM_XCD": "2"},
+                                 {"PGM_PM_KREV": "1"}])
+def test_bp_block_order_knobs_bit_exact(gpu, tmp_path, env):
+    """The block-to-tile order knobs of the specialised batched-BP steps (bijective XCD grouping of any
+    block count, the XCD partition along the kept dim the row operands carry, the reversed decode)
+    only change which block computes which output: every clique belief of a 1,002-row pathfinder
+    calibration is bit-identical to the default order's (separate processes: the knobs are read once)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    worker = os.path.join(root, "tests", "workers", "c4_variant.py")
+    outs = []
+    for e in ({}, env):
+        out = str(tmp_path / f"c4_{len(outs)}.npz")
+        r = subprocess.run([sys.executable, worker, out], cwd=root, env={**os.environ, **e}, timeout=240,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(np.load(out))
+    a, b = outs
+    assert sorted(a.files) == sorted(b.files) and len(a.files) == 103
+    for k in a.files:
+        assert np.array_equal(a[k], b[k], equal_nan=True), k

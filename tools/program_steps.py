@@ -43,6 +43,8 @@ def main():
         (prog, *_), = runner.plan._progs.values()
     res = prog.time_steps()
     tot = sum(us for us, _ in res)
+    if not prog._levels:
+        job_detail(prog, res)
     import torch
 
     prog.run()
@@ -90,6 +92,22 @@ def main():
     top = int(os.environ.get("TOP", "25"))
     for us, note in sorted(res, key=lambda r: -r[0])[:top]:
         print(f"{us:9.1f} us  {note[:220] if len(sys.argv) < 4 else note}")
+
+
+def job_detail(prog, res, top=6):
+    """Plain program: the jobs of the slowest steps (_plain_recs grouped by launch, in launch order),
+    each with the bytes its footprint spans (hazard.py)."""
+    units = sorted({r.step for r in prog._plain_recs})
+    if len(units) != len(res):
+        return
+    by = {}
+    for r in prog._plain_recs:
+        by.setdefault(r.step, []).append(r)
+    for i in sorted(range(len(res)), key=lambda i: -res[i][0])[:top]:
+        jobs = by[units[i]]
+        print(f"{res[i][0]:8.1f} us  {res[i][1][:60]}")
+        for r in sorted(jobs, key=lambda r: -sum(hi - lo for lo, hi, _ in r.foot or []))[:8]:
+            print(f"           {sum(hi - lo for lo, hi, _ in r.foot or []) / 1e6:8.3f} MB  {r.note[:110]}")
 
 
 if __name__ == "__main__":
