@@ -312,10 +312,20 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+class _HostBytes:
+    """The bytes of a HostBuffer as an __array_interface__ exporter that keeps the buffer alive: numpy
+    arrays made from it (and their views) hold the memory, so it is freed only when the HostBuffer and
+    every array on it are gone."""
+
+    def __init__(self, owner, ptr, nbytes):
+        self._owner = owner
+        self.__array_interface__ = {"data": (ptr, False), "shape": (nbytes,), "typestr": "|u1", "version": 3}
+
+
 class HostBuffer:
     """Pinned, mapped, coherent host memory that kernels read and write directly (pgm_host_alloc):
     `array` (numpy) and `tensor` (a CPU torch view of the same bytes, for descriptor building) share
-    it; freed with the object."""
+    it; freed once the object and every array / tensor viewing it are gone (the arrays reference it)."""
 
     def __init__(self, shape, dtype):
         import torch
@@ -324,10 +334,11 @@ class HostBuffer:
         dtype = np.dtype(dtype)
         n = int(np.prod(shape)) if len(shape) else 1
         p = ctypes.c_void_p()
-        check(L.pgm_host_alloc(ctypes.byref(p), max(1, n * dtype.itemsize)), "host_alloc")
+        nbytes = max(1, n * dtype.itemsize)
+        check(L.pgm_host_alloc(ctypes.byref(p), nbytes), "host_alloc")
         self._p = p
-        raw = (ctypes.c_char * max(1, n * dtype.itemsize)).from_address(p.value)
-        self.array = np.frombuffer(raw, dtype=dtype, count=n).reshape(shape)
+        raw = np.asarray(_HostBytes(self, p.value, nbytes))
+        self.array = raw[:n * dtype.itemsize].view(dtype).reshape(shape)
         self.tensor = torch.from_numpy(self.array)
 
     def __del__(self):

@@ -53,6 +53,23 @@ class DiscreteFactor(BaseFactor, StateNameMixin):
             self._dev = None
         super(DiscreteFactor, self).store_state_names(variables, cardinality, state_names)
 
+    @classmethod
+    def _trusted(cls, variables, cardinality, values, tables):
+        """Internal constructor for results the engine built itself (compiled query answers): the
+        arguments are already consistent (a host fp64 array of the right size, distinct variables),
+        so the constructor's checks and the state tables are skipped — `tables` maps each variable to
+        a StateTable the caller keeps; the factor gets its own copies of the three dicts, as __init__
+        gives it."""
+        self = cls.__new__(cls)
+        self.variables = list(variables)
+        self.cardinality = np.array(cardinality, dtype=int)
+        self._host = values.reshape(tuple(int(c) for c in cardinality))
+        self._dev = None
+        self.state_names = {v: list(tables[v].names) for v in self.variables}
+        self.name_to_no = {v: dict(tables[v].to_no) for v in self.variables}
+        self.no_to_name = {v: dict(tables[v].to_name) for v in self.variables}
+        return self
+
     # ------------------------------------------------------------------ storage
     # Two copies may exist: `_dev` (fp64 device tensor) and `_host` (ndarray).  A host array that
     # has been handed to the caller (`values` getter, or an array passed to the setter) may be

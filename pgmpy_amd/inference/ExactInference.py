@@ -233,14 +233,18 @@ class VariableElimination(Inference):
         if codes is None:
             codes = [model.get_cpds(v).get_state_no(v, evidence[v]) for v in ev_vars]
         vals = runner.run(codes)
-        states = {v: model.get_cpds(v).state_names[v] for v in variables}
+        # state tables of the query variables, taken once per runner like the code tables above
+        qtabs = runner.__dict__.get("_query_tables")
+        if qtabs is None:
+            from ..utils.state_name import StateTable
+
+            qtabs = runner._query_tables = {v: StateTable(model.get_cpds(v).state_names[v]) for v in variables}
         if joint:
-            return DiscreteFactor(list(variables), list(plan.cards), vals,
-                                  state_names={v: states[v] for v in variables})
+            return DiscreteFactor._trusted(variables, plan.cards, vals, qtabs)
         res = {}
         for i, v in enumerate(variables):
             a = plan.acc_off[i]
-            res[v] = DiscreteFactor([v], [plan.cards[i]], vals[a:a + plan.cards[i]], state_names={v: states[v]})
+            res[v] = DiscreteFactor._trusted([v], [plan.cards[i]], vals[a:a + plan.cards[i]], qtabs)
         return res
 
     @E.serialized
