@@ -202,8 +202,16 @@ class VariableElimination(Inference):
         recompiles.  Thread-safe: the cache is locked and each runner serialises its own buffers."""
         from .plan import PatternPlan, QueryRunner
 
-        ev_vars = sorted(evidence, key=str)
-        key = (tuple(variables), tuple(ev_vars), bool(joint))
+        ek = tuple(evidence)  # the sorted evidence variables, cached per insertion order (C2: 100 names)
+        sorted_cache = self.__dict__.get("_ev_sorted")
+        if sorted_cache is None:
+            sorted_cache = self.__dict__.setdefault("_ev_sorted", {})
+        ev_vars = sorted_cache.get(ek)
+        if ev_vars is None:
+            if len(sorted_cache) >= 256:
+                sorted_cache.clear()
+            ev_vars = sorted_cache[ek] = tuple(sorted(evidence, key=str))
+        key = (tuple(variables), ev_vars, bool(joint))
         lock = self.__dict__.get("_compiled_lock")
         if lock is None:
             lock = self.__dict__.setdefault("_compiled_lock", threading.Lock())
@@ -211,7 +219,7 @@ class VariableElimination(Inference):
             cache = self.__dict__.setdefault("_compiled", {})
             runner = cache.pop(key, None)
             if runner is None or not runner.plan.is_current():
-                plan = PatternPlan(self.model, variables, ev_vars, {v: i for i, v in enumerate(ev_vars)})
+                plan = PatternPlan(self.model, variables, list(ev_vars), {v: i for i, v in enumerate(ev_vars)})
                 runner = QueryRunner(plan, joint)
                 while len(cache) >= 64:
                     cache.pop(next(iter(cache)))

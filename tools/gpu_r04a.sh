@@ -12,7 +12,7 @@ line() {  # file label
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench96_full.json 2> gpurun_out/${TAG}_bench96_full.err || { tail -30 gpurun_out/${TAG}_bench96_full.err; exit 1; }
 line gpurun_out/${TAG}_bench96_full.json b96_full
 for B in 24 48 96; do
-  for R in 1 2; do
+  for R in 1; do
     timeout -k 10 300 python bench.py --steps 20 --warmup 5 --batches $B --no-cpu-baseline --no-api-e2e > gpurun_out/${TAG}_bench${B}_$R.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
     line gpurun_out/${TAG}_bench${B}_$R.json b${B}_$R
   done
