@@ -136,6 +136,28 @@ def serialized(fn):
     return wrapper
 
 
+_tls_stream = threading.local()
+
+
+def thread_stream():
+    """This thread's own HIP stream (a torch.cuda.Stream per thread and device, non-blocking): compiled
+    single queries replay and wait on it, so concurrent threads neither order their launches behind
+    each other nor wait for each other's work (a spin on the shared default stream waits for every
+    thread's launches).  Created after the default stream has drained, so buffers that work queued
+    there initialised are complete before the first launch on it."""
+    import torch
+
+    d = torch.cuda.current_device()
+    per = getattr(_tls_stream, "by_dev", None)
+    if per is None:
+        per = _tls_stream.by_dev = {}
+    s = per.get(d)
+    if s is None:
+        torch.cuda.current_stream().synchronize()
+        s = per[d] = torch.cuda.Stream(device=d)
+    return s
+
+
 def exclusive(fn):
     """Run `fn` holding device_lock exclusively (HIP graph captures)."""
 

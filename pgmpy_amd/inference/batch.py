@@ -288,15 +288,18 @@ def _frame_categoricals(data, columns):
     try:
         mgr = data._mgr
         arrays, blknos, blklocs = mgr.arrays, mgr.blknos, mgr.blklocs
-        loc = data.columns.get_indexer(columns)
-        out = []
-        for i in loc:
-            if i < 0 or blklocs[i] != 0:
+        if len(columns) == len(data.columns) and all(a is b for a, b in zip(columns, data.columns)):
+            loc = np.arange(len(columns))  # the frame's own column order (predict's call)
+        else:
+            loc = data.columns.get_indexer(columns)
+            if (loc < 0).any():
                 return None
-            a = arrays[blknos[i]]
-            if not isinstance(a, pd.Categorical):
-                return None
-            out.append(a)
+        if len(loc) and np.asarray(blklocs)[loc].any():  # every column its own one-column block
+            return None
+        cat = pd.Categorical
+        out = [arrays[b] for b in np.asarray(blknos)[loc].tolist()]
+        if not all(type(a) is cat or isinstance(a, cat) for a in out):
+            return None
         return out
     except Exception:  # pandas internals moved: the public accessor
         out = []
@@ -345,15 +348,25 @@ def ingest_columnar(model, data, columns):
     n = len(data)
     raws, luts, addrs = [], [], []
     i8 = np.dtype(np.int8)
+    cpd_of = getattr(model, "_cpd_index", None) or {}
+    addressof, char_at = ctypes.addressof, ctypes.c_char.from_buffer
     for col, arr in zip(columns, cats):
         try:
-            raw = arr.codes  # public, a read-only view of the codes (no copy)
-        except (AttributeError, TypeError):  # pragma: no cover - pandas API moved: the general encoder
-            return None
+            raw = arr._codes  # the codes ndarray itself (the public .codes makes a read-only view per call)
+        except AttributeError:  # pragma: no cover - pandas internals moved: the public accessor
+            try:
+                raw = arr.codes
+            except (AttributeError, TypeError):
+                return None  # the general encoder takes the frame
         if raw.dtype is not i8 or not raw.flags.c_contiguous:
             return None
-        addrs.append(raw.__array_interface__["data"][0])
-        cpd = model.get_cpds(col)
+        try:  # the buffer protocol's address: ~5x cheaper than building __array_interface__ per column
+            addrs.append(addressof(char_at(raw)) if n else 0)
+        except (TypeError, ValueError):  # a read-only or empty buffer
+            addrs.append(raw.__array_interface__["data"][0])
+        cpd = cpd_of.get(col)
+        if cpd is None:
+            cpd = model.get_cpds(col)  # raises the reference's error for a column that is not a node
         st = cpd.state_names[col]
         if len(st) >= MISSING:
             raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")

@@ -586,7 +586,7 @@ class PatternPlan:
         for n in {min(chunk, n_rows - c0) for c0 in range(0, n_rows, chunk)}:
             self.prepare_steps(n, outs)
 
-    def query_one(self, codes, key):
+    def query_one(self, codes, key, stream=None):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v, already checked
         against the state names on the host) through the steps program whose codes and result live in
         host memory the kernels access directly: fill the codes, one graph launch, one synchronize.
@@ -599,8 +599,8 @@ class PatternPlan:
                 sel = self._ev_sel = [self.col_of[v] for v in self.ev_used]
             if sel:
                 host["codes"].array[:, 0] = [codes[i] for i in sel]
-            s = N.stream_handle()
-            prog.run()
+            s = N.stream_handle(stream)
+            prog.run(stream)
             N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
             return host[key].array.reshape(-1).copy()
 
@@ -679,29 +679,40 @@ class QueryRunner:
         self.out = plan.alloc_outputs(1, marginals=not joint, joint=joint)
         self.key = "joint" if joint else "marg"
         self.h_out = torch.empty(tuple(self.out[self.key].shape), dtype=torch.float64, pin_memory=True)
+        # runs go to the calling thread's own stream (engine.thread_stream): what the default stream
+        # queued for these buffers (zero fills) completes first
+        torch.cuda.current_stream().synchronize()
 
     def run(self, codes):
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
         the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
         L = N.lib()
+        import torch
+
         # any program the query replays is captured before this runner's lock is taken (engine.DeviceLock)
         if self.plan.kind != "fused":
             self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
         else:
             self.plan.prepare_run(1, [self.key])
+        ts = E.thread_stream()
         with self.lock:
             if self.plan.kind != "fused":  # host copies inside the captured graph: one launch + one sync
-                return self.plan.query_one(codes, self.key)
-            s = N.stream_handle()
-            hc = self.h_codes.numpy()
-            hc[:len(codes), 0] = codes
-            N.check(L.pgm_memcpy_h2d(N.ptr(self.d_codes), ctypes.c_void_p(self.h_codes.data_ptr()),
-                                     hc.nbytes, s), "memcpy_h2d")
-            self.plan.run(self.d_codes, 1, 0, 1, self.out)
-            dst = self.out[self.key]
-            N.check(L.pgm_memcpy_d2h(ctypes.c_void_p(self.h_out.data_ptr()), N.ptr(dst),
-                                     dst.numel() * 8, s), "memcpy_d2h")
-            return self.h_out.numpy().reshape(-1).copy()
+                return self.plan.query_one(codes, self.key, stream=ts)
+            with torch.cuda.stream(ts):
+                return self._run_fused(L, codes)
+
+    def _run_fused(self, L, codes):
+        """The fused path on the current (this thread's) stream: codes up, one pass, result down."""
+        s = N.stream_handle()
+        hc = self.h_codes.numpy()
+        hc[:len(codes), 0] = codes
+        N.check(L.pgm_memcpy_h2d(N.ptr(self.d_codes), ctypes.c_void_p(self.h_codes.data_ptr()),
+                                 hc.nbytes, s), "memcpy_h2d")
+        self.plan.run(self.d_codes, 1, 0, 1, self.out)
+        dst = self.out[self.key]
+        N.check(L.pgm_memcpy_d2h(ctypes.c_void_p(self.h_out.data_ptr()), N.ptr(dst),
+                                 dst.numel() * 8, s), "memcpy_d2h")
+        return self.h_out.numpy().reshape(-1).copy()
 
 
 class BoundRows:
