@@ -88,6 +88,25 @@ def main():
     res["download_ms"], host = med(lambda: B.download(out["marg"]))
     names = [v + "_" + str(s) for v in order for s in m.get_cpds(v).state_names[v]]
     res["frame_from_block_ms"], _ = med(lambda: pd.DataFrame(host.T, columns=names, index=cat.index))
+    # the direct path's own stages, timed alone on the same frame
+    ing = B._ingest(m, cat)
+    res["direct_ingest_ms"], ing = med(lambda: B._ingest(m, cat))
+    res["direct_plan_ms"], plan = med(lambda: B._single_fused_plan(m, cat, *ing, order))
+    res["direct_fused_to_host_ms"], marg = med(lambda: B._fused_to_host(plan, ing[2], ing[0], ing[1], n, True))
+    res["direct_frame_ms"], _ = med(lambda: pd.DataFrame(marg.T, columns=names, index=cat.index, copy=False))
+    res["direct_nodes_minus_columns_ms"], _ = med(lambda: list(set(m.nodes()) - set(cat.columns)))
+    import cProfile
+    import io
+    import pstats
+
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(5):
+        m.predict_probability(cat)
+    pr.disable()
+    buf = io.StringIO()
+    pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(14)
+    res["cprofile_predict_probability_x5"] = buf.getvalue().splitlines()[-22:]
     print(json.dumps(res), flush=True)
 
 

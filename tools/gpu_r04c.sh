@@ -11,6 +11,10 @@ c4() {  # label rows env...
   env "$@" timeout -k 10 300 python bench.py --workload c4 --rows $ROWS --steps 20 --warmup 3 > gpurun_out/${TAG}_c4_${ROWS}_${L}_$R.json 2> gpurun_out/${TAG}_c4.err || { tail -30 gpurun_out/${TAG}_c4.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/${TAG}_c4_${ROWS}_${L}_$R.json')); print('c4 $ROWS $L', round(d['value']), round(d['ms_per_step'],3), 'ms')"
 }
+# C5 MAP host-delivery loop under a kernel + memory-copy trace (where do 0.3 ms per step go?)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$ROOT/gpurun_out/${TAG}_c5trace" -o t --output-format csv -- \
+  python3 "$ROOT/bench.py" --workload c5 --c5-output map --steps 20 --warmup 5 > "$ROOT/gpurun_out/${TAG}_c5trace.json" 2> "$ROOT/gpurun_out/${TAG}_c5trace.err") \
+  || { echo "c5 trace failed"; tail -5 gpurun_out/${TAG}_c5trace.err; }
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_kernels_gpu.py -k block_order_knobs > gpurun_out/${TAG}_knobs.log 2>&1; rc=$?; tail -8 gpurun_out/${TAG}_knobs.log; [ $rc -le 1 ] || exit 1
 for R in 1; do
   for ROWS in 4000 1000; do

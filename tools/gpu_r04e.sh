@@ -25,6 +25,8 @@ ENVS=PGM_NOTHING=1 c3 q2_wg512 --queues 2
 ENVS=PGM_NOTHING=1 c3 q8_wg512 --queues 8
 ENVS=PGM_ROWS_JIT_WG=256 c3 q4_wg256
 ENVS=PGM_ROWS_JIT_WG=1024 c3 q4_wg1024
+ENVS=PGM_ROWS_JIT_WG=128 c3 q4_wg128
+ENVS=PGM_ROWS_JIT_WG=192 c3 q4_wg192
 ENVS=PGM_ROWS_JIT_WG=256 c3 q8_wg256 --queues 8
 ENVS=PGM_NOTHING=1 c3 ring_prestart --launch ring --ring-prestart
 ENVS=PGM_NOTHING=1 c3 ring --launch ring

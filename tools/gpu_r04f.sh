@@ -1,0 +1,16 @@
+# round 4: C3 workgroup-size confirmation in the HBM regime (96 batches, 4 queues; three interleaved
+# repeats) and the direct API path's stage profile
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+TAG=${1:-r04f}
+timeout -k 10 300 python tools/e2e_profile.py > gpurun_out/${TAG}_e2e_profile.json 2> gpurun_out/${TAG}_e2e.err || { tail -20 gpurun_out/${TAG}_e2e.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_e2e_profile.json')); print({k: v for k, v in d.items() if k != 'cprofile_predict_probability_x5'}); print('\n'.join(d['cprofile_predict_probability_x5']))"
+c3() {  # label wg
+  env PGM_ROWS_JIT_WG=$2 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api-e2e --no-ring-roofline > gpurun_out/${TAG}_c3_$1.json 2> gpurun_out/${TAG}_c3.err || { tail -20 gpurun_out/${TAG}_c3.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${TAG}_c3_$1.json')); r=d['roofline']; print('c3 $1', round(d['value']/1e9,2), 'G', 'frac', round(r['frac'],3), 'wall', round(r['frac_wall'],3), r['grid'])"
+}
+for R in 1 2 3; do
+  for WG in 192 512 128 1024 320; do
+    c3 wg${WG}_$R $WG
+  done
+done
