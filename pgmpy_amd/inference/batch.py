@@ -618,15 +618,36 @@ def predict_probability_frame(model, data):
 
 
 def _append_columns(base, vals, order):
-    """base's columns then vals[c] for c in order, as a new frame.  PGM_API_APPEND=concat (A/B):
-    pd.concat of the two frames; default: a shallow copy of base (its column blocks shared, not
-    copied) with the new columns set on it."""
+    """base's columns then vals[c] for c in order, as a new frame whose observed columns share base's
+    buffers (as DataFrame.copy(deep=False) shares them; DESIGN.md deviation 5).  Default: one new
+    BlockManager holding base's blocks plus one block per new column (a munin frame has ~1,000
+    categorical blocks: setting columns one by one on a copy costs ~2 ms each, pd.concat copies
+    every block).  PGM_API_APPEND=concat (A/B): pd.concat of the two frames (independent copies);
+    =shallow: a shallow copy with the columns set on it.  Any pandas-internals mismatch falls back
+    to the shallow form."""
     import warnings
 
     import pandas as pd
 
-    if os.environ.get("PGM_API_APPEND", "shallow") == "concat":
+    mode = os.environ.get("PGM_API_APPEND", "blocks")
+    if mode == "concat":
         return pd.concat([base, pd.DataFrame(vals, index=base.index, columns=order)], axis=1)
+    if mode == "blocks":
+        try:
+            from pandas._libs.internals import BlockPlacement
+            from pandas.core.internals.blocks import new_block
+            from pandas.core.internals.managers import BlockManager
+
+            nb = len(base.columns)
+            blocks = list(base._mgr.blocks)
+            for k, c in enumerate(order):
+                v = np.asarray(vals[c])
+                blocks.append(new_block(v.reshape(1, -1), placement=BlockPlacement(slice(nb + k, nb + k + 1)),
+                                        ndim=2))
+            axes = [base.columns.append(pd.Index(list(order))), base.index]
+            return pd.DataFrame._from_mgr(BlockManager(tuple(blocks), axes, verify_integrity=False), axes=axes)
+        except Exception:  # pragma: no cover - pandas internals moved: the public form below
+            pass
     out = base.copy(deep=False)
     with warnings.catch_warnings():  # a frame of ~1,000 categorical blocks is "fragmented" by design
         warnings.simplefilter("ignore", pd.errors.PerformanceWarning)

@@ -417,6 +417,33 @@ def test_program_hazard_check_catches_undeclared_and_unordered_access():
     assert any("without an ordering" in m for m in prog.check_hazards())
 
 
+def test_predict_output_frame_assembly():
+    """predict's result frame (batch._append_columns): the observed columns then the MAP columns, built
+    as one block manager over the input's blocks plus one block per new column, equals pd.concat's
+    frame (dtypes, order, index) on mixed block layouts (multi-column float block, categoricals, a
+    non-default index)."""
+    import os
+
+    from pgmpy_amd.inference.batch import _append_columns
+
+    base = pd.DataFrame({"a": pd.Categorical(["x", "y", "x", "y"]), "f1": [1.0, 2, 3, 4], "f2": [0.5, 0, 1, 2],
+                         "c": pd.Categorical(["u", "u", "v", "u"])}, index=[5, 3, 9, 1])
+    vals = {"p": np.array(["s0", "s1", "s0", "s1"], dtype=object), "q": np.array([np.nan, "t", "t", "r"], dtype=object)}
+    got = _append_columns(base, vals, ["p", "q"])
+    old = os.environ.get("PGM_API_APPEND")
+    os.environ["PGM_API_APPEND"] = "concat"
+    try:
+        want = _append_columns(base, vals, ["p", "q"])
+    finally:
+        if old is None:
+            os.environ.pop("PGM_API_APPEND")
+        else:
+            os.environ["PGM_API_APPEND"] = old
+    assert got.equals(want) and list(got.columns) == list(want.columns)
+    assert list(got.dtypes) == list(want.dtypes) and list(got.index) == [5, 3, 9, 1]
+    assert list(base.columns) == ["a", "f1", "f2", "c"]  # the input frame is not modified
+
+
 def test_device_lock_readers_writer_semantics():
     """engine.DeviceLock (SURVEY §8(b) threading): shared holds overlap across threads, an exclusive
     hold excludes everyone, holds nest, and two threads that each hold it shared and then ask for it
