@@ -199,16 +199,18 @@ static int pm_knob(const char *name, int dflt) {
 
 // Decode order of a step's kept outer dims, fastest first (the last one is the slowest: with the XCD
 // grouping each XCD takes a contiguous range of it).  Default: the belief's own order (its fastest
-// dim fastest, so a block's neighbours write neighbouring addresses).  PGM_PM_KREV=1: reversed.
+// dim fastest, so a block's neighbours write neighbouring addresses) — PGM_PM_XPART=0.  PGM_PM_KREV=1: reversed.
 // PGM_PM_XPART=1: the kept dim carried by the most row-operand bytes becomes the slowest, so each XCD
 // reads a disjoint slice of every operand that carries it (instead of all 8 re-reading an operand that
 // lacks the belief's slowest dim); =2: in addition the other dims vary fastest in order of the bytes
 // that carry them (least first), so consecutive blocks re-read the same operand entries while they are
-// in the XCD's L2.  cards[q], bytes_of(q) = row-operand bytes that vary along kept dim q.
+// in the XCD's L2 — the default since r04c (C4 pathfinder, 4,000 rows, with PGM_PM_XCD=2: fetch 7.75 ->
+// 6.32 GB per sweep, 1.04x the steps' own reads; profiles/r04c/).  cards[q], bytes_of(q) = row-operand
+// bytes that vary along kept dim q.
 template <class BytesOf>
 static std::vector<int> pm_kept_order(int kx, const unsigned *cards, BytesOf bytes_of) {
   static const int krev = pm_knob("PGM_PM_KREV", 0);
-  static const int xpart = pm_knob("PGM_PM_XPART", 0);
+  static const int xpart = pm_knob("PGM_PM_XPART", 2);  // r04c: 2 (fetch 7.75 -> 6.32 GB per 4,000-row sweep)
   std::vector<int> ord;
   for (int qi = 0; qi < kx; ++qi) ord.push_back(krev ? qi : kx - 1 - qi);
   if (!xpart || kx < 2) return ord;
@@ -698,7 +700,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // forced 2 / 4 for every step, or a minimum of 4: slower, profiles/r02bw_c4_xi.txt)
   static const int xi_min = pm_knob("PGM_PM_XI_MIN", 2);
   static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
-  static const int xcd_knob = pm_knob("PGM_PM_XCD", 1);
+  static const int xcd_knob = pm_knob("PGM_PM_XCD", 2);  // r04c: 2 (with XPART 2: +1.9 % / +3 % at 4,000 / 1,000 rows)
   static const int nt = pm_knob("PGM_PM_NT", 1);
   static const int wt = pm_knob("PGM_PM_WT", 0);  // write-through product stores (A/B knob)
   static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
@@ -859,7 +861,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
   sp.store = false;
   sp.gx = (sp.mm.NP + 255) / 256;
   sp.total = (uint64_t)sp.gx * sp.mm.n_outer;
-  sp.xcd = pm_knob("PGM_PM_XCD", 1) >= 2 || (pm_knob("PGM_PM_XCD", 1) == 1 && sp.total % 8 == 0);
+  sp.xcd = pm_knob("PGM_PM_XCD", 2) >= 2 || (pm_knob("PGM_PM_XCD", 2) == 1 && sp.total % 8 == 0);
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;
   const std::string src = pm_source({sp}, starts, &blocks);

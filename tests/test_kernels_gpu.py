@@ -942,13 +942,15 @@ def test_two_marginals_one_pass(gpu, rows, red, ratio):
     np.testing.assert_allclose(E.to_host(Ms[1]), f(full, axis=(0, 1)), rtol=1e-13)
 
 
-@pytest.mark.parametrize("env", [{"PGM_PM_XCD": "2"}, {"PGM_PM_XPART": "1"}, {"PGM_PM_XPART": "2", "PGM_PM_XCD": "2"},
-                                 {"PGM_PM_KREV": "1"}])
+@pytest.mark.parametrize("env", [{"PGM_PM_XCD": "1", "PGM_PM_XPART": "0"}, {"PGM_PM_XPART": "1"}, {"PGM_PM_XCD": "0"},
+                                 {"PGM_PM_KREV": "1", "PGM_PM_XPART": "0"}])
 def test_bp_block_order_knobs_bit_exact(gpu, tmp_path, env):
     """The block-to-tile order knobs of the specialised batched-BP steps (bijective XCD grouping of any
     block count, the XCD partition along the kept dim the row operands carry, the reversed decode)
     only change which block computes which output: every clique belief of a 1,002-row pathfinder
-    calibration is bit-identical to the default order's (separate processes: the knobs are read once)."""
+    calibration is bit-identical to the default order's (r04 default: XCD grouping of any block count,
+    XPART 2; against r03's order, the XPART 1 form, no grouping, the reversed decode; separate processes:
+    the knobs are read once)."""
     import subprocess
     import sys
 

@@ -14,3 +14,7 @@ for R in 1 2 3; do
     c3 wg${WG}_$R $WG
   done
 done
+for OUT in map marginals; do
+  timeout -k 10 300 python bench.py --workload c5 --c5-output $OUT --steps 50 --warmup 5 > gpurun_out/${TAG}_c5_host_$OUT.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${TAG}_c5_host_$OUT.json')); print('c5 host $OUT', round(d['value']/1e9,3), 'G rows/s', 'ms/step', round(d['ms_per_step'],3), 'kernel', round(d['kernel_ms'],4), 'copy', round(d['copy_ms'],3), 'GB/s', round(d['copy_GBps'],1))"
+done
