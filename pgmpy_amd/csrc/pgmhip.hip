@@ -202,18 +202,42 @@ __device__ __forceinline__ void contract_flat(const ContractK &p, const double *
         }
       }
     } else {
-      for (uint32_t ro = r0; ro < r1; ++ro) {
-        int64_t ra, rb;
-        decode_ro(p, ro, ra, rb);
-        const double *a = A + oa + ra;
-        const double *b = B + ob + rb;
-        for (uint32_t ri = lane_g; ri < p.ri_card; ri += G) {
-          double v;
-          if constexpr (CMB == PGM_COMBINE_COPY)
-            v = a[(int64_t)ri * p.ri_sa];
-          else
-            v = combine<CMB>(a[(int64_t)ri * p.ri_sa], b[(int64_t)ri * p.ri_sb]);
-          acc = red_op<RED>(acc, v);
+      // G lanes per output, each striding the innermost reduction dim from its lane; this lane's entries
+      // (reduction-outer major, its innermost indices minor — the summation order of the r03 loop) are
+      // walked UNR at a time with every operand load of a group issued before the group is summed (r04:
+      // the r03 loop waited for each load before the next, one memory round trip per entry — C2's levels
+      // with long reduction-outer walks; same order, bit-identical sums).  G <= ri_card (host plan), so
+      // every lane has at least one entry per reduction-outer index.
+      constexpr int UNR = 8;
+      uint32_t ro = r0, ri = lane_g;
+      int64_t ra = 0, rb = 0;
+      bool live = ro < r1;
+      if (live) decode_ro(p, ro, ra, rb);
+      while (live) {
+        double xa[UNR], xb[UNR];
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (live) {
+            xa[u] = A[oa + ra + (int64_t)ri * p.ri_sa];
+            if constexpr (CMB != PGM_COMBINE_COPY) xb[u] = B[ob + rb + (int64_t)ri * p.ri_sb];
+            cnt = u + 1;
+            ri += G;
+            if (ri >= p.ri_card) {
+              ri = lane_g;
+              if (++ro < r1) decode_ro(p, ro, ra, rb);
+              else live = false;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          if (u < cnt) {
+            if constexpr (CMB == PGM_COMBINE_COPY)
+              acc = red_op<RED>(acc, xa[u]);
+            else
+              acc = red_op<RED>(acc, combine<CMB>(xa[u], xb[u]));
+          }
         }
       }
     }
@@ -2522,11 +2546,15 @@ void pgmi_appendf(std::string &o, const char *fmt, ...) {
 // rows per launch — one CPT staging per 1,024 rows and a quarter of the workgroup dispatches of
 // 256 x one row — 26.4 -> 29.1-31.1 G rows/s at 20 steps, 36.2 -> 47.1 G at 400; one queue and
 // 1M-row launches unchanged (profiles/r02bq_c3_wg_rowform_sweep.txt, r02br_c3_wg_rowform_confirm.txt)
+// r04 (96 resident batches, the HBM regime: profiles/r04e, r04f): 320 — 157 blocks of 640 rows per
+// 100 k-row launch keep more CUs streaming than 98 x 1,024 once the outputs go to HBM instead of the
+// Infinity Cache; three interleaved repeats, 20 steps: 26.6 / 26.7 / 27.9 G rows/s against 27.3 / 25.1 /
+// 25.3 G at 512 (192: 27.0 / 26.7 / 26.0; 128: 25.7 / 25.6 / 26.6; 1,024: 25.5 / 24.7 / 25.5)
 static int jit_wg() {
   static const int wg = [] {
     const char *e = getenv("PGM_ROWS_JIT_WG");
-    const int v = e ? atoi(e) : 512;
-    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 512;
+    const int v = e ? atoi(e) : 320;
+    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 320;
   }();
   return wg;
 }

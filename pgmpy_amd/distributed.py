@@ -13,6 +13,8 @@ leave a rank one of two ways:
 
 CPTs are replicated: each rank compiles its own plan (munin's CPTs are 787 KB).
 """
+import ctypes
+
 import numpy as np
 
 
@@ -69,11 +71,18 @@ class HostDelivery:
     stream, ordered after the launch, so the copy of step k overlaps the launch of step k + 1.
     Each GPU's copies use its own host link."""
 
-    def __init__(self, shape, dtype, depth=2, device=None):
+    def __init__(self, shape, dtype, depth=2, device=None, same_stream=None):
+        import os
+
         import torch
 
         self.depth = int(depth)
         self.hosts = [torch.empty(tuple(shape), dtype=dtype, pin_memory=True) for _ in range(self.depth)]
+        # same_stream: the copy goes on the launch stream itself, right behind its launch (no overlap of
+        # copy k with launch k + 1, no cross-stream events) — knob PGM_HOST_DELIVERY=same (A/B)
+        if same_stream is None:
+            same_stream = os.environ.get("PGM_HOST_DELIVERY", "separate") == "same"
+        self.same_stream = bool(same_stream)
         self.stream = torch.cuda.Stream(device=device)
         self._copied = [torch.cuda.Event() for _ in range(self.depth)]
         self._ready = [torch.cuda.Event() for _ in range(self.depth)]
@@ -89,19 +98,27 @@ class HostDelivery:
         depth; returns that pinned host tensor (complete after wait(k))."""
         import torch
 
+        from . import _native as N
+
         i = k % self.depth
-        self._ready[i].record(stream)
-        self.stream.wait_event(self._ready[i])
-        with torch.cuda.stream(self.stream):
-            self.hosts[i].copy_(src, non_blocking=True)
-        self._copied[i].record(self.stream)
+        cs = stream if self.same_stream else self.stream
+        if not self.same_stream:
+            self._ready[i].record(stream)
+            cs.wait_event(self._ready[i])
+        if not src.is_contiguous():
+            raise ValueError("HostDelivery: the device result must be contiguous")
+        h = self.hosts[i]
+        N.check(N.lib().pgm_memcpy_d2h_async(ctypes.c_void_p(h.data_ptr()), N.ptr(src), h.numel() * h.element_size(),
+                                             N.stream_handle(cs)), "memcpy_d2h_async")
+        self._copied[i].record(cs)
         self._used[i] = True
         return self.hosts[i]
 
     def wait(self, k=None):
         """Every queued copy (k None) or step k's copy has completed."""
         if k is None:
-            self.stream.synchronize()
+            for e in self._copied:
+                e.synchronize()
         else:
             self._copied[k % self.depth].synchronize()
         return None if k is None else self.hosts[k % self.depth]
