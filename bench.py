@@ -859,8 +859,8 @@ def bench_c5_host(args, dist, rank, world):
     result of predict_probability / predict is a host DataFrame, and a funnel into one GPU (the RCCL
     gather, --c5-delivery rccl) moves every row's 136 B through rank 0's links.  One step = each
     rank's fused-plan launch over its block (device-resident evidence) into device buffer k % 2 +
-    the DMA of that buffer into pinned host buffer k % 2 on a copy stream; launch k + 1 overlaps
-    copy k (launch k + 2 waits for copy k, which frees its buffer)."""
+    the DMA of that buffer into pinned host buffer k % 2, ordered as HostDelivery's mode says (default
+    "lanes": launch k and copy k on stream lane k % 2, so copy k overlaps launch k + 1)."""
     import torch
 
     from pgmpy_amd.distributed import HostDelivery, shard_bounds
@@ -888,16 +888,19 @@ def bench_c5_host(args, dist, rank, world):
     key = "map" if want_map else "marg"
     outs = [plan.alloc_outputs(rows, marginals=not want_map, map_=want_map) for _ in range(2)]
     delivery = HostDelivery(tuple(outs[0][key].shape), outs[0][key].dtype, depth=2, device=dev)
-    hosts, cs = delivery.hosts, delivery.stream
+    hosts = delivery.hosts
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     ls = torch.cuda.Stream(device=dev)
-    bounds = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=ls) for i in range(2)]
+    bounds = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=delivery.launch_stream(i, ls))
+              for i in range(2)]
+    single = plan.bind(d_codes, rows, 0, rows, outs[0], err=err, stream=ls)
     kname, k_blocks, k_wg = bounds[0].kernel()
 
     def step(k):
-        delivery.acquire(k, ls)  # device buffer k % 2 and host slot k % 2 are free
+        s = delivery.launch_stream(k, ls)
+        delivery.acquire(k, s)  # device buffer k % 2 and host slot k % 2 are free
         bounds[k % 2].run()
-        delivery.deliver(k, outs[k % 2][key], ls)
+        delivery.deliver(k, outs[k % 2][key], s)
 
     for k in range(max(args.warmup, 2)):
         step(k)
@@ -906,7 +909,7 @@ def bench_c5_host(args, dist, rank, world):
     t_start = time.perf_counter()
     for k in range(args.steps):
         step(k)
-    cs.synchronize()
+    delivery.wait()
     torch.cuda.synchronize()
     t_end = time.perf_counter()
     barrier(dist)
@@ -917,14 +920,14 @@ def bench_c5_host(args, dist, rank, world):
     with torch.cuda.stream(ls):
         timer.start()
         for k in range(args.steps):
-            bounds[k % 2].run()
+            single.run()
         kernel_ms = timer.stop_ms() / args.steps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with torch.cuda.stream(cs):
+    with torch.cuda.stream(ls):
         for k in range(args.steps):
             hosts[k % 2].copy_(outs[k % 2][key], non_blocking=True)
-    cs.synchronize()
+    ls.synchronize()
     copy_ms = (time.perf_counter() - t0) * 1e3 / args.steps
     copy_bytes = hosts[0].numel() * hosts[0].element_size()
     parity = None
@@ -966,8 +969,8 @@ def bench_c5_host(args, dist, rank, world):
                                 "marginals delivered to pinned host memory per rank"),
                    "network": "munin", "missing": variables, "global_rows_per_step": total,
                    "rows_per_gpu_per_step": rows, "delivery": "host",
-                   "launch": "bound fused-plan launch on a launch stream into device buffer k % 2, DMA to pinned "
-                             "host buffer k % 2 on a copy stream (launch k + 1 overlaps copy k)",
+                   "launch": f"bound fused-plan launch into device buffer k % 2, DMA to pinned host buffer k % 2, "
+                             f"HostDelivery mode {delivery.mode!r}",
                    "parallelism": f"rows sharded over {world} rank(s), no collective: each rank's own host link"},
         "kernel_ms": kernel_ms, "copy_ms": copy_ms, "copy_bytes_per_rank": copy_bytes,
         "copy_GBps": copy_bytes / (copy_ms * 1e-3) / 1e9,

@@ -3487,7 +3487,16 @@ static unsigned batch_levels_cap() {
   return cap;
 }
 
-static const uint32_t kBatchMaxBlocksPerJob = 256;
+// workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that); A/B
+// knob PGM_BATCH_MAX_BLOCKS
+static uint64_t batch_max_blocks() {
+  static const uint64_t cap = [] {
+    const char *e = getenv("PGM_BATCH_MAX_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint64_t)std::min(v, 1L << 20) : (uint64_t)256;
+  }();
+  return cap;
+}
 
 extern "C" {
 
@@ -3515,7 +3524,7 @@ int pgm_batch_create(void **handle) {
 
 static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads) {
   if (h->d_jobs) return fail(PGM_EINVAL, "batch: already finalized");
-  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), kBatchMaxBlocksPerJob);
+  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), batch_max_blocks());
   if (h->block_job.size() + nb > 0x7fffffffull) return fail(PGM_EINVAL, "batch: too many blocks");
   J.block0 = (uint32_t)h->block_job.size();
   J.nblocks = (uint32_t)nb;

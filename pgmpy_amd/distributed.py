@@ -5,8 +5,9 @@ collective: every rank runs the same plan on its own block of rows.  Results
 leave a rank one of two ways:
 
 * HostDelivery (default for C5): each rank DMAs its block's results into pinned
-  host memory over its own host link, double-buffered so step k's copy overlaps
-  step k + 1's launch — no collective, every GPU's link carries only its share;
+  host memory over its own host link, double-buffered on two stream lanes so step
+  k's copy overlaps step k + 1's launch — no collective, every GPU's link carries
+  only its share;
 * gather_rows: one gather of per-row results to rank 0 (torch.distributed
   `gather`; backend "nccl" is RCCL over xGMI on MI355X, "gloo" on CPU for the
   tests) — every row's bytes funnel into rank 0's links.
@@ -64,45 +65,64 @@ def run_sharded(executor, codes_host, n_rows, dist, gather=True):
 
 class HostDelivery:
     """Results of consecutive launches delivered into pinned host buffers of this rank's node, with no
-    collective (SURVEY.md §8(e)'s alternative to the gather): `depth` pinned buffers and one copy
-    stream.  Step k: acquire(k, stream) before the launch that writes the step's device buffer (the
-    launch stream then waits until slot k % depth's previous copy-out is done, so that device buffer
-    and that host buffer are free), then deliver(k, device_tensor, stream) after it: a DMA on the copy
-    stream, ordered after the launch, so the copy of step k overlaps the launch of step k + 1.
-    Each GPU's copies use its own host link."""
+    collective (SURVEY.md §8(e)'s alternative to the gather): `depth` pinned host buffers, one per
+    device result buffer.  Step k: launch on launch_stream(k, stream), after acquire(k, stream) (slot
+    k % depth's previous copy-out is done, so that device buffer and that host buffer are free), then
+    deliver(k, device_tensor, stream) queues the DMA into host slot k % depth behind the launch.
+    Each GPU's copies use its own host link.  Three orderings (`mode`, knob PGM_HOST_DELIVERY):
 
-    def __init__(self, shape, dtype, depth=2, device=None, same_stream=None):
+    * "lanes" (default): one stream per slot.  Step k launches and copies on lane k % depth, so the
+      copy of step k overlaps the launch of step k + 1 on the other lane with no cross-stream event:
+      a lane's next launch is ordered after its own previous copy by the stream itself.
+    * "same": launch and copy on the caller's stream, one behind the other (no overlap).
+    * "separate": copies on one copy stream, ordered after their launches by cross-stream events.
+      Measured on MI355X (profiles/r04h/) those events cost more than the overlap gains: MAP rows
+      1.9 G rows/s against 8.0 G for "same"."""
+
+    MODES = ("lanes", "same", "separate")
+
+    def __init__(self, shape, dtype, depth=2, device=None, mode=None, lanes=None):
         import os
 
         import torch
 
         self.depth = int(depth)
+        self.mode = mode or os.environ.get("PGM_HOST_DELIVERY", "lanes")
+        if self.mode not in self.MODES:
+            raise ValueError(f"HostDelivery: mode {self.mode!r} is not one of {self.MODES}")
         self.hosts = [torch.empty(tuple(shape), dtype=dtype, pin_memory=True) for _ in range(self.depth)]
-        # same_stream: the copy goes on the launch stream itself, right behind its launch (no overlap of
-        # copy k with launch k + 1, no cross-stream events) — knob PGM_HOST_DELIVERY=same (A/B)
-        if same_stream is None:
-            same_stream = os.environ.get("PGM_HOST_DELIVERY", "separate") == "same"
-        self.same_stream = bool(same_stream)
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = torch.cuda.Stream(device=device) if self.mode == "separate" else None
+        # lanes: another HostDelivery's lanes may be shared (several results of one launch)
+        self.lanes = None
+        if self.mode == "lanes":
+            self.lanes = list(lanes) if lanes is not None else [torch.cuda.Stream(device=device)
+                                                                 for _ in range(self.depth)]
+            if len(self.lanes) != self.depth:
+                raise ValueError("HostDelivery: one lane per slot")
         self._copied = [torch.cuda.Event() for _ in range(self.depth)]
         self._ready = [torch.cuda.Event() for _ in range(self.depth)]
         self._used = [False] * self.depth
 
+    def launch_stream(self, k, stream):
+        """The stream step k's launch (and its deliver) must be queued on."""
+        return self.lanes[k % self.depth] if self.lanes is not None else stream
+
     def acquire(self, k, stream):
         i = k % self.depth
-        if self._used[i]:
+        if self._used[i] and self.lanes is None:
             stream.wait_event(self._copied[i])
 
     def deliver(self, k, src, stream):
-        """Queue the copy of `src` (written by work already queued on `stream`) into host slot k %
-        depth; returns that pinned host tensor (complete after wait(k))."""
-        import torch
-
+        """Queue the copy of `src` (written by work already queued on `stream`, which is
+        launch_stream(k, ...)) into host slot k % depth; returns that pinned host tensor (complete
+        after wait(k))."""
         from . import _native as N
 
         i = k % self.depth
-        cs = stream if self.same_stream else self.stream
-        if not self.same_stream:
+        if self.lanes is not None and stream is not self.lanes[i]:
+            raise ValueError("HostDelivery: step k's result must be produced on launch_stream(k)")
+        cs = self.stream if self.mode == "separate" else stream
+        if self.mode == "separate":
             self._ready[i].record(stream)
             cs.wait_event(self._ready[i])
         if not src.is_contiguous():

@@ -444,6 +444,16 @@ def test_predict_output_frame_assembly():
     assert list(base.columns) == ["a", "f1", "f2", "c"]  # the input frame is not modified
 
 
+def test_host_delivery_rejects_unknown_mode():
+    """HostDelivery's ordering knob is one of three named modes (pgmpy_amd/distributed.py); a typo is an
+    error, not a silent fallback to another ordering."""
+    from pgmpy_amd.distributed import HostDelivery
+
+    assert HostDelivery.MODES == ("lanes", "same", "separate")
+    with pytest.raises(ValueError, match="not one of"):
+        HostDelivery((4,), None, mode="overlap")
+
+
 def test_device_lock_readers_writer_semantics():
     """engine.DeviceLock (SURVEY §8(b) threading): shared holds overlap across threads, an exclusive
     hold excludes everyone, holds nest, and two threads that each hold it shared and then ask for it

@@ -69,15 +69,16 @@ def main(out_path, mode="gather"):
         outs = [plan.alloc_outputs(m, marginals=True, map_=True) for _ in range(2)]
         err = torch.zeros(1, dtype=torch.int32, device=d.device)
         ls = torch.cuda.Stream()
-        bounds = [plan.bind(d, m, 0, m, o, err=err, stream=ls) for o in outs]
         dm = HostDelivery(tuple(outs[0]["marg"].shape), torch.float64, device=d.device)
-        dp = HostDelivery(tuple(outs[0]["map"].shape), torch.int32, device=d.device)
+        dp = HostDelivery(tuple(outs[0]["map"].shape), torch.int32, device=d.device, lanes=dm.lanes)
+        bounds = [plan.bind(d, m, 0, m, o, err=err, stream=dm.launch_stream(i, ls)) for i, o in enumerate(outs)]
         for k in range(5):  # consecutive steps through the double buffers, copies overlapping launches
-            dm.acquire(k, ls)
-            dp.acquire(k, ls)
+            s = dm.launch_stream(k, ls)
+            dm.acquire(k, s)
+            dp.acquire(k, s)
             bounds[k % 2].run()
-            dm.deliver(k, outs[k % 2]["marg"], ls)
-            dp.deliver(k, outs[k % 2]["map"], ls)
+            dm.deliver(k, outs[k % 2]["marg"], s)
+            dp.deliver(k, outs[k % 2]["map"], s)
         hm, hp = dm.wait(4), dp.wait(4)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
