@@ -21,6 +21,7 @@ A compiled plan is immutable; run() is re-entrant on distinct outputs.
 """
 import ctypes
 import threading
+from operator import itemgetter
 
 import numpy as np
 
@@ -408,7 +409,7 @@ class PatternPlan:
                 c = self.__dict__.get("_compact")
                 if c is None:
                     c = copy.copy(self)
-                    for k in ("_handle", "_handle_joint", "_plan", "_progs", "_compact"):
+                    for k in ("_handle", "_handle_joint", "_plan", "_progs", "_compact", "_ev_sel"):
                         c.__dict__.pop(k, None)
                     c._handle = None
                     c._handle_joint = None
@@ -596,9 +597,11 @@ class PatternPlan:
             prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
             sel = self.__dict__.get("_ev_sel")
             if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
-                sel = self._ev_sel = [self.col_of[v] for v in self.ev_used]
-            if sel:
-                host["codes"].array[:, 0] = [codes[i] for i in sel]
+                idx = [self.col_of[v] for v in self.ev_used]
+                sel = self._ev_sel = ((lambda c, i=idx[0]: (c[i],)) if len(idx) == 1 else
+                                      itemgetter(*idx) if idx else None)
+            if sel is not None:
+                host["codes"].array[:, 0] = sel(codes)
             s = N.stream_handle(stream)
             prog.run(stream)
             N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block

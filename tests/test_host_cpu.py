@@ -444,6 +444,42 @@ def test_predict_output_frame_assembly():
     assert list(base.columns) == ["a", "f1", "f2", "c"]  # the input frame is not modified
 
 
+def test_query_name_checks_cached_per_model_structure(monkeypatch):
+    """VariableElimination.query skips the variable-name checks for a (query, evidence) name pair it
+    already checked, keyed on the model's structure epoch (ExactInference.py, C2 host path); the checks
+    themselves still raise as the reference does (ExactInference.py:292-300)."""
+    from pgmpy_amd.inference import VariableElimination
+    from pgmpy_amd.inference import plan as P
+    from pgmpy_amd.utils import get_example_model
+
+    class Runner:  # the device replay replaced by a constant: only the host path is under test
+        def __init__(self, plan, joint):
+            self.plan, self.joint = plan, joint
+
+        def run(self, codes):
+            assert len(codes) == len(self.plan.evidence_vars)
+            return np.full(self.plan.P if self.joint else self.plan.n_acc, 0.5)
+
+    monkeypatch.setattr(P, "QueryRunner", Runner)
+    m = get_example_model("alarm")
+    ve = VariableElimination(m)
+    ev = {"HR": "LOW", "CVP": "NORMAL"}
+    for _ in range(2):
+        f = ve.query(["BP"], ev, show_progress=False)
+        assert f.variables == ["BP"] and f.state_names["BP"] == m.states["BP"]
+    assert len(ve._valid_keys) == 1
+    with pytest.raises(ValueError):
+        ve.query(["BP"], {**ev, "BP": "LOW"}, show_progress=False)
+    with pytest.raises(KeyError):
+        ve.query(["BP"], {"HR": "NOPE", "CVP": "NORMAL"}, show_progress=False)
+    from pgmpy_amd.factors.discrete import TabularCPD
+
+    m.add_node("extra")  # a structural change: the names are checked again
+    m.add_cpds(TabularCPD("extra", 2, [[0.5], [0.5]]))
+    ve.query(["BP"], ev, show_progress=False)
+    assert len(ve._valid_keys) == 2
+
+
 def test_host_delivery_rejects_unknown_mode():
     """HostDelivery's ordering knob is one of three named modes (pgmpy_amd/distributed.py); a typo is an
     error, not a silent fallback to another ordering."""
