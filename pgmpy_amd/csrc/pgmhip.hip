@@ -593,6 +593,95 @@ static void coalesce(Dims &d, int nops) {
 
 static const bool g_no_rows2 = getenv("PGM_NO_ROWS2") != nullptr;  // tuning/testing: 8-B row paths only
 
+// Flat mode walks the outputs in the order of the kept dims (the last one fastest across lanes).  The
+// outputs, and each output's own reduction walk, are the same in any order, so the host may pick the
+// order whose wave-wide accesses touch the fewest cache lines: the given one (C's layout) or the kept
+// dims sorted by one operand's strides (that operand read in address order).  Cost of an order: the
+// 128-B lines one wave's 64 consecutive outputs touch, per operand, weighted by that operand's accesses
+// per output (A and B: one per reduction entry; C: one store, counted twice).  Bit-identical results.
+// Measured no faster on C1 / C2 / C4 (profiles/r04j/: the widest C2 level stays at 12 us), so off; A/B
+// knob PGM_CONTRACT_ORDER=1.
+static const bool g_keep_order = [] {
+  const char *e = getenv("PGM_CONTRACT_ORDER");
+  return e && e[0] == '1';
+}();
+
+// 128-B lines touched by each operand's accesses of the 64 consecutive outputs from out0 (digits walked
+// incrementally, all three operands at once)
+static void wave_lines(const Dims &kd, uint64_t out0, uint64_t n_out, uint64_t lines_out[3]) {
+  int64_t dig[PGM_MAX_DIMS], off[3] = {0, 0, 0};
+  uint64_t idx = out0;
+  for (int k = kd.n - 1; k >= 0; --k) {
+    dig[k] = (int64_t)(idx % (uint64_t)kd.card[k]);
+    idx /= (uint64_t)kd.card[k];
+    for (int t = 0; t < 3; ++t) off[t] += dig[k] * kd.s[t][k];
+  }
+  int64_t ln[3][64];
+  int n = 0;
+  for (uint64_t l = 0; l < 64 && out0 + l < n_out; ++l, ++n) {
+    for (int t = 0; t < 3; ++t) ln[t][n] = (off[t] * 8) >> 7;
+    for (int k = kd.n - 1; k >= 0; --k) {  // next output: innermost digit + 1 with carry
+      for (int t = 0; t < 3; ++t) off[t] += kd.s[t][k];
+      if (++dig[k] < kd.card[k]) break;
+      for (int t = 0; t < 3; ++t) off[t] -= kd.card[k] * kd.s[t][k];
+      dig[k] = 0;
+    }
+  }
+  for (int t = 0; t < 3; ++t) {
+    std::sort(ln[t], ln[t] + n);
+    lines_out[t] = (uint64_t)(std::unique(ln[t], ln[t] + n) - ln[t]);
+  }
+}
+
+static uint64_t order_cost(const Dims &kd, bool use_b, uint64_t n_red, uint64_t n_out) {
+  // two sample waves: the first, and one in the middle of the index space
+  const uint64_t w[2] = {0, (n_out / 2) & ~63ull};
+  uint64_t c = 0;
+  for (uint64_t o : w) {
+    uint64_t l[3];
+    wave_lines(kd, o, n_out, l);
+    c += n_red * (l[0] + (use_b ? l[1] : 0)) + 2 * l[2];
+  }
+  return c;
+}
+
+static void choose_keep_order(Dims &kd, bool use_b, uint64_t n_red, uint64_t n_out) {
+  if (!g_keep_order || kd.n < 2 || n_out < 4096 || kd.card[kd.n - 1] >= 64) return;
+  {  // the innermost dim already unit-stride or broadcast for every operand: nothing to gain
+    const int x = kd.n - 1;
+    const auto unit = [](int64_t v) { return v == 0 || v == 1 || v == -1; };
+    if (kd.s[2][x] == 1 && unit(kd.s[0][x]) && (!use_b || unit(kd.s[1][x]))) return;
+  }
+  Dims best = kd;
+  uint64_t best_cost = order_cost(kd, use_b, n_red, n_out);
+  for (int t = 0; t < 3; ++t) {
+    if (t == 1 && !use_b) continue;
+    // kept dims by descending |stride| of operand t (dims it broadcasts over first), stable
+    int perm[PGM_MAX_DIMS];
+    for (int i = 0; i < kd.n; ++i) perm[i] = i;
+    std::stable_sort(perm, perm + kd.n, [&](int a, int b) {
+      const int64_t sa = kd.s[t][a] < 0 ? -kd.s[t][a] : kd.s[t][a];
+      const int64_t sb = kd.s[t][b] < 0 ? -kd.s[t][b] : kd.s[t][b];
+      if ((sa == 0) != (sb == 0)) return sa == 0;
+      return sa > sb;
+    });
+    Dims cand;
+    cand.n = kd.n;
+    for (int i = 0; i < kd.n; ++i) {
+      cand.card[i] = kd.card[perm[i]];
+      for (int u = 0; u < 3; ++u) cand.s[u][i] = kd.s[u][perm[i]];
+    }
+    coalesce(cand, 3);
+    if (cand.n == 0 || cand.card[cand.n - 1] >= 64) continue;  // would change the kernel family
+    const uint64_t c = order_cost(cand, use_b, n_red, n_out);
+    if (c < best_cost) {
+      best_cost = c;
+      best = cand;
+    }
+  }
+  kd = best;
+}
+
 static const uint64_t kTargetThreads = 256ull * 2048;  // 256 CUs x 32 waves x 64 lanes
 
 struct ContractLaunch {
@@ -634,6 +723,7 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
                 (unsigned long long)n_out, (unsigned long long)n_red);
   coalesce(kd, 3);
   coalesce(rd, 2);
+  choose_keep_order(kd, d->combine != PGM_COMBINE_COPY, n_red, n_out);
   // few outputs (flat mode) and one long reduction run: cut the run into (outer x chunk) so the
   // split-K below has reduction-outer indices to distribute (a batched dot product over a packed
   // operand pair would otherwise leave 64 lanes per output walking the whole run)
@@ -3488,7 +3578,7 @@ static unsigned batch_levels_cap() {
 }
 
 // workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that); A/B
-// knob PGM_BATCH_MAX_BLOCKS
+// knob PGM_BATCH_MAX_BLOCKS (1,024 / 4,096: no change on C1 / C2 / C4, profiles/r04j/)
 static uint64_t batch_max_blocks() {
   static const uint64_t cap = [] {
     const char *e = getenv("PGM_BATCH_MAX_BLOCKS");
