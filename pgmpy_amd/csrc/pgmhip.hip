@@ -1569,6 +1569,43 @@ __global__ __launch_bounds__(256) void k_batch_wg(const BatchJob *__restrict__ j
   }
 }
 
+// A batch whose jobs are all contractions with one (combine, reduce) pair — every C2 / C1 path level —
+// runs this instead of k_batch: k_batch carries every job kind's code (167 KB of instructions, 123
+// VGPRs), this one only the two contraction bodies.  Same per-job code, so bit-identical results.  A/B
+// knob PGM_BATCH_SPECIALISE=0.
+template <int CMB, int RED>
+__global__ __launch_bounds__(256) void k_batch_c(const BatchJob *__restrict__ jobs,
+                                                 const uint32_t *__restrict__ block_job) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[b]);
+  const BatchJob &J = jobs[j];
+  const uint64_t tid = (uint64_t)(b - J.block0) * blockDim.x + threadIdx.x;
+  const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
+  if (J.c.row_mode == 2)
+    contract_flat2<CMB, RED>(J.c, J.A, J.B, J.C, tid, n);
+  else
+    contract_flat<CMB, RED>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0);
+}
+
+// The same for a batch of n-ary products only (C4's levelled BP sweep: the separator-sized products).
+__global__ __launch_bounds__(256) void k_batch_p(const BatchJob *__restrict__ jobs,
+                                                 const uint32_t *__restrict__ block_job) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[b]);
+  const BatchJob &J = jobs[j];
+  const uint64_t tid = (uint64_t)(b - J.block0) * blockDim.x + threadIdx.x;
+  const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
+  if (J.pn.pairs) {
+    if (J.pn.n_ops <= 2) prodn_flat2<2>(J.pn, J.C, tid, n);
+    else if (J.pn.n_ops <= 4) prodn_flat2<4>(J.pn, J.C, tid, n);
+    else prodn_flat2<PMAX>(J.pn, J.C, tid, n);
+    return;
+  }
+  if (J.pn.n_ops <= 2) prodn_flat<2>(J.pn, J.C, tid, n);
+  else if (J.pn.n_ops <= 4) prodn_flat<4>(J.pn, J.C, tid, n);
+  else prodn_flat<PMAX>(J.pn, J.C, tid, n);
+}
+
 __device__ __forceinline__ void batch_block(const BatchJob *__restrict__ jobs, const uint32_t *__restrict__ block_job,
                                             uint32_t b) {
   const uint32_t j = __builtin_amdgcn_readfirstlane(block_job[b]);
@@ -3555,6 +3592,7 @@ struct BatchHandle {
   unsigned grid = 0;          // persistent grid (levelled batch)
   unsigned long long timeout_ticks = 0;
   int32_t mode = PGM_BATCH_GRID;  // PGM_BATCH_ONE_WORKGROUP: k_batch_wg
+  int32_t spec = -1;  // every job a contraction with one (combine, reduce): combine * 3 + reduce; products: 100
 };
 
 // workgroups of k_batch_levels that are resident at once (the grid barrier needs all of them),
@@ -3575,6 +3613,32 @@ static unsigned batch_levels_cap() {
     }
   });
   return cap;
+}
+
+static const int32_t kBatchSpecProducts = 100;  // BatchHandle::spec of a products-only batch
+static const bool g_batch_specialise = [] {
+  const char *e = getenv("PGM_BATCH_SPECIALISE");
+  return !(e && e[0] == '0');
+}();
+
+template <int CMB>
+static void launch_batch_cr(int red, dim3 g, hipStream_t s, const BatchJob *jobs, const uint32_t *map) {
+  switch (red) {
+    case PGM_RED_NONE: hipLaunchKernelGGL((k_batch_c<CMB, PGM_RED_NONE>), g, dim3(256), 0, s, jobs, map); break;
+    case PGM_RED_SUM: hipLaunchKernelGGL((k_batch_c<CMB, PGM_RED_SUM>), g, dim3(256), 0, s, jobs, map); break;
+    default: hipLaunchKernelGGL((k_batch_c<CMB, PGM_RED_MAX>), g, dim3(256), 0, s, jobs, map); break;
+  }
+}
+
+static void launch_batch_c(int spec, dim3 g, hipStream_t s, const BatchJob *jobs, const uint32_t *map) {
+  const int red = spec % 3;
+  switch (spec / 3) {
+    case PGM_COMBINE_MUL: launch_batch_cr<PGM_COMBINE_MUL>(red, g, s, jobs, map); break;
+    case PGM_COMBINE_ADD: launch_batch_cr<PGM_COMBINE_ADD>(red, g, s, jobs, map); break;
+    case PGM_COMBINE_DIV: launch_batch_cr<PGM_COMBINE_DIV>(red, g, s, jobs, map); break;
+    case PGM_COMBINE_DIV_RAW: launch_batch_cr<PGM_COMBINE_DIV_RAW>(red, g, s, jobs, map); break;
+    default: launch_batch_cr<PGM_COMBINE_COPY>(red, g, s, jobs, map); break;
+  }
 }
 
 // workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that); A/B
@@ -3777,6 +3841,16 @@ int pgm_batch_finalize(void *handle) {
   if (h->d_jobs || h->jobs.empty()) return PGM_OK;
   if (h->level_off.back() < h->block_job.size()) h->level_off.push_back((uint32_t)h->block_job.size());
   const size_t n_levels = h->level_off.size() - 1;
+  h->spec = -1;
+  if (g_batch_specialise) {
+    bool uni = true;
+    for (const BatchJob &J : h->jobs)
+      uni = uni && J.kind == 0 && J.cmb == h->jobs[0].cmb && J.red == h->jobs[0].red;
+    if (uni) h->spec = h->jobs[0].cmb * 3 + h->jobs[0].red;
+    bool prod = true;
+    for (const BatchJob &J : h->jobs) prod = prod && J.kind == 2;
+    if (prod) h->spec = kBatchSpecProducts;
+  }
   hipError_t e = hipMalloc((void **)&h->d_jobs, sizeof(BatchJob) * h->jobs.size());
   if (e == hipSuccess) e = hipMalloc((void **)&h->d_map, sizeof(uint32_t) * h->block_job.size());
   if (e == hipSuccess)
@@ -3827,6 +3901,10 @@ int pgm_batch_run(void *handle, void *stream) {
     for (uint32_t l = 0; l < n_levels; ++l)
       hipLaunchKernelGGL(k_batch, dim3(h->level_off[l + 1] - h->level_off[l]), dim3(256), 0, S(stream), h->d_jobs,
                          h->d_map + h->level_off[l]);
+  } else if (h->spec == kBatchSpecProducts) {
+    hipLaunchKernelGGL(k_batch_p, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
+  } else if (h->spec >= 0) {
+    launch_batch_c(h->spec, dim3((unsigned)h->block_job.size()), S(stream), h->d_jobs, h->d_map);
   } else {
     hipLaunchKernelGGL(k_batch, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
   }
