@@ -1553,6 +1553,68 @@ __global__ __launch_bounds__(256) void k_batch_levels(const BatchJob *__restrict
   }
 }
 
+// A single-workgroup levelled batch of contractions only (the tail of a contraction path, C1 / C2): the
+// job descriptors (contraction part only), the block map and the level table are copied into LDS once at
+// the start — every load of them independent, issued together — so each level's blocks read their
+// descriptor from LDS instead of a block-map load followed by a dependent descriptor load from memory
+// (two round trips per level).  Same per-job code as k_batch_wg, so the same results bit for bit.
+struct alignas(16) ChainJob {
+  int32_t cmb, red;
+  uint32_t block0, nblocks;
+  const double *A, *B;
+  double *C;
+  ContractK c;
+};
+
+template <int CMB>
+__device__ __forceinline__ void chain_contract_c(const ChainJob &J, uint64_t tid, uint64_t n) {
+  if (J.c.row_mode == 2) {
+    switch (J.red) {
+      case PGM_RED_NONE: contract_flat2<CMB, PGM_RED_NONE>(J.c, J.A, J.B, J.C, tid, n); break;
+      case PGM_RED_SUM: contract_flat2<CMB, PGM_RED_SUM>(J.c, J.A, J.B, J.C, tid, n); break;
+      default: contract_flat2<CMB, PGM_RED_MAX>(J.c, J.A, J.B, J.C, tid, n); break;
+    }
+    return;
+  }
+  switch (J.red) {
+    case PGM_RED_NONE: contract_flat<CMB, PGM_RED_NONE>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+    case PGM_RED_SUM: contract_flat<CMB, PGM_RED_SUM>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+    default: contract_flat<CMB, PGM_RED_MAX>(J.c, J.A, J.B, J.C, nullptr, tid, n, 0); break;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_batch_wg_c(const ChainJob *__restrict__ jobs,
+                                                    const uint32_t *__restrict__ block_job,
+                                                    const uint32_t *__restrict__ level_off, uint32_t n_levels,
+                                                    uint32_t n_jobs, uint32_t n_blocks) {
+  extern __shared__ uint4 chain_lds[];
+  const uint32_t jq = n_jobs * (uint32_t)(sizeof(ChainJob) / 16);
+  const uint4 *src = reinterpret_cast<const uint4 *>(jobs);
+  for (uint32_t i = threadIdx.x; i < jq; i += blockDim.x) chain_lds[i] = src[i];
+  uint32_t *lmap = reinterpret_cast<uint32_t *>(chain_lds + jq);
+  for (uint32_t i = threadIdx.x; i < n_blocks; i += blockDim.x) lmap[i] = block_job[i];
+  uint32_t *llev = lmap + n_blocks;
+  for (uint32_t i = threadIdx.x; i <= n_levels; i += blockDim.x) llev[i] = level_off[i];
+  __syncthreads();
+  const ChainJob *sj = reinterpret_cast<const ChainJob *>(chain_lds);
+  for (uint32_t l = 0; l < n_levels; ++l) {
+    const uint32_t e = llev[l + 1];
+    for (uint32_t b = llev[l]; b < e; ++b) {
+      const ChainJob &J = sj[lmap[b]];
+      const uint64_t tid = (uint64_t)(b - J.block0) * blockDim.x + threadIdx.x;
+      const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
+      switch (J.cmb) {
+        case PGM_COMBINE_MUL: chain_contract_c<PGM_COMBINE_MUL>(J, tid, n); break;
+        case PGM_COMBINE_ADD: chain_contract_c<PGM_COMBINE_ADD>(J, tid, n); break;
+        case PGM_COMBINE_DIV: chain_contract_c<PGM_COMBINE_DIV>(J, tid, n); break;
+        case PGM_COMBINE_DIV_RAW: chain_contract_c<PGM_COMBINE_DIV_RAW>(J, tid, n); break;
+        default: chain_contract_c<PGM_COMBINE_COPY>(J, tid, n); break;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Several tiny dependent levels in ONE workgroup: each level's blocks run one after another on the same
 // 256 threads, a workgroup barrier after each (the block bodies may use LDS; the next level reads what
 // this workgroup wrote, which a workgroup-scope release/acquire makes visible).  Replaces one launch per
@@ -3593,6 +3655,8 @@ struct BatchHandle {
   unsigned long long timeout_ticks = 0;
   int32_t mode = PGM_BATCH_GRID;  // PGM_BATCH_ONE_WORKGROUP: k_batch_wg
   int32_t spec = -1;  // every job a contraction with one (combine, reduce): combine * 3 + reduce; products: 100
+  ChainJob *d_chain = nullptr;  // ONE_WORKGROUP batch of contractions only: descriptors staged in LDS
+  size_t chain_lds = 0;         // dynamic LDS bytes of k_batch_wg_c
 };
 
 // workgroups of k_batch_levels that are resident at once (the grid barrier needs all of them),
@@ -3616,6 +3680,13 @@ static unsigned batch_levels_cap() {
 }
 
 static const int32_t kBatchSpecProducts = 100;  // BatchHandle::spec of a products-only batch
+// single-workgroup chains of contractions: descriptors staged in LDS (k_batch_wg_c) up to this many bytes
+// of tables; A/B knob PGM_CHAIN_LDS=0 for k_batch_wg
+static const size_t kChainLdsMax = 48 * 1024;
+static const bool g_chain_lds = [] {
+  const char *e = getenv("PGM_CHAIN_LDS");
+  return !(e && e[0] == '0');
+}();
 static const bool g_batch_specialise = [] {
   const char *e = getenv("PGM_BATCH_SPECIALISE");
   return !(e && e[0] == '0');
@@ -3828,6 +3899,9 @@ static void batch_free(BatchHandle *h) {
   if (h->d_map) (void)hipFree(h->d_map);
   if (h->d_level) (void)hipFree(h->d_level);
   if (h->d_bar) (void)hipFree(h->d_bar);
+  if (h->d_chain) (void)hipFree(h->d_chain);
+  h->d_chain = nullptr;
+  h->chain_lds = 0;
   h->d_jobs = nullptr;
   h->d_map = nullptr;
   h->d_level = nullptr;
@@ -3861,6 +3935,29 @@ int pgm_batch_finalize(void *handle) {
     e = hipMalloc((void **)&h->d_level, sizeof(uint32_t) * h->level_off.size());
     if (e == hipSuccess)
       e = hipMemcpy(h->d_level, h->level_off.data(), sizeof(uint32_t) * h->level_off.size(), hipMemcpyHostToDevice);
+    // contractions only, and the staged tables fit the LDS budget: k_batch_wg_c
+    bool contract_only = g_chain_lds;
+    for (const BatchJob &J : h->jobs) contract_only = contract_only && J.kind == 0;
+    const size_t lds = h->jobs.size() * sizeof(ChainJob) + 4 * (h->block_job.size() + h->level_off.size());
+    if (e == hipSuccess && contract_only && lds <= kChainLdsMax) {
+      std::vector<ChainJob> cj(h->jobs.size());
+      for (size_t i = 0; i < h->jobs.size(); ++i) {
+        const BatchJob &J = h->jobs[i];
+        ChainJob &c = cj[i];
+        memset(&c, 0, sizeof c);
+        c.cmb = J.cmb;
+        c.red = J.red;
+        c.block0 = J.block0;
+        c.nblocks = J.nblocks;
+        c.A = J.A;
+        c.B = J.B;
+        c.C = J.C;
+        c.c = J.c;
+      }
+      e = hipMalloc((void **)&h->d_chain, sizeof(ChainJob) * cj.size());
+      if (e == hipSuccess) e = hipMemcpy(h->d_chain, cj.data(), sizeof(ChainJob) * cj.size(), hipMemcpyHostToDevice);
+      if (e == hipSuccess) h->chain_lds = lds;
+    }
     if (e == hipSuccess) e = hipDeviceSynchronize();
   } else if (e == hipSuccess && n_levels > 1) {
     uint32_t widest = 0;
@@ -3892,7 +3989,10 @@ int pgm_batch_run(void *handle, void *stream) {
   if (h->jobs.empty()) return PGM_OK;
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
   const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
-  if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
+  if (h->mode == PGM_BATCH_ONE_WORKGROUP && h->d_chain) {
+    hipLaunchKernelGGL(k_batch_wg_c, dim3(1), dim3(256), h->chain_lds, S(stream), (const ChainJob *)h->d_chain,
+                       h->d_map, h->d_level, n_levels, (uint32_t)h->jobs.size(), (uint32_t)h->block_job.size());
+  } else if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
     hipLaunchKernelGGL(k_batch_wg, dim3(1), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level, n_levels);
   } else if (n_levels > 1 && h->grid > 0) {
     hipLaunchKernelGGL(k_batch_levels, dim3(h->grid), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level,
