@@ -1583,26 +1583,31 @@ __device__ __forceinline__ void chain_contract_c(const ChainJob &J, uint64_t tid
   }
 }
 
-__global__ __launch_bounds__(256) void k_batch_wg_c(const ChainJob *__restrict__ jobs,
+// 1,024 threads = kChainVB virtual 256-thread blocks: a level's blocks run kChainVB at a time (each
+// virtual block's 4 waves as one block of k_batch), one workgroup barrier per level.
+static constexpr uint32_t kChainVB = 4;
+
+__global__ __launch_bounds__(256 * kChainVB) void k_batch_wg_c(const ChainJob *__restrict__ jobs,
                                                     const uint32_t *__restrict__ block_job,
                                                     const uint32_t *__restrict__ level_off, uint32_t n_levels,
                                                     uint32_t n_jobs, uint32_t n_blocks) {
   extern __shared__ uint4 chain_lds[];
   const uint32_t jq = n_jobs * (uint32_t)(sizeof(ChainJob) / 16);
   const uint4 *src = reinterpret_cast<const uint4 *>(jobs);
-  for (uint32_t i = threadIdx.x; i < jq; i += blockDim.x) chain_lds[i] = src[i];
+  for (uint32_t i = threadIdx.x; i < jq; i += blockDim.x) chain_lds[i] = src[i];  // all loads independent
   uint32_t *lmap = reinterpret_cast<uint32_t *>(chain_lds + jq);
   for (uint32_t i = threadIdx.x; i < n_blocks; i += blockDim.x) lmap[i] = block_job[i];
   uint32_t *llev = lmap + n_blocks;
   for (uint32_t i = threadIdx.x; i <= n_levels; i += blockDim.x) llev[i] = level_off[i];
   __syncthreads();
   const ChainJob *sj = reinterpret_cast<const ChainJob *>(chain_lds);
+  const uint32_t vb = threadIdx.x / 256, lt = threadIdx.x % 256;
   for (uint32_t l = 0; l < n_levels; ++l) {
     const uint32_t e = llev[l + 1];
-    for (uint32_t b = llev[l]; b < e; ++b) {
+    for (uint32_t b = llev[l] + vb; b < e; b += kChainVB) {
       const ChainJob &J = sj[lmap[b]];
-      const uint64_t tid = (uint64_t)(b - J.block0) * blockDim.x + threadIdx.x;
-      const uint64_t n = (uint64_t)J.nblocks * blockDim.x;
+      const uint64_t tid = (uint64_t)(b - J.block0) * 256 + lt;
+      const uint64_t n = (uint64_t)J.nblocks * 256;
       switch (J.cmb) {
         case PGM_COMBINE_MUL: chain_contract_c<PGM_COMBINE_MUL>(J, tid, n); break;
         case PGM_COMBINE_ADD: chain_contract_c<PGM_COMBINE_ADD>(J, tid, n); break;
@@ -1610,8 +1615,8 @@ __global__ __launch_bounds__(256) void k_batch_wg_c(const ChainJob *__restrict__
         case PGM_COMBINE_DIV_RAW: chain_contract_c<PGM_COMBINE_DIV_RAW>(J, tid, n); break;
         default: chain_contract_c<PGM_COMBINE_COPY>(J, tid, n); break;
       }
-      __syncthreads();
     }
+    __syncthreads();  // the level's outputs are complete before the next level reads them
   }
 }
 
@@ -3712,6 +3717,17 @@ static void launch_batch_c(int spec, dim3 g, hipStream_t s, const BatchJob *jobs
   }
 }
 
+// a batch contraction job with a reduction takes G lanes per output (G a power of two up to the innermost
+// reduction extent) while its outputs x G stay under this many lanes; A/B knob PGM_BATCH_LANES
+static uint64_t batch_lanes_cap() {
+  static const uint64_t cap = [] {
+    const char *e = getenv("PGM_BATCH_LANES");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint64_t)v : (uint64_t)4096;
+  }();
+  return cap;
+}
+
 // workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that); A/B
 // knob PGM_BATCH_MAX_BLOCKS (1,024 / 4,096: no change on C1 / C2 / C4, profiles/r04j/)
 static uint64_t batch_max_blocks() {
@@ -3783,7 +3799,7 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   k.red_chunk = k.n_ro;
   // (a single-workgroup levelled batch runs its blocks one after another: spread a job over at most
   // one block's lanes there)
-  const uint64_t lanes_cap = h->mode == PGM_BATCH_ONE_WORKGROUP ? 256 : 4096;
+  const uint64_t lanes_cap = h->mode == PGM_BATCH_ONE_WORKGROUP ? 256 : batch_lanes_cap();
   int g = 0;
   if (d->reduce != PGM_RED_NONE && (uint64_t)k.n_ro * k.ri_card > 1)
     while (g < 6 && ((uint64_t)k.n_out << g) < lanes_cap && (1u << (g + 1)) <= k.ri_card) ++g;
@@ -3990,7 +4006,7 @@ int pgm_batch_run(void *handle, void *stream) {
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
   const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
   if (h->mode == PGM_BATCH_ONE_WORKGROUP && h->d_chain) {
-    hipLaunchKernelGGL(k_batch_wg_c, dim3(1), dim3(256), h->chain_lds, S(stream), (const ChainJob *)h->d_chain,
+    hipLaunchKernelGGL(k_batch_wg_c, dim3(1), dim3(256 * kChainVB), h->chain_lds, S(stream), (const ChainJob *)h->d_chain,
                        h->d_map, h->d_level, n_levels, (uint32_t)h->jobs.size(), (uint32_t)h->block_job.size());
   } else if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
     hipLaunchKernelGGL(k_batch_wg, dim3(1), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level, n_levels);

@@ -35,13 +35,14 @@ PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 14))  # C4 1,000 ro
 # with its agent-scope write-back / invalidate costs more than a kernel boundary), so off by default.
 LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
 # plain programs: consecutive dependency levels of at most this many 256-thread blocks each run in ONE
-# single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP: the levels' blocks one after another with a
-# workgroup barrier between them) instead of one launch each — the tail of a contraction path (C1 / C2:
-# the last levels down to the query marginal, then its normalisation).  Measured no faster (r03aa: C2
-# 0.215-0.221 ms/query with chains of <= 4-block levels against 0.208-0.210 without; C1 0.082-0.095 vs
-# 0.082-0.084): a tiny level's cost is its dependent load chain, not the launch, so it stays an A/B knob
-# (0 = off, the default; the test sets it).
-WG_CHAIN_BLOCKS = int(os.environ.get("PGM_WG_CHAIN_BLOCKS", 0))
+# single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP: a level's blocks four at a time in a
+# 1,024-thread workgroup, a workgroup barrier between levels) instead of one launch each — the tail of a
+# contraction path (C1 / C2: the last levels down to the query marginal, then its normalisation).  r03
+# measured it no faster with the generic batch kernel, one 256-thread block at a time (C2 0.215-0.221
+# ms/query against 0.208-0.210); r04's contraction-only chain kernel stages the descriptors in LDS
+# (k_batch_wg_c): C2 0.173-0.174 against 0.179 ms, C1 0.067 against 0.069-0.071 (profiles/r04o/; 8 or
+# more blocks per level: C1 slower).  0 = one launch per level.
+WG_CHAIN_BLOCKS = int(os.environ.get("PGM_WG_CHAIN_BLOCKS", 4))
 # a plain Program's batch of ONE job: the job's own launch (pgm_contract / pgm_gather: the planner may
 # split a long reduction; the descriptor travels by value in the kernel arguments) or, with
 # PGM_ONE_JOB_AS_BATCH=1 (A/B knob), a one-job pgm_batch launch (descriptor in device memory)

@@ -700,7 +700,7 @@ def test_levelled_batch_chain_matches_numpy(gpu, monkeypatch):
 
 def test_single_workgroup_level_chain_matches_numpy(gpu, monkeypatch):
     """A plain Program's consecutive tiny levels (batches of at most PGM_WG_CHAIN_BLOCKS blocks) run as
-    ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP / k_batch_wg): two interleaved chains
+    ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP / k_batch_wg_c): two interleaved chains
     of dependent contractions, a wide level in the middle that keeps its own launch, a chain after it;
     every level equals numpy, on repeated runs and through a captured HIP graph."""
     import torch
@@ -708,7 +708,7 @@ def test_single_workgroup_level_chain_matches_numpy(gpu, monkeypatch):
     import pgmpy_amd.program as P
     from pgmpy_amd.program import Program
 
-    monkeypatch.setattr(P, "WG_CHAIN_BLOCKS", 4)  # off by default (no faster on C1 / C2), tested here
+    monkeypatch.setattr(P, "WG_CHAIN_BLOCKS", 4)  # the default since r04; pinned here
     E = _e()
     rng = np.random.default_rng(11)
     n_a, n_b = 6, 5  # tiny levels before / after the wide one
