@@ -107,6 +107,7 @@ class Program:
         self.merged_parts = {}  # step index -> full notes of the specialised steps merged into it
         self._plain_recs = []  # plain Program: one record per launch / batch job (check_hazards only)
         self._unit = 0  # plain Program: launch counter behind _Rec.step
+        self._plain_lowered = -1  # plain Program: len(_steps) right after the last lowering
 
     # ------------------------------------------------------------------ batching
     def begin_batch(self):
@@ -289,7 +290,9 @@ class Program:
     def _lower(self):
         """Levelled Program -> steps: per level, its unbatched launches then one batch launch."""
         if not self._levels:
-            self._lower_batches()
+            if len(self._steps) != self._plain_lowered:  # steps recorded since the last lowering
+                self._lower_batches()
+                self._plain_lowered = len(self._steps)
             return
         if self._lowered:
             return
@@ -679,10 +682,12 @@ class Program:
 
     # ------------------------------------------------------------------ execution
     def run(self, stream=None):
-        self._ready()
+        g = self._graph
+        if g is None:  # a captured program was lowered and prepared before its capture
+            self._ready()
         s = N.stream_handle(stream)
-        if self._graph is not None:
-            N.check(N.lib().pgm_graph_launch(self._graph, s), "graph_launch")
+        if g is not None:
+            N.check(N.lib().pgm_graph_launch(g, s), "graph_launch")
         else:
             for step in self._steps:
                 step(s)
