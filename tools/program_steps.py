@@ -23,6 +23,7 @@ def main():
         bjt = BatchedJunctionTree(junction_tree_from_model(m))
         leaves = sorted(v for v in m.nodes() if m.out_degree(v) == 0)
         sch = bjt.schedule(n, leaves, graph=False, marginals=False)
+        sch.codes.zero_()  # valid evidence (state 0 everywhere): the findings kernels flag bad codes
         prog = sch.prog
     else:
         import random
