@@ -3763,9 +3763,23 @@ int pgm_batch_create(void **handle) {
   return *handle ? PGM_OK : fail(PGM_ENOMEM, "batch_create: host allocation");
 }
 
-static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads) {
+// a batch contraction without a reduction (a broadcast product or a copy: one load per operand per output)
+// may take more workgroups than one that reduces: its lanes otherwise walk several outputs one after
+// another, a full memory round trip each (C2's 448,000-output product level: 11.7 -> 8.9 us at 1,024
+// blocks, profiles/r04t/), while the reducing jobs of a level were measured slower with more; A/B knob
+// PGM_BATCH_MAX_BLOCKS_PRODUCT
+static uint64_t batch_max_blocks_product() {
+  static const uint64_t cap = [] {
+    const char *e = getenv("PGM_BATCH_MAX_BLOCKS_PRODUCT");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint64_t)std::min(v, 1L << 20) : (uint64_t)1024;
+  }();
+  return cap;
+}
+
+static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads, uint64_t cap = 0) {
   if (h->d_jobs) return fail(PGM_EINVAL, "batch: already finalized");
-  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), batch_max_blocks());
+  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), cap ? cap : batch_max_blocks());
   if (h->block_job.size() + nb > 0x7fffffffull) return fail(PGM_EINVAL, "batch: too many blocks");
   J.block0 = (uint32_t)h->block_job.size();
   J.nblocks = (uint32_t)nb;
@@ -3816,9 +3830,9 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   if (pairs) pairs = (!va || (k.ri_sa % 2 == 0 && ((uintptr_t)A & 15) == 0)) && (!vb || (k.ri_sb % 2 == 0 && ((uintptr_t)B & 15) == 0));
   if (pairs) {
     k.row_mode = 2;
-    return batch_append(h, J, (uint64_t)k.n_out / 2);
+    return batch_append(h, J, (uint64_t)k.n_out / 2, k.n_red <= 1 ? batch_max_blocks_product() : 0);
   }
-  return batch_append(h, J, (uint64_t)k.n_out << g);
+  return batch_append(h, J, (uint64_t)k.n_out << g, k.n_red <= 1 ? batch_max_blocks_product() : 0);
 }
 
 int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
