@@ -731,6 +731,12 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.red = reduce;
   sp.XI = XI;
   sp.unroll = unroll;
+  // a step of few blocks (C4 at 1,000 rows) has few waves per CU to hide its loads: a longer unroll keeps
+  // more of a lane's entries in flight.  A/B knob PGM_PM_UNROLL_SMALL = block count below which the unroll is
+  // PGM_PM_UNROLL_SMALL_N (default 16); 0 (the default) = off
+  static const int small_blocks = pm_knob("PGM_PM_UNROLL_SMALL", 0);
+  static const int small_unroll = pm_knob("PGM_PM_UNROLL_SMALL_N", 16);
+  if (small_blocks > 0 && total < (uint64_t)small_blocks) sp.unroll = small_unroll;
   sp.store = C != nullptr;
   sp.has_m = has_m;
   // PGM_PM_XCD: 1 = XCD grouping when the block count is a multiple of 8, 2 = always (bijective remap)
