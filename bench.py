@@ -709,6 +709,9 @@ def bench_c3(args, dist, rank, world):
             result["cpu_baseline"]["cores_on_host"] = os.cpu_count()
         if world == 1 and not args.no_api_e2e:
             result["api_e2e"] = api_e2e_rate(model, codes_all, nodes, missing)
+    if not args.no_c5:
+        result["c5"] = c5_subline(args, dist, rank, world, model, variables, observed, plan, codes_ev, d_codes,
+                                  rows * nb)
     if dist is not None:
         # the result delivery (outside the timed region in this weak-scaling line; --workload c5
         # times it inside the step): every rank's [17, rows] marginals to rank 0
@@ -722,6 +725,85 @@ def bench_c3(args, dist, rank, world):
         result["gather_ms"] = (time.perf_counter() - g0) * 1e3
         result["gather_backend"] = _BACKEND
     return result
+
+
+def host_dma_probe(nbytes=136_000_000, reps=8):
+    """How much device-to-host DMA one GPU's host link takes with one and with two concurrent streams
+    (each stream its own pinned host buffer and device source): the ceiling C5's host delivery runs at
+    per rank (Multi-GPU).  GB/s = bytes copied / wall time of all copies."""
+    import torch
+
+    from pgmpy_amd import _native as N
+
+    n = nbytes // 8
+    src = [torch.ones(n, dtype=torch.float64, device="cuda") for _ in range(2)]
+    dst = [torch.empty(n, dtype=torch.float64, pin_memory=True) for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    L = N.lib()
+
+    def copy(i, nb):
+        N.check(L.pgm_memcpy_d2h_async(ctypes.c_void_p(dst[i].data_ptr()), N.ptr(src[i]), nb,
+                                       N.stream_handle(streams[i])), "memcpy_d2h_async")
+
+    def run(n_streams, nb):
+        for i in range(n_streams):
+            copy(i, nb)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for i in range(n_streams):
+                copy(i, nb)
+        torch.cuda.synchronize()
+        return n_streams * nb * reps / (time.perf_counter() - t0) / 1e9
+
+    one = run(1, n * 8)
+    two_split = run(2, n * 4)  # the same bytes split over two streams
+    two_full = run(2, n * 8)   # twice the bytes, one full copy per stream
+    ok = bool(dst[0][:4].sum().item() == 4.0)
+    del src, dst
+    return {"bytes_per_copy": n * 8, "reps": reps, "one_stream_GBps": one, "two_streams_split_GBps": two_split,
+            "two_streams_full_GBps": two_full, "copies_checked": ok}
+
+
+def c5_subline(args, dist, rank, world, model, variables, observed, plan, codes_host, d_codes, ld):
+    """BASELINE.json configs[4] inside the default line: 1 M rows per step split
+    over the N ranks (strong scaling), each rank's block taken from its C3 resident rows (batch 0 and
+    its seeded permutations), timed three ways after the C3 window: delivered to pinned host memory per
+    rank (predict_probability's marginals, and predict's MAP indices), and gathered to rank 0 over
+    RCCL (bench_c5).  Every rank runs it (collectives inside); rank 0's dict is reported."""
+    import copy
+
+    from pgmpy_amd.distributed import shard_bounds
+
+    total = 1_000_000
+    lo, hi = shard_bounds(total, world, rank)
+    rows5 = hi - lo
+    if rows5 > ld:
+        return {"skipped": f"{rows5} rows per rank exceed the {ld} resident C3 rows"}
+    inp = {"model": model, "variables": variables, "observed": observed, "plan": plan, "codes_host": codes_host,
+           "d_codes": d_codes, "ld": ld, "rows": rows5, "total": total,
+           "data": "synthetic (rank r's C3 resident rows: forward-sampled with seed 42+r and seeded row "
+                   "permutations of them)"}
+    out = {"workload": "C5 (BASELINE.json configs[4]): munin predict_probability / predict template, 1M rows per "
+                       "step split over the ranks (strong scaling)",
+           "global_rows_per_step": total, "rows_per_gpu_per_step": rows5, "n_gpus": world}
+    keep = ("value", "unit", "ms_per_step", "steps", "kernel_ms", "copy_ms", "copy_bytes_per_rank", "copy_GBps",
+            "pipelined_step_over_copy", "gather_ms", "launch_ms", "gather_backend", "gather_bytes_to_rank0",
+            "roofline", "parity")
+    for name, fn, output in (("host", bench_c5_host, "marginals"), ("host_map", bench_c5_host, "map"),
+                             ("rccl", bench_c5, "marginals")):
+        a = copy.copy(args)
+        a.rows, a.c5_output = total, output
+        try:
+            r = fn(a, dist, rank, world, inp=inp)
+            out[name] = {k: r[k] for k in keep if k in r}
+            out[name]["delivery"] = r["config"].get("delivery", "rccl" if fn is bench_c5 else "host")
+        except Exception as e:  # reported, never silently dropped; the headline stands on its own
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+    out["value"] = out["host"].get("value")
+    if rank == 0:
+        out["host_dma_probe"] = host_dma_probe()
+    return out
 
 
 def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_codes, outs, err, codes_all, nodes,
@@ -853,17 +935,10 @@ def bench_c3_ring(args, dist, rank, world, model, missing, variables, plan, d_co
     return result
 
 
-def bench_c5_host(args, dist, rank, world):
-    """C5 delivered to host memory (the default, --c5-delivery host): every rank writes its block's
-    results into pinned host memory of its node over its OWN host link, with no collective — the
-    result of predict_probability / predict is a host DataFrame, and a funnel into one GPU (the RCCL
-    gather, --c5-delivery rccl) moves every row's 136 B through rank 0's links.  One step = each
-    rank's fused-plan launch over its block (device-resident evidence) into device buffer k % 2 +
-    the DMA of that buffer into pinned host buffer k % 2, ordered as HostDelivery's mode says (default
-    "lanes": launch k and copy k on stream lane k % 2, so copy k overlaps launch k + 1)."""
-    import torch
-
-    from pgmpy_amd.distributed import HostDelivery, shard_bounds
+def c5_inputs(args, rank, world):
+    """C5's own inputs (--workload c5): rank r's contiguous block of the 1 M rows, forward-sampled with
+    seed (42, first row of the block), all 1,038 observed columns resident on the device."""
+    from pgmpy_amd.distributed import shard_bounds
     from pgmpy_amd.inference.batch import upload_codes
     from pgmpy_amd.inference.plan import PatternPlan
     from pgmpy_amd.utils import get_example_model
@@ -875,14 +950,87 @@ def bench_c5_host(args, dist, rank, world):
     total = args.rows
     lo, hi = shard_bounds(total, world, rank)
     rows = hi - lo
+    t0 = time.perf_counter()
     codes_all, nodes = forward_sample_codes(model, rows, seed=(42, lo))
     observed = [v for v in nodes if v not in set(variables)]
     pos = {v: i for i, v in enumerate(nodes)}
     codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])
     del codes_all
+    log(f"[rank {rank}] rows [{lo}, {hi}) sampled in {time.perf_counter() - t0:.1f}s")
     plan = PatternPlan(model, variables, observed, {v: i for i, v in enumerate(observed)})
     assert plan.kind == "fused", plan.describe()
-    d_codes = upload_codes(codes_ev)
+    return {"model": model, "variables": variables, "observed": observed, "plan": plan, "codes_host": codes_ev,
+            "d_codes": upload_codes(codes_ev), "ld": rows, "rows": rows, "total": total,
+            "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))"}
+
+
+def rotating_roofline(plan, codes_host, rows, want_map, err, steps, min_over_mall=4.2):
+    """Per-launch roofline of the fused pass at `rows` rows with an HBM-sized working set: nb batches,
+    each its own compact evidence columns (the plan's used columns, batch i a seeded row permutation of
+    codes_host's first `rows` rows) and its own output buffer, nb x (bytes per launch) >= min_over_mall x
+    the 256 MiB Infinity Cache; back-to-back launches on one stream rotate over them, so no launch finds
+    its outputs or inputs still in the MALL.  kernel_ms = HIP-event span / launches (a rocprofv3 kernel
+    trace of the same command reports each launch)."""
+    import math
+
+    import torch
+
+    from pgmpy_amd.inference.batch import upload_codes
+
+    cp = plan.compact()
+    bpr = plan.algorithmic_bytes_per_row(marginals=not want_map, map_=want_map)
+    nb = max(2, math.ceil(min_over_mall * MALL_BYTES / (bpr * rows)))
+    used = codes_host[[plan.col_of[v] for v in plan.ev_used], :rows]
+    prng = np.random.default_rng(2025)
+    host = np.empty((used.shape[0], rows * nb), dtype=np.uint8)
+    for i in range(nb):
+        host[:, i * rows:(i + 1) * rows] = used if i == 0 else used[:, prng.permutation(rows)]
+    d = upload_codes(host)
+    outs = [cp.alloc_outputs(rows, marginals=not want_map, map_=want_map) for _ in range(nb)]
+    st = torch.cuda.Stream(device=d.device)
+    bounds = [cp.bind(d, rows * nb, i * rows, rows, outs[i], err=err, stream=st) for i in range(nb)]
+    n_launch = max(steps, 2 * nb)
+    with torch.cuda.stream(st):
+        for b in bounds:  # first use: every buffer touched once
+            b.run()
+        timer = HipTimer()
+        timer.start()
+        for j in range(n_launch):
+            bounds[j % nb].run()
+        timer.mark_end()
+    torch.cuda.synchronize()
+    ms = timer.elapsed_ms() / n_launch
+    assert int(err.item()) == 0
+    kname, k_blocks, k_wg = bounds[0].kernel()
+    del bounds, outs, d
+    ws = bpr * rows * nb
+    achieved = bpr * rows / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
+            "grid": {"blocks": k_blocks, "workgroup": k_wg}, "kernel_ms": ms, "launches": n_launch,
+            "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows, "rotating_batches": nb,
+            "working_set_bytes": ws, "working_set_over_mall": ws / MALL_BYTES,
+            "working_set_exceeds_mall": ws > MALL_BYTES,
+            "kernel_ms_note": "HIP-event span / launches of back-to-back launches on one stream, each batch its "
+                              "own compact evidence columns and output buffer, rotating (outside the window)"}
+
+
+def bench_c5_host(args, dist, rank, world, inp=None):
+    """C5 delivered to host memory (the default, --c5-delivery host): every rank writes its block's
+    results into pinned host memory of its node over its OWN host link, with no collective — the
+    result of predict_probability / predict is a host DataFrame, and a funnel into one GPU (the RCCL
+    gather, --c5-delivery rccl) moves every row's 136 B through rank 0's links.  One step = each
+    rank's fused-plan launch over its block (device-resident evidence) into device buffer k % 2 +
+    the DMA of that buffer into pinned host buffer k % 2, ordered as HostDelivery's mode says (default
+    "lanes": launch k and copy k on stream lane k % 2, so copy k overlaps launch k + 1).
+    `inp` (c5_inputs' dict) lets the default C3 line run this step on its own resident rows."""
+    import torch
+
+    from pgmpy_amd.distributed import HostDelivery
+
+    inp = inp or c5_inputs(args, rank, world)
+    plan, variables, observed = inp["plan"], inp["variables"], inp["observed"]
+    d_codes, ld, rows, total, codes_ev = inp["d_codes"], inp["ld"], inp["rows"], inp["total"], inp["codes_host"]
     dev = d_codes.device
     want_map = args.c5_output == "map"
     key = "map" if want_map else "marg"
@@ -891,10 +1039,8 @@ def bench_c5_host(args, dist, rank, world):
     hosts = delivery.hosts
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     ls = torch.cuda.Stream(device=dev)
-    bounds = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=delivery.launch_stream(i, ls))
+    bounds = [plan.bind(d_codes, ld, 0, rows, outs[i], err=err, stream=delivery.launch_stream(i, ls))
               for i in range(2)]
-    single = plan.bind(d_codes, rows, 0, rows, outs[0], err=err, stream=ls)
-    kname, k_blocks, k_wg = bounds[0].kernel()
 
     def step(k):
         s = delivery.launch_stream(k, ls)
@@ -915,14 +1061,10 @@ def bench_c5_host(args, dist, rank, world):
     barrier(dist)
     elapsed = max_over_ranks(dist, t_end - t_start)
     assert int(err.item()) == 0
-    # the parts alone, outside the window: the launch, and the copy-out (each back to back, one stream)
-    timer = HipTimer()
-    with torch.cuda.stream(ls):
-        timer.start()
-        for k in range(args.steps):
-            single.run()
-        kernel_ms = timer.stop_ms() / args.steps
-    torch.cuda.synchronize()
+    # the parts alone, outside the window: the launch over rotating HBM-sized buffers (the roofline),
+    # and the copy-out (back to back, one stream)
+    roof = rotating_roofline(plan, codes_ev, rows, want_map, err, args.steps)
+    kernel_ms = roof["kernel_ms"]
     t0 = time.perf_counter()
     with torch.cuda.stream(ls):
         for k in range(args.steps):
@@ -956,13 +1098,12 @@ def bench_c5_host(args, dist, rank, world):
         parity = ({"rows_checked": checked, "map_mismatches": wrong, "ok": wrong == 0} if want_map else
                   {"rows_checked": checked, "max_rel_err": worst, "ok": worst <= 1e-6, "checked_on": "host copy"})
     ms_per_step = elapsed * 1e3 / args.steps
-    bpr = plan.algorithmic_bytes_per_row(marginals=not want_map, map_=want_map)
-    achieved = bpr * rows / (kernel_ms * 1e-3) / 1e9
+    roof["step_bound"] = "host link (PCIe D2H of the block's results)"
     return {
         "metric": METRIC, "value": total * args.steps / elapsed, "unit": "queries/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))",
+        "data": inp["data"],
         "config": {"workload": ("C5 munin predict (MAP) template, 1M rows per step sharded over the ranks, "
                                 "int32 MAP indices delivered to pinned host memory per rank") if want_map else
                                ("C5 munin predict_probability template, 1M rows per step sharded over the ranks, "
@@ -975,46 +1116,26 @@ def bench_c5_host(args, dist, rank, world):
         "kernel_ms": kernel_ms, "copy_ms": copy_ms, "copy_bytes_per_rank": copy_bytes,
         "copy_GBps": copy_bytes / (copy_ms * 1e-3) / 1e9,
         "pipelined_step_over_copy": ms_per_step / copy_ms if copy_ms else None,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
-                     "grid": {"blocks": k_blocks, "workgroup": k_wg}, "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows,
-                     "step_bound": "host link (PCIe D2H of the block's results)"},
+        "roofline": roof,
         "parity": parity,
     }
 
 
-def bench_c5(args, dist, rank, world):
-    """C5 (BASELINE.json configs[4]): ROWS (1,000,000) munin template rows per step over all ranks,
-    contiguous blocks per rank (distributed.shard_bounds), strong scaling.  One step = every rank's
-    bound fused-plan launch over its block + the gather of the [17, rows] fp64 marginals to rank 0
-    (torch.distributed.gather: RCCL over xGMI with the nccl backend).  Rank 0 owns a [world, 17,
-    block] receive buffer allocated once; blocks are padded to the largest so one gather serves all."""
+def bench_c5(args, dist, rank, world, inp=None):
+    """C5 (BASELINE.json configs[4]) with the RCCL funnel (--c5-delivery rccl): ROWS (1,000,000) munin
+    template rows per step over all ranks, contiguous blocks per rank (distributed.shard_bounds),
+    strong scaling.  One step = every rank's bound fused-plan launch over its block + the gather of the
+    [17, rows] fp64 marginals to rank 0 (torch.distributed.gather: RCCL over xGMI with the nccl
+    backend).  Rank 0 owns a [world, 17, block] receive buffer allocated once; blocks are padded to the
+    largest so one gather serves all.  `inp`: see bench_c5_host."""
     import torch
 
     from pgmpy_amd.distributed import shard_bounds
-    from pgmpy_amd.inference.batch import upload_codes
-    from pgmpy_amd.inference.plan import PatternPlan
-    from pgmpy_amd.utils import get_example_model
-    from pgmpy_amd.utils.sampling import forward_sample_codes
 
-    model = get_example_model("munin")
-    missing_list = random.Random(0).sample(sorted(model.nodes()), 3)
-    variables = list(set(missing_list))
-    total = args.rows
-    lo, hi = shard_bounds(total, world, rank)
-    rows = hi - lo
+    inp = inp or c5_inputs(args, rank, world)
+    plan, variables, observed = inp["plan"], inp["variables"], inp["observed"]
+    d_codes, ld, rows, total, codes_ev = inp["d_codes"], inp["ld"], inp["rows"], inp["total"], inp["codes_host"]
     block = max(h - l for l, h in (shard_bounds(total, world, r) for r in range(world)))
-    t0 = time.perf_counter()
-    codes_all, nodes = forward_sample_codes(model, rows, seed=(42, lo))
-    observed = [v for v in nodes if v not in set(variables)]
-    pos = {v: i for i, v in enumerate(nodes)}
-    codes_ev = np.ascontiguousarray(codes_all[[pos[v] for v in observed]])
-    del codes_all
-    log(f"[rank {rank}] rows [{lo}, {hi}) sampled in {time.perf_counter() - t0:.1f}s")
-    plan = PatternPlan(model, variables, observed, {v: i for i, v in enumerate(observed)})
-    assert plan.kind == "fused", plan.describe()
-    d_codes = upload_codes(codes_ev)
     dev = d_codes.device
     want_map = getattr(args, "c5_output", "marginals") == "map"
     # three output buffers on three streams: step k's launch writes buffer k % 3 on stream k % 3
@@ -1034,8 +1155,7 @@ def bench_c5(args, dist, rank, world):
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     streams = [torch.cuda.Stream(device=dev) for _ in range(nbuf)]
     torch.cuda.synchronize()
-    bounds = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=streams[i]) for i in range(nbuf)]
-    kname, k_blocks, k_wg = bounds[0].kernel()
+    bounds = [plan.bind(d_codes, ld, 0, rows, outs[i], err=err, stream=streams[i]) for i in range(nbuf)]
     nccl = dist is not None and _BACKEND == "nccl"
     recvs = [None] * nbuf
     if dist is not None and rank == 0:
@@ -1085,7 +1205,7 @@ def bench_c5(args, dist, rank, world):
     torch.cuda.synchronize()
     launch_ms = max_over_ranks(dist, (time.perf_counter() - l0) * 1e3 / args.steps)
     # one launch's own duration: the same launches one after another on one stream (HIP events)
-    seq = [plan.bind(d_codes, rows, 0, rows, outs[i], err=err, stream=streams[0]) for i in range(nbuf)]
+    seq = [plan.bind(d_codes, ld, 0, rows, outs[i], err=err, stream=streams[0]) for i in range(nbuf)]
     with torch.cuda.stream(streams[0]):
         timer = HipTimer()
         timer.start()
@@ -1101,7 +1221,7 @@ def bench_c5(args, dist, rank, world):
     torch.cuda.synchronize()
     gather_ms = max_over_ranks(dist, (time.perf_counter() - g0) * 1e3 / args.steps)
     bpr = plan.algorithmic_bytes_per_row(marginals=not want_map, map_=want_map)
-    achieved = bpr * rows / (kernel_ms * 1e-3) / 1e9
+    roof = rotating_roofline(plan, codes_ev, rows, want_map, err, args.steps)
     parity = None
     if rank == 0:
         from oracle import ve as OVE  # checker only: first rows of rank 0's block
@@ -1148,7 +1268,7 @@ def bench_c5(args, dist, rank, world):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (forward-sampled munin evidence rows, seed (42, first row of the block))",
+        "data": inp["data"],
         "config": {"workload": ("C5 munin predict (MAP) template, 1M rows per step sharded over the ranks + gather "
                                 "of the int32 MAP indices to rank 0") if want_map else
                                ("C5 munin predict_probability template, 1M rows per step sharded over the ranks "
@@ -1162,15 +1282,8 @@ def bench_c5(args, dist, rank, world):
         "launch_ms": launch_ms,
         "gather_backend": _BACKEND if dist is not None else None,
         "gather_bytes_to_rank0": (8 if not want_map else 4) * (plan.n_acc if not want_map else 1) * block * (world - 1),
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "frac_wall": bpr * rows / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": None, "kernel": kname or plan.kernel_name(), "grid": {"blocks": k_blocks, "workgroup": k_wg},
-                     "kernel_ms": kernel_ms, "kernel_ms_note": "HIP-event span per launch of back-to-back "
-                     "launches on one stream rotating the output buffers, outside the window",
-                     "algorithmic_bytes_per_row": bpr, "bytes_per_launch": bpr * rows,
-                     "output_buffers": nbuf, "working_set_bytes": bpr * rows * nbuf,
-                     "working_set_exceeds_mall": bpr * rows * nbuf > MALL_BYTES},
+        "roofline": dict(roof, frac_wall=bpr * rows / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         three_buffer_kernel_ms=kernel_ms),
         "parity": parity,
     }
 
@@ -1283,21 +1396,13 @@ def bench_c4(args):
     from pgmpy_amd.inference.EliminationOrder import junction_tree_from_model
     from pgmpy_amd.inference.batch import upload_codes
     from pgmpy_amd.utils import get_example_model
-    from pgmpy_amd.utils.sampling import forward_sample_codes
+    from pgmpy_amd.utils.sampling import leaf_findings_codes
 
     m = get_example_model("pathfinder")
     jt = junction_tree_from_model(m)
     bjt = BatchedJunctionTree(jt)
-    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
     n = args.rows
-    codes, nodes = forward_sample_codes(m, n, seed=7)
-    rng = np.random.default_rng(7)
-    ev_vars = leaves
-    ev = np.full((len(ev_vars), n), 255, dtype=np.uint8)
-    for r in range(n):
-        pick = rng.choice(len(ev_vars), size=4, replace=False)
-        for j in pick:
-            ev[j, r] = codes[nodes.index(ev_vars[j]), r]
+    ev, ev_vars, _, _ = leaf_findings_codes(m, n, per_row=4, seed=7)
     d = upload_codes(ev)
     for _ in range(args.warmup):
         bjt.calibrate_codes(d, ev_vars, n)
@@ -1309,6 +1414,7 @@ def bench_c4(args):
     dt = (time.perf_counter() - t0) / args.steps
     bpc = bjt.bytes_per_calibration()
     sch = bjt.schedule(n, ev_vars, "marginalize", False)
+    parity = _c4_parity(m, cal, ev, ev_vars, n)
     step_bytes = sum(sch.prog.step_bytes) / n if sch.prog.step_bytes else None
     return {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
             "rows_per_step": n, "ms_per_step": dt * 1e3, "bytes_per_calibration": bpc,
@@ -1321,7 +1427,26 @@ def bench_c4(args):
                     "every tensor each reads or writes (operands re-read by the collect and distribute passes, "
                     "aggregates); the reference schedule's figure reads and writes every belief in both passes "
                     "(SURVEY §8(d) C4)",
-            "cliques": len(bjt.cliques)}
+            "cliques": len(bjt.cliques), "parity": parity}
+
+
+def _c4_parity(m, cal, ev, ev_vars, n):
+    """After the timed region: 16 rows of the last timed calibration (first, last, 14 seeded), every
+    entry of every clique belief against the oracle's calibration of the row's findings (the checker;
+    tests/test_inference_gpu.py::test_pathfinder_c4_bench_schedule runs 32 rows)."""
+    from oracle import bp as OBP
+    from oracle.network import load_network
+    from pgmpy_amd.inference.EliminationOrder import min_fill_decomposition
+
+    rows = sorted({0, n - 1} | set(int(x) for x in np.random.default_rng(11).choice(n, min(n, 14), replace=False)))
+    bags, edges = min_fill_decomposition(m)
+    try:
+        worst, entries = OBP.check_batched_rows(load_network("pathfinder"), bags, edges,
+                                                cal.clique_beliefs_rows(rows), ev, ev_vars, rows, rtol=1e-9)
+        return {"ok": True, "rows_checked": len(rows), "entries": entries, "max_rel_err": worst, "rtol": 1e-9,
+                "oracle": "oracle/bp.py (pinned to tests/golden/pathfinder_bp.*)"}
+    except AssertionError as e:
+        return {"ok": False, "rows_checked": len(rows), "error": str(e)[:400]}
 
 
 def main():
@@ -1340,6 +1465,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="c3: skip the C5 sub-object (1M rows split over the ranks: host delivery, MAP, RCCL gather)")
     ap.add_argument("--no-ring-roofline", action="store_true",
                     help="c3: skip the single-launch (resident ring) roofline after the timed region")
     ap.add_argument("--release-mode", default="barrier", choices=["launch", "barrier"],

@@ -89,3 +89,26 @@ def marginals(net, bags, beliefs):
                     out[var] = m / m.sum()
                 break
     return out
+
+
+def check_batched_rows(net, bags, edges, beliefs_rows, ev_codes, ev_vars, rows, op="sum", rtol=1e-9):
+    """Checker for a batched calibration: for each row r in `rows`, the row's findings (codes != 255 of
+    `ev_codes[:, r]`) through apply_evidence + calibrate, compared entry by entry with the device's
+    beliefs (`beliefs_rows[clique][i]` for rows[i], clique axes in the bag's order).  Returns
+    (max relative error over entries > 1e-300, number of entries compared); raises AssertionError at
+    the first clique outside `rtol`."""
+    pots = initial_potentials(net, bags)
+    worst, n = 0.0, 0
+    for i, r in enumerate(rows):
+        ev = {v: net.states[v][int(ev_codes[j, r])] for j, v in enumerate(ev_vars) if ev_codes[j, r] != 255}
+        want, _ = calibrate(bags, edges, apply_evidence(net, pots, bags, ev), op=op)
+        for b in bags:
+            w = want[b].aligned(list(b)).ravel()
+            g = beliefs_rows[tuple(b)][i]
+            np.testing.assert_allclose(g, w, rtol=rtol, atol=1e-300,
+                                       err_msg=f"row {r} clique {b[:4]}... evidence {ev}")
+            nz = np.abs(w) > 1e-300
+            if nz.any():
+                worst = max(worst, float(np.max(np.abs(g[nz] - w[nz]) / np.abs(w[nz]))))
+            n += w.size
+    return worst, n

@@ -313,19 +313,29 @@ def stream_handle(stream=None):
 
 
 class _HostBytes:
-    """The bytes of a HostBuffer as an __array_interface__ exporter that keeps the buffer alive: numpy
-    arrays made from it (and their views) hold the memory, so it is freed only when the HostBuffer and
-    every array on it are gone."""
+    """Owner of one pinned host allocation (pgm_host_alloc), exported through __array_interface__:
+    numpy arrays made from it (and their views) reference it, so the memory is freed by reference
+    counting as soon as the last of them is gone (no cycle back to the HostBuffer)."""
 
-    def __init__(self, owner, ptr, nbytes):
-        self._owner = owner
+    def __init__(self, ptr, nbytes):
+        self._p = ctypes.c_void_p(ptr)
         self.__array_interface__ = {"data": (ptr, False), "shape": (nbytes,), "typestr": "|u1", "version": 3}
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            try:
+                load_library().pgm_host_free(p)
+            except Exception:
+                pass
+            self._p = None
 
 
 class HostBuffer:
     """Pinned, mapped, coherent host memory that kernels read and write directly (pgm_host_alloc):
     `array` (numpy) and `tensor` (a CPU torch view of the same bytes, for descriptor building) share
-    it; freed once the object and every array / tensor viewing it are gone (the arrays reference it)."""
+    it; the memory belongs to the _HostBytes object the arrays are based on and is freed once the
+    HostBuffer and every array / tensor viewing it are gone."""
 
     def __init__(self, shape, dtype):
         import torch
@@ -336,19 +346,9 @@ class HostBuffer:
         p = ctypes.c_void_p()
         nbytes = max(1, n * dtype.itemsize)
         check(L.pgm_host_alloc(ctypes.byref(p), nbytes), "host_alloc")
-        self._p = p
-        raw = np.asarray(_HostBytes(self, p.value, nbytes))
+        raw = np.asarray(_HostBytes(p.value, nbytes))
         self.array = raw[:n * dtype.itemsize].view(dtype).reshape(shape)
         self.tensor = torch.from_numpy(self.array)
-
-    def __del__(self):
-        p = getattr(self, "_p", None)
-        if p is not None and p.value:
-            try:
-                load_library().pgm_host_free(p)
-            except Exception:
-                pass
-            self._p = None
 
 
 def ptr(t):

@@ -136,6 +136,26 @@ def serialized(fn):
     return wrapper
 
 
+def serialized_instance(fn):
+    """`serialized` plus the object's own re-entrant lock, for entry points that change the object's
+    state (BeliefPropagation.query swaps self.model for the pruned model and back, calibrate overwrites
+    the clique beliefs and replays one cached schedule's buffers): two threads on one such object run
+    one after the other, threads on different objects still overlap.  The object lock is taken BEFORE
+    the shared device hold, so a thread waiting for it holds no share of device_lock and cannot block
+    a capture's exclusive hold (DeviceLock's one rule)."""
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        lk = self.__dict__.get("_instance_lock")
+        if lk is None:
+            lk = self.__dict__.setdefault("_instance_lock", threading.RLock())
+        with lk:
+            with device_lock.shared():
+                return fn(self, *args, **kwargs)
+
+    return wrapper
+
+
 _tls_stream = threading.local()
 
 

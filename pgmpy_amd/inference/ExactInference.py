@@ -27,6 +27,7 @@ from operator import itemgetter
 import networkx as nx
 import numpy as np
 
+from .. import _native as N
 from .. import engine as E
 from ..factors import factor_product
 from ..factors.discrete import DiscreteFactor
@@ -170,7 +171,10 @@ class VariableElimination(Inference):
         node_map = getattr(self.model, "_node", None)  # networkx's node dict: a plain membership test
         if (isinstance(self.model, DiscreteBayesianNetwork) and elimination_order == "greedy"
                 and all(v in (node_map if node_map is not None else self.model)
-                        for v in itertools.chain(variables, evidence))):
+                        for v in itertools.chain(variables, evidence))
+                and all(self.model.get_cardinality(v) < N.PGM_EV_MISSING for v in evidence)):
+            # (a compiled plan reads uint8 evidence codes: a variable of 255+ states takes the strided
+            # view path below, which has no such limit)
             if virtual_evidence is None and type(evidence) is dict:
                 valid = self.__dict__.setdefault("_valid_keys", {})
                 if len(valid) >= 256:
@@ -486,11 +490,11 @@ class BeliefPropagation(Inference):
         for parent, child in order:  # distribute: root -> leaves
             self._update_beliefs(parent, child, operation)
 
-    @E.serialized
+    @E.serialized_instance
     def calibrate(self):
         self._calibrate_junction_tree(operation="marginalize")
 
-    @E.serialized
+    @E.serialized_instance
     def max_calibrate(self):
         self._calibrate_junction_tree(operation="maximize")
 
@@ -566,7 +570,7 @@ class BeliefPropagation(Inference):
         return {v: phi.marginalize([u for u in variables if u != v], inplace=False).normalize(inplace=False)
                 for v in variables}
 
-    @E.serialized
+    @E.serialized_instance
     def query(self, variables, evidence=None, virtual_evidence=None, joint=True, show_progress=True):
         """P(variables | evidence) via BP (ExactInference.py:1117-1220)."""
         evidence = evidence if evidence is not None else dict()
@@ -590,7 +594,7 @@ class BeliefPropagation(Inference):
             return result.normalize(inplace=False)
         return result
 
-    @E.serialized
+    @E.serialized_instance
     def map_query(self, variables=None, evidence=None, virtual_evidence=None, show_progress=True):
         # ExactInference.py:1222-1317
         variables = [] if variables is None else variables
@@ -615,7 +619,7 @@ class BeliefPropagation(Inference):
         self.model = orig_model
         return final
 
-    @E.serialized
+    @E.serialized_instance
     def calibrate_batch(self, evidence, operation="marginalize"):
         """Batched calibration: one calibration per evidence row.
 
@@ -730,7 +734,7 @@ class BeliefPropagationWithMessagePassing(Inference):
                     self.cache[self._key(src, dst)] = val
             raise AssertionError("message schedule did not reach the query variable")
 
-    @E.serialized
+    @E.serialized_instance
     def query(self, variables, evidence=None, virtual_evidence=None, get_messages=False, precomp_messages=None):
         # ExactInference.py:1509-1627
         common_vars = set(evidence if evidence is not None else []).intersection(set(variables))

@@ -517,14 +517,26 @@ def _single_fused_plan(model, data, columns, col_of, ev, variables):
     return plan
 
 
+# result blocks above this many bytes are pinned with pgm_host_alloc instead of torch's caching host
+# allocator: a result frame built on the block keeps it page-locked for as long as the
+# caller keeps the frame, and torch's allocator would keep it cached (locked) after that as well, so
+# repeated large predictions could exhaust the lockable memory; pgm_host_alloc memory is unlocked
+# and returned when the last array on it is freed (a hipHostMalloc per call: ~0.1 ms per 100 MB)
+PINNED_CACHE_MAX = int(os.environ.get("PGM_API_PINNED_CACHE_MAX", 64 << 20))
+
+
 def _pinned(shape, dtype):
-    """A page-locked host array from torch's caching host allocator: DMA reads / writes it directly,
-    and its memory returns to the allocator's cache when the last array viewing it is freed (a
-    result frame built on it owns it)."""
+    """A page-locked host array that DMA reads / writes directly.  Small blocks come from torch's
+    caching host allocator (their memory returns to its cache when the last array viewing it is
+    freed); blocks above PINNED_CACHE_MAX bytes from pgm_host_alloc, released to the system when
+    the last array viewing them (e.g. the result frame built on them) is freed."""
     import torch
 
-    t = torch.empty(shape, dtype=dtype, pin_memory=True)
-    return t.numpy()
+    t = torch.empty(0, dtype=dtype)
+    nbytes = int(np.prod(shape)) * t.element_size()
+    if nbytes > PINNED_CACHE_MAX:
+        return N.HostBuffer(tuple(shape), t.numpy().dtype).array
+    return torch.empty(shape, dtype=dtype, pin_memory=True).numpy()
 
 
 def _fused_to_host(plan, ev, columns, col_of, n, marginals):
@@ -587,6 +599,66 @@ def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars, ing
         yield plan, rows, host
 
 
+
+def wide_columns(model, columns):
+    """Evidence columns whose variable has more states than the uint8 codes of the batched plans hold
+    (state numbers 0..253; 254 marks a non-state, 255 = NaN).  The reference has no such limit
+    (utils/state_name.py:71-84): frames with one of these take _rowwise_frame."""
+    return [c for c in columns if int(model.get_cardinality(c)) >= MISSING]
+
+
+def _rowwise_frame(model, data, kind, seed=None):
+    """predict / predict_probability / query_batch for frames with a wide evidence column (see
+    wide_columns): the reference's own loop over distinct rows (DiscreteBayesianNetwork.py:866-910:
+    groupby over every column with dropna=False, one query per distinct row), each query a device
+    VariableElimination call (the strided-view contraction path, which takes any state count).  NaN
+    cells are unobserved, as in the batched path.  kind: "marg" (predict_probability), "map"
+    (predict), "sample" (predict(stochastic=True): DiscreteFactor.sample of the row's joint with a
+    fresh Generator(seed) per distinct row, L879-882)."""
+    import pandas as pd
+
+    from .ExactInference import VariableElimination
+
+    columns = list(data.columns)
+    order = list(set(model.nodes()) - set(columns))
+    n = len(data)
+    ve = VariableElimination(model)
+    groups = data.groupby(columns, dropna=False, sort=False).indices if n else {}
+    if kind == "marg":
+        cols = {var + "_" + str(s): np.empty(n) for var in order for s in model.get_cpds(var).state_names[var]}
+    else:
+        vals = {c: np.full(n, np.nan, dtype=object) for c in order}
+        filled = {}
+    for key, rows in groups.items():
+        key = key if isinstance(key, tuple) else (key,)
+        evidence = {c: v for c, v in zip(columns, key) if not pd.isna(v)}
+        if kind == "marg":
+            res = ve.query(order, evidence, joint=False, show_progress=False)
+            for var in order:
+                for k, st in enumerate(model.get_cpds(var).state_names[var]):
+                    cols[var + "_" + str(st)][rows] = float(np.asarray(res[var].values)[k])
+            continue
+        variables = order + [c for c in columns if c not in evidence]
+        if kind == "map":
+            assignment = ve.map_query(variables, evidence, show_progress=False)
+            draws = {v: np.full(len(rows), assignment[v], dtype=object) for v in variables}
+        else:
+            smp = ve.query(variables, evidence, joint=True, show_progress=False).sample(len(rows), seed=seed)
+            draws = {v: smp[v].to_numpy(object) for v in variables}
+        for v in variables:
+            if v in vals:
+                vals[v][rows] = draws[v]
+            else:
+                if v not in filled:
+                    filled[v] = data[v].to_numpy(object).copy()
+                filled[v][rows] = draws[v]
+    if kind == "marg":
+        return pd.DataFrame(cols, index=data.index)
+    base = data.assign(**filled) if filled else data
+    out = pd.concat([base, pd.DataFrame(vals, index=data.index, columns=order)], axis=1)
+    return out if out.index.is_monotonic_increasing else out.sort_index()
+
+
 def predict_probability_frame(model, data):
     """DiscreteBayesianNetwork.predict_probability (DiscreteBayesianNetwork.py:912-989)."""
     import pandas as pd
@@ -596,6 +668,8 @@ def predict_probability_frame(model, data):
     n = len(data)
     if n == 0:  # the reference builds its frame from empty per-column lists: no columns at all
         return pd.DataFrame({}, index=data.index)
+    if wide_columns(model, data.columns):
+        return _rowwise_frame(model, data, "marg")
     ingested = _ingest(model, data)
     plan = _single_fused_plan(model, data, *ingested, order)
     if plan is not None:
@@ -664,6 +738,8 @@ def predict_frame(model, data):
     order = list(missing_variables)
     if len(data) == 0:  # the reference indexes the first group of an empty groupby
         raise IndexError("list index out of range (predict on an empty DataFrame)")
+    if wide_columns(model, data.columns):
+        return _rowwise_frame(model, data, "map")
     ingested = _ingest(model, data)
     plan = _single_fused_plan(model, data, *ingested, order)
     if plan is not None:  # one pattern, no NaN cell: the MAP columns straight from the pinned index
@@ -758,6 +834,8 @@ def predict_stochastic_frame(model, data, seed=None):
     n = len(data)
     if n == 0:
         raise IndexError("list index out of range (predict on an empty DataFrame)")
+    if wide_columns(model, columns):
+        return _rowwise_frame(model, data, "sample", seed=seed)
     ev = ingest_frame(model, data, columns, row_hash=True)
     _, first, inv = np.unique(ev.row_hash, axis=0, return_index=True, return_inverse=True)
     inv = inv.reshape(-1)
@@ -830,6 +908,22 @@ def query_batch(model, variables, evidence, joint=False):
         res = {v: np.empty((n, c)) for v, c in zip(variables, cards)}
     columns = list(evidence.columns)
     col_of = {c: i for i, c in enumerate(columns)}
+    if wide_columns(model, columns):  # per row through device VariableElimination (see _rowwise_frame)
+        from .ExactInference import VariableElimination
+
+        import pandas as pd
+
+        ve = VariableElimination(model)
+        for r in range(n):
+            row = evidence.iloc[r]
+            ev_r = {c: row[c] for c in columns if not pd.isna(row[c])}
+            q = ve.query(list(variables), ev_r, joint=joint, show_progress=False)
+            if joint:
+                res[r] = np.asarray(q.values).transpose([q.variables.index(v) for v in variables])
+            else:
+                for v in variables:
+                    res[v][r] = np.asarray(q[v].values)
+        return res
     ev = ingest_frame(model, evidence, columns)
     import torch
 

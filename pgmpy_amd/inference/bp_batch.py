@@ -42,6 +42,18 @@ class BatchedCalibration:
         out = E.contract(t, ls + [E.ROW], None, None, [E.ROW] + list(clique), combine="copy")
         return E.to_host(out)[row].ravel()
 
+    def clique_beliefs_rows(self, rows):
+        """{clique: [len(rows), Π card]} host copies of the given rows' beliefs, axes in each clique
+        tuple's order (C-order flat) — one device pass and one download per clique."""
+        torch = E._torch()
+        idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=E.device())
+        out = {}
+        for c, (t, ls) in self.beliefs.items():
+            full = E.contract(t, ls + [E.ROW], None, None, list(c) + [E.ROW], combine="copy")
+            sel = full.reshape(-1, self.n_rows).index_select(1, idx)
+            out[c] = E.to_host(sel).T.copy()
+        return out
+
     def marginal(self, var):
         """[n_rows, card] normalized marginal of `var` per row."""
         if var in self._marg:

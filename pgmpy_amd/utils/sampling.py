@@ -43,3 +43,19 @@ def codes_to_frame(model, codes, nodes, columns=None):
     columns = nodes if columns is None else columns
     pos = {v: i for i, v in enumerate(nodes)}
     return pd.DataFrame({c: np.asarray(states[c], dtype=object)[codes[pos[c]]] for c in columns})
+
+
+def leaf_findings_codes(model, n, per_row=4, seed=7):
+    """The C4 evidence of SURVEY.md §8(d): every leaf of `model` is an evidence column, and each row
+    observes `per_row` of them (chosen per row by a seeded generator) at a forward-sampled state; the
+    others are 255 (unobserved).  Returns (codes [n_leaves, n] uint8, leaves, sampled codes, nodes).
+    bench.py's C4 line and its parity test build their batch through this one function."""
+    leaves = sorted(v for v in model.nodes() if model.out_degree(v) == 0)
+    codes, nodes = forward_sample_codes(model, n, seed=seed)
+    rng = np.random.default_rng(seed)
+    ev = np.full((len(leaves), n), 255, dtype=np.uint8)
+    rows = [nodes.index(v) for v in leaves]
+    for r in range(n):
+        for j in rng.choice(len(leaves), size=per_row, replace=False):
+            ev[j, r] = codes[rows[j], r]
+    return ev, leaves, codes, nodes

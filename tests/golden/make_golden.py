@@ -24,7 +24,8 @@ Fixture inventory (SURVEY.md §8(c) "Golden vectors"):
   alarm_predict_stochastic.json  predict(stochastic=True, seed=7) on duplicated alarm rows
   alarm_bp.npz / .json         BP calibration on a min-fill JT of alarm (full beliefs)
   munin_predict.npz            C3 template rows, MAP codes and marginals
-  munin_c2_query.json          C2: 100 leaf findings -> 1 root posterior
+  munin_c2_query.json          C2: 100 leaf findings -> 1 root posterior (row 0)
+  munin_c2_rows.json           C2 on all 20 sampled rows: root + two joint=False sets
   pathfinder_bp.npz / .json    C4: min-fill JT + beliefs (checksums) + marginals
 """
 import argparse
@@ -586,6 +587,54 @@ def gen_munin_c2():
     _dump("munin_c2_query.json", {"variables": q, "evidence": evidence, "result": _fac_json(r), "seconds": dt})
 
 
+def _c2_pattern():
+    """The C2 evidence pattern: the same 100 leaf findings E and root q as gen_munin_c2, plus two
+    joint=False query sets of non-root variables (a node with its parent / children in munin's nerve
+    chains). They were picked among 100 seeded local sets by the reference's own greedy path cost
+    (<= 1e10 multiply-adds, <= 3.6e7-entry intermediates, so each query takes ~1 min here); a random
+    4-variable set costs ~4e11 (~30 min per query)."""
+    m, samples = _munin_rows(20, seed=0)
+    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
+    roots = sorted(n for n in m.nodes() if m.in_degree(n) == 0)
+    rng = random.Random(100000)
+    E = rng.sample(leaves, 100)
+    q = [rng.choice(roots)]
+    qms = [["R_MEDD2_SALOSS", "R_DIFFN_LNLW_MEDD2_SALOSS", "R_MEDD2_DSLOW_EW", "R_MEDD2_EFFAXLOSS"],
+           ["L_MEDD2_DISP_EW", "L_DIFFN_MEDD2_DISP", "L_MEDD2_DISP_EWD"]]
+    return m, samples, E, q, qms
+
+
+def _c2_row_worker(i):
+    _setup()
+    from pgmpy.inference import VariableElimination
+
+    m, samples, E, q, qms = _c2_pattern()
+    evidence = {v: str(samples.iloc[i][v]) for v in E}
+    ve = VariableElimination(m)
+    out = {"row": i, "evidence": evidence, "separate": [], "seconds": []}
+    t0 = time.time()
+    out["root"] = _fac_json(ve.query(q, evidence, show_progress=False))
+    out["seconds"].append(time.time() - t0)
+    for qm in qms:
+        t0 = time.time()
+        sep = ve.query(qm, evidence, joint=False, show_progress=False)
+        out["seconds"].append(time.time() - t0)
+        out["separate"].append({k: _fac_json(v) for k, v in sep.items()})
+    return out
+
+
+def gen_munin_c2_rows(jobs=6, rows=20):
+    """C2 on every row of forward_sample(size=20, seed=0): the same 100 findings and root as
+    munin_c2_query.json (one evidence pattern, one compiled plan per query) -> the root posterior, and
+    two joint=False queries over 3-4 non-root variables (ExactInference.py:349-440, greedy path; the
+    per-variable results are marginalize + normalize of the joint, L423-432)."""
+    _, _, E, q, qms = _c2_pattern()
+    with Pool(jobs) as pool:
+        res = pool.map(_c2_row_worker, list(range(rows)), chunksize=1)
+    res.sort(key=lambda r: r["row"])
+    _dump("munin_c2_rows.json", {"variables": q, "separate_variables": qms, "evidence_variables": E, "rows": res})
+
+
 # ----------------------------------------------------------------------------- Markov networks
 def _sorted_fac(phi):
     """A factor as {variables sorted, values aligned to them} (hash-order independent)."""
@@ -764,6 +813,7 @@ GENS = {
     "alarm_predict_stochastic": gen_alarm_predict_stochastic,
     "munin_predict": gen_munin_predict,
     "munin_c2": gen_munin_c2,
+    "munin_c2_rows": gen_munin_c2_rows,
 }
 
 if __name__ == "__main__":
@@ -777,6 +827,8 @@ if __name__ == "__main__":
         t0 = time.time()
         if name == "munin_predict":
             gen_munin_predict(a.munin_rows, a.jobs)
+        elif name == "munin_c2_rows":
+            gen_munin_c2_rows(min(a.jobs, 6))
         else:
             GENS[name]()
         print(f"[{name}] {time.time() - t0:.1f}s")

@@ -648,3 +648,35 @@ def test_bench_cpu_baselines_run():
     one, allcore = bench.cpu_baselines_c3(argparse.Namespace(rows=300, cpu_seconds=0.5))
     assert one["value"] > 0 and one["cores"] == 1 and one["kind"] == "port"
     assert allcore["value"] > 0 and allcore["cores"] >= 1
+
+
+def test_c4_junction_tree_is_the_golden_tree():
+    """bench.py's C4 line builds its tree with junction_tree_from_model (min-fill decomposition); the
+    pathfinder BP fixture (tests/golden/pathfinder_bp.json) holds the reference's beliefs on a tree the
+    generator built the same way. They must be the same tree: bags in the same order (bags[0] is
+    the sweep's root) and the same edges."""
+    import json
+
+    from pgmpy_amd.inference.EliminationOrder import min_fill_decomposition
+    from pgmpy_amd.utils import get_example_model
+
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "pathfinder_bp.json")))
+    bags, edges = min_fill_decomposition(get_example_model("pathfinder"))
+    assert bags == [tuple(b) for b in meta["bags"]]
+    assert {frozenset(e) for e in edges} == {frozenset((tuple(a), tuple(b))) for a, b in meta["edges"]}
+
+
+def test_c4_leaf_findings_shape():
+    """The C4 evidence generator: every leaf a column, exactly 4 findings per row, the rest 255, each
+    finding the row's forward-sampled state."""
+    from pgmpy_amd.utils import get_example_model
+    from pgmpy_amd.utils.sampling import leaf_findings_codes
+
+    m = get_example_model("pathfinder")
+    ev, leaves, codes, nodes = leaf_findings_codes(m, 500, per_row=4, seed=7)
+    assert leaves == sorted(v for v in m.nodes() if m.out_degree(v) == 0)
+    assert ev.shape == (len(leaves), 500)
+    assert ((ev != 255).sum(axis=0) == 4).all()
+    rows = np.array([nodes.index(v) for v in leaves])
+    obs = ev != 255
+    assert (ev[obs] == codes[rows][obs]).all()
