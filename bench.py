@@ -1289,40 +1289,44 @@ def bench_c5(args, dist, rank, world, inp=None):
 
 
 def bench_c2(args):
-    """C2: one munin query, 100 leaf findings -> 1 root, greedy device contraction."""
+    """C2: one munin query, 100 leaf findings -> 1 root, greedy device contraction.  The evidence rows
+    are the reference's own (tests/golden/munin_c2_rows.json: forward_sample(size=20, seed=0) of
+    pgmpy, the same 100 findings per row, so one compiled plan): step k queries row k % 20, and
+    after the timed region every row's root posterior is checked against the reference's value."""
     import torch
 
     from pgmpy_amd.inference import VariableElimination
-    from pgmpy_amd.inference.contraction import plan_stats
     from pgmpy_amd.utils import get_example_model
-    from pgmpy_amd.utils.sampling import forward_sample_codes
 
+    with open(os.path.join(ROOT, "tests", "golden", "munin_c2_rows.json")) as f:
+        g = json.load(f)
     m = get_example_model("munin")
-    leaves = sorted(n for n in m.nodes() if m.out_degree(n) == 0)
-    roots = sorted(n for n in m.nodes() if m.in_degree(n) == 0)
-    rng = random.Random(100000)
-    E = rng.sample(leaves, 100)
-    q = [rng.choice(roots)]
-    codes, nodes = forward_sample_codes(m, 1, seed=0)
-    st = m.states
-    evidence = {v: st[v][codes[nodes.index(v), 0]] for v in E}
+    q = g["variables"]
+    rows = [r["evidence"] for r in g["rows"]]
     ve = VariableElimination(m)
     torch.cuda.synchronize()
     t_cold = time.perf_counter()
-    ve.query(q, evidence, show_progress=False)  # first query of the pattern: prune, plan, compile, capture
+    ve.query(q, rows[0], show_progress=False)  # first query of the pattern: prune, plan, compile, capture
     torch.cuda.synchronize()
     t_cold = time.perf_counter() - t_cold
-    for _ in range(args.warmup):
-        ve.query(q, evidence, show_progress=False)
+    for k in range(args.warmup):
+        ve.query(q, rows[k % len(rows)], show_progress=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r = ve.query(q, evidence, show_progress=False)
+    for k in range(args.steps):
+        r = ve.query(q, rows[k % len(rows)], show_progress=False)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     runner, = ve._compiled.values()
     plan = runner.plan
     ps = plan.path_stats(1)
+    worst, ok = 0.0, True
+    for row, ev in zip(g["rows"], rows):
+        got = ve.query(q, ev, show_progress=False)
+        want = np.asarray(row["root"]["values"], dtype=np.float64)
+        x = np.asarray(got.values).ravel()
+        ok &= bool(np.allclose(x, want, rtol=1e-6, atol=1e-12))
+        worst = max(worst, float(np.max(np.abs(x - want))))
     return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
             "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
             "plan": {"kind": plan.kind, **ps},
@@ -1331,6 +1335,9 @@ def bench_c2(args):
             "reference": {"value": 52.7, "unit": "s/query", "note": "pgmpy numpy path, survey container (not this host)"},
             "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
                     "same query/evidence variables); first_query_s includes pruning, planning and graph capture",
+            "data": "the reference's 20 forward-sampled munin rows (tests/golden/munin_c2_rows.json), step k = row k % 20",
+            "parity": {"ok": ok, "rows_checked": len(rows), "max_abs_err": worst, "rtol": 1e-6, "atol": 1e-12,
+                       "against": "reference root posteriors (tests/golden/munin_c2_rows.json)"},
             "result": list(np.asarray(r.values))}
 
 
