@@ -313,30 +313,25 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
 /* a findings-indicator job (pgm_indicator's arguments): all of a BP sweep's findings in one launch */
 int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
                             int64_t s_state, int64_t s_row, int32_t *err_flag);
-/* Levelled batch (several dependency levels of a compiled contraction path in ONE launch): jobs added
- * after pgm_batch_add_level belong to the next level and may read earlier levels' outputs.  run then
- * launches one persistent kernel whose workgroups (all resident: the grid is capped by the occupancy)
- * stride over each level's blocks and meet at a grid barrier (agent-scope release/acquire) between
- * levels — the levels of ExactInference.py:404-406's contraction without one launch each.  A barrier
- * that waits > 2 s (residency violated by another persistent kernel) gives up; pgm_batch_info then
- * reports timed_out = 1 (and resets the barrier).  One handle must not run on two streams at once. */
+/* Single-workgroup levelled batch (mode PGM_BATCH_ONE_WORKGROUP, set before the first job): jobs added
+ * after pgm_batch_add_level belong to the next level and may read earlier levels' outputs.  run
+ * launches ONE 1,024-thread workgroup that stages every job descriptor, the block map and the level
+ * table in LDS and executes each level's blocks (four 256-thread virtual blocks at a time) with a
+ * workgroup barrier between levels (no grid barrier, no cache maintenance: producer and consumer are
+ * the same workgroup) — for chains of tiny dependent levels (the last levels of a contraction path
+ * down to the query marginal and its normalisation, ExactInference.py:404-421), whose
+ * one-launch-per-level cost is all launch latency.  Contraction jobs only, tables <= 48 KB
+ * (finalize: PGM_EINVAL otherwise).  pgm_batch_add_level needs this mode (PGM_EINVAL in the default
+ * PGM_BATCH_GRID mode: one level, one launch).  ABI 20 removed the persistent grid-barrier form
+ * (measured slower than one launch per level, r03) and pgm_batch_info. */
 int pgm_batch_add_level(void *handle);
-/* Single-workgroup levelled batch (set before finalize): run launches ONE workgroup that executes every
- * level's blocks in order, one block after another, with a workgroup barrier between them (no grid
- * barrier, no cache maintenance: producer and consumer are the same workgroup) — for chains of tiny
- * dependent levels (the last levels of a contraction path down to the query marginal and its
- * normalisation, ExactInference.py:404-421), whose one-launch-per-level cost is all launch latency.
- * mode: PGM_BATCH_GRID (default: the persistent grid above) or PGM_BATCH_ONE_WORKGROUP, set before the
- * first job (its contraction jobs are then planned to occupy as few blocks as their outputs allow). */
 enum { PGM_BATCH_GRID = 0, PGM_BATCH_ONE_WORKGROUP = 1 };
 int pgm_batch_set_mode(void *handle, int32_t mode);
 /* blocks (256-thread workgroups) the jobs added so far occupy; the levelled single-workgroup kernel
- * runs them one after another, so callers keep it to levels of a few blocks */
+ * runs them four at a time, so callers keep it to levels of a few blocks */
 int pgm_batch_blocks(void *handle, int64_t *blocks);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
-/* levels, persistent grid (0: one launch per level), and (synchronising) whether a barrier timed out */
-int pgm_batch_info(void *handle, int32_t *n_levels, int32_t *grid, int32_t *timed_out);
 int pgm_batch_destroy(void *handle);
 
 

@@ -185,8 +185,6 @@ _SIGS = {
     "pgm_batch_add_level": ([_P], ctypes.c_int),
     "pgm_batch_finalize": ([_P], ctypes.c_int),
     "pgm_batch_run": ([_P, _P], ctypes.c_int),
-    "pgm_batch_info": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
-                        ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "pgm_batch_destroy": ([_P], ctypes.c_int),
     "pgm_codes_select": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, ctypes.c_int64, _P, _P],
                          ctypes.c_int),

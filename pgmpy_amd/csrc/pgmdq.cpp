@@ -58,7 +58,6 @@ struct DirectQueue {
   // system-scope release barrier packet.  PGM_DQ_ACQ / PGM_DQ_REL override (A/B knobs).
   uint16_t acq_scope = HSA_FENCE_SCOPE_NONE;
   uint16_t fresh_acq_scope = HSA_FENCE_SCOPE_SYSTEM;
-  int rel_override = -1;
   bool fresh = true;          // next dispatch is the first since bind/sync
   bool need_release = false;  // dispatches since the last system-scope release
   uint64_t last_kernel = 0;   // index of the last kernel dispatch (timer end)
@@ -236,26 +235,14 @@ int pgm_dq_create(int hip_device, void **out) {
   if (!dq->freq) dq->freq = 1;
   dq->ring.reserve(kRing);
   // completion signals without an interrupt event (HSA_AMD_SIGNAL_AMD_GPU_ONLY): the CP only writes
-  // the value (and the profiling timestamps); the host polls it.  A/B knob PGM_DQ_SIGNAL=event.
-  const bool event_sig = getenv("PGM_DQ_SIGNAL") && strcmp(getenv("PGM_DQ_SIGNAL"), "event") == 0;
+  // the value (and the profiling timestamps); the host polls it (an interrupt signal: +0.5 us per
+  // dispatch, profiles/r02e_store_release_ab.json)
   for (uint64_t i = 0; i < kRing; ++i) {
     hsa_signal_t s;
-    st = event_sig ? hsa_signal_create(0, 0, nullptr, &s)
-                   : hsa_amd_signal_create(0, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s);
+    st = hsa_amd_signal_create(0, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s);
     if (st != HSA_STATUS_SUCCESS) return bail(fail(PGM_EDEVICE, "dq_create: hsa_signal_create: %s", hsa_msg(st)));
     dq->ring.push_back(s);
   }
-  auto scope_env = [](const char *name, uint16_t dflt) -> uint16_t {  // A/B knobs
-    const char *e = getenv(name);
-    if (!e) return dflt;
-    if (strcmp(e, "none") == 0) return HSA_FENCE_SCOPE_NONE;
-    if (strcmp(e, "agent") == 0) return HSA_FENCE_SCOPE_AGENT;
-    if (strcmp(e, "system") == 0) return HSA_FENCE_SCOPE_SYSTEM;
-    return dflt;
-  };
-  dq->acq_scope = scope_env("PGM_DQ_ACQ", dq->acq_scope);
-  dq->fresh_acq_scope = scope_env("PGM_DQ_FRESH_ACQ", dq->fresh_acq_scope);
-  if (getenv("PGM_DQ_REL")) dq->rel_override = scope_env("PGM_DQ_REL", HSA_FENCE_SCOPE_AGENT);
   *out = dq;
   return PGM_OK;
 }
@@ -387,8 +374,7 @@ int pgm_dq_bind_rows(void *handle, void *bound, void **out) {
   db->dq = dq;
   db->blocks = L.blocks;
   db->wg = L.wg;
-  db->rel_scope = dq->rel_override >= 0 ? (uint16_t)dq->rel_override
-                                        : (uint16_t)(L.write_through ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT);
+  db->rel_scope = (uint16_t)(L.write_through ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT);
   bool reader = false, exec = false;
   auto bail = [&](int rc2) {
     if (exec) (void)hsa_executable_destroy(db->exec);

@@ -35,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 19  // 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 20  // 20: pgm_batch_info and the grid-barrier levelled batch removed (levels: single-workgroup mode only); 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -591,96 +591,7 @@ static void coalesce(Dims &d, int nops) {
   d = o;
 }
 
-static const bool g_no_rows2 = getenv("PGM_NO_ROWS2") != nullptr;  // tuning/testing: 8-B row paths only
-
-// Flat mode walks the outputs in the order of the kept dims (the last one fastest across lanes).  The
-// outputs, and each output's own reduction walk, are the same in any order, so the host may pick the
-// order whose wave-wide accesses touch the fewest cache lines: the given one (C's layout) or the kept
-// dims sorted by one operand's strides (that operand read in address order).  Cost of an order: the
-// 128-B lines one wave's 64 consecutive outputs touch, per operand, weighted by that operand's accesses
-// per output (A and B: one per reduction entry; C: one store, counted twice).  Bit-identical results.
-// Measured no faster on C1 / C2 / C4 (profiles/r04j/: the widest C2 level stays at 12 us), so off; A/B
-// knob PGM_CONTRACT_ORDER=1.
-static const bool g_keep_order = [] {
-  const char *e = getenv("PGM_CONTRACT_ORDER");
-  return e && e[0] == '1';
-}();
-
-// 128-B lines touched by each operand's accesses of the 64 consecutive outputs from out0 (digits walked
-// incrementally, all three operands at once)
-static void wave_lines(const Dims &kd, uint64_t out0, uint64_t n_out, uint64_t lines_out[3]) {
-  int64_t dig[PGM_MAX_DIMS], off[3] = {0, 0, 0};
-  uint64_t idx = out0;
-  for (int k = kd.n - 1; k >= 0; --k) {
-    dig[k] = (int64_t)(idx % (uint64_t)kd.card[k]);
-    idx /= (uint64_t)kd.card[k];
-    for (int t = 0; t < 3; ++t) off[t] += dig[k] * kd.s[t][k];
-  }
-  int64_t ln[3][64];
-  int n = 0;
-  for (uint64_t l = 0; l < 64 && out0 + l < n_out; ++l, ++n) {
-    for (int t = 0; t < 3; ++t) ln[t][n] = (off[t] * 8) >> 7;
-    for (int k = kd.n - 1; k >= 0; --k) {  // next output: innermost digit + 1 with carry
-      for (int t = 0; t < 3; ++t) off[t] += kd.s[t][k];
-      if (++dig[k] < kd.card[k]) break;
-      for (int t = 0; t < 3; ++t) off[t] -= kd.card[k] * kd.s[t][k];
-      dig[k] = 0;
-    }
-  }
-  for (int t = 0; t < 3; ++t) {
-    std::sort(ln[t], ln[t] + n);
-    lines_out[t] = (uint64_t)(std::unique(ln[t], ln[t] + n) - ln[t]);
-  }
-}
-
-static uint64_t order_cost(const Dims &kd, bool use_b, uint64_t n_red, uint64_t n_out) {
-  // two sample waves: the first, and one in the middle of the index space
-  const uint64_t w[2] = {0, (n_out / 2) & ~63ull};
-  uint64_t c = 0;
-  for (uint64_t o : w) {
-    uint64_t l[3];
-    wave_lines(kd, o, n_out, l);
-    c += n_red * (l[0] + (use_b ? l[1] : 0)) + 2 * l[2];
-  }
-  return c;
-}
-
-static void choose_keep_order(Dims &kd, bool use_b, uint64_t n_red, uint64_t n_out) {
-  if (!g_keep_order || kd.n < 2 || n_out < 4096 || kd.card[kd.n - 1] >= 64) return;
-  {  // the innermost dim already unit-stride or broadcast for every operand: nothing to gain
-    const int x = kd.n - 1;
-    const auto unit = [](int64_t v) { return v == 0 || v == 1 || v == -1; };
-    if (kd.s[2][x] == 1 && unit(kd.s[0][x]) && (!use_b || unit(kd.s[1][x]))) return;
-  }
-  Dims best = kd;
-  uint64_t best_cost = order_cost(kd, use_b, n_red, n_out);
-  for (int t = 0; t < 3; ++t) {
-    if (t == 1 && !use_b) continue;
-    // kept dims by descending |stride| of operand t (dims it broadcasts over first), stable
-    int perm[PGM_MAX_DIMS];
-    for (int i = 0; i < kd.n; ++i) perm[i] = i;
-    std::stable_sort(perm, perm + kd.n, [&](int a, int b) {
-      const int64_t sa = kd.s[t][a] < 0 ? -kd.s[t][a] : kd.s[t][a];
-      const int64_t sb = kd.s[t][b] < 0 ? -kd.s[t][b] : kd.s[t][b];
-      if ((sa == 0) != (sb == 0)) return sa == 0;
-      return sa > sb;
-    });
-    Dims cand;
-    cand.n = kd.n;
-    for (int i = 0; i < kd.n; ++i) {
-      cand.card[i] = kd.card[perm[i]];
-      for (int u = 0; u < 3; ++u) cand.s[u][i] = kd.s[u][perm[i]];
-    }
-    coalesce(cand, 3);
-    if (cand.n == 0 || cand.card[cand.n - 1] >= 64) continue;  // would change the kernel family
-    const uint64_t c = order_cost(cand, use_b, n_red, n_out);
-    if (c < best_cost) {
-      best_cost = c;
-      best = cand;
-    }
-  }
-  kd = best;
-}
+static constexpr bool g_no_rows2 = false;  // (r01's 8-B-only row paths: 0.54-0.70x the 16-B rate)
 
 static const uint64_t kTargetThreads = 256ull * 2048;  // 256 CUs x 32 waves x 64 lanes
 
@@ -723,7 +634,6 @@ static int plan_contract(const pgm_contract_desc *d, ContractLaunch &L) {
                 (unsigned long long)n_out, (unsigned long long)n_red);
   coalesce(kd, 3);
   coalesce(rd, 2);
-  choose_keep_order(kd, d->combine != PGM_COMBINE_COPY, n_red, n_out);
   // few outputs (flat mode) and one long reduction run: cut the run into (outer x chunk) so the
   // split-K below has reduction-outer indices to distribute (a batched dot product over a packed
   // operand pair would otherwise leave 64 lanes per output walking the whole run)
@@ -1106,80 +1016,6 @@ __device__ __forceinline__ double prodm_combine(const ProdMK &p, const double (&
   return prod;
 }
 
-template <int NOPS, int RED>
-__global__ __launch_bounds__(256) void k_productn_marg2(const ProdMK p, double *C, double *__restrict__ M) {
-  __shared__ int64_t tc[RMAX_MARG];
-  __shared__ int64_t to[NOPS][RMAX_MARG];
-  const uint32_t NR = p.n_red;
-  for (uint32_t j = threadIdx.x; j < NR; j += blockDim.x) {
-    uint32_t idx = j;
-    int64_t oc = 0, oo[NOPS];
-#pragma unroll
-    for (int i = 0; i < NOPS; ++i) oo[i] = 0;
-    for (int k = p.nr - 1; k >= 0; --k) {
-      const uint32_t q = fdiv(idx, p.rdiv[k]);
-      const uint32_t dg = idx - q * p.rdiv[k].d;
-      oc += (int64_t)dg * p.rsc[k];
-#pragma unroll
-      for (int i = 0; i < NOPS; ++i) oo[i] += (int64_t)dg * p.rs[i][k];
-      idx = q;
-    }
-    tc[j] = oc;
-#pragma unroll
-    for (int i = 0; i < NOPS; ++i) to[i][j] = oo[i];
-  }
-  __syncthreads();
-  const int kx = p.nk - 1;
-  const uint32_t xstep = gridDim.x * blockDim.x;
-  for (uint32_t o = blockIdx.y; o < p.n_outer; o += gridDim.y) {
-    int64_t oc = 0, om = 0, off[NOPS];
-#pragma unroll
-    for (int i = 0; i < NOPS; ++i) off[i] = 0;
-    uint32_t idx = o;
-    for (int k = kx - 1; k >= 0; --k) {
-      const uint32_t q = fdiv(idx, p.kdiv[k]);
-      const uint32_t dg = idx - q * p.kdiv[k].d;
-      oc += (int64_t)dg * p.ksc[k];
-      om += (int64_t)dg * p.ksm[k];
-#pragma unroll
-      for (int i = 0; i < NOPS; ++i) off[i] += (int64_t)dg * p.ks[i][k];
-      idx = q;
-    }
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < p.NP; x += xstep) {
-      auto load = [&](uint32_t j, double2 (&v)[NOPS]) {
-#pragma unroll
-        for (int i = 0; i < NOPS; ++i) {
-          const double *b = p.ops[i] + off[i] + to[i][j];
-          if (p.vec[i]) {
-            v[i] = ((const double2 *)b)[x];
-          } else {
-            const double s = b[0];
-            v[i] = make_double2(s, s);
-          }
-        }
-      };
-      double2 acc = make_double2(red_init<RED>(), red_init<RED>());
-      double2 cur[NOPS], nxt[NOPS];
-      load(0, cur);
-      for (uint32_t j = 0; j < NR; ++j) {
-        if (j + 1 < NR) load(j + 1, nxt);  // next entry's operands in flight during this one's store
-        double lo[NOPS], hi[NOPS];
-#pragma unroll
-        for (int i = 0; i < NOPS; ++i) {
-          lo[i] = cur[i].x;
-          hi[i] = cur[i].y;
-        }
-        const double2 pr = make_double2(prodm_combine<NOPS>(p, lo), prodm_combine<NOPS>(p, hi));
-        if (C) ((double2 *)(C + oc + tc[j]))[x] = pr;  // C == nullptr: the marginal only
-        acc.x = red_op<RED>(acc.x, pr.x);
-        acc.y = red_op<RED>(acc.y, pr.y);
-#pragma unroll
-        for (int i = 0; i < NOPS; ++i) cur[i] = nxt[i];
-      }
-      ((double2 *)(M + om))[x] = acc;
-    }
-  }
-}
 
 // j-outer form: for each reduced entry j the block sweeps its x range (XI row pairs per lane,
 // x = x0 + i*256), so every store instruction of the block lands in one contiguous run of the
@@ -1341,9 +1177,8 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   // row-dim operand that lacks a kept dim is read again by every block along that dim, so the dims
   // lacked by the largest such operands go innermost: the blocks sharing an operand slice then run
   // back to back and find it in L2 (pathfinder's root: 129-258 MB separator aggregates broadcast over
-  // its other variables).  Knob PGM_MARG_KORDER=0 keeps the clique's label order.
-  static const bool korder = !(getenv("PGM_MARG_KORDER") && atoi(getenv("PGM_MARG_KORDER")) == 0);
-  if (korder && k.nk > 1) {
+  // its other variables).
+  if (k.nk > 1) {
     double score[KMAX];
     for (int i = 0; i < k.nk; ++i) {
       score[i] = 0.0;
@@ -1381,19 +1216,17 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   k.NP = (uint32_t)(NX / 2);
   const uint64_t xb = (k.NP + 255) / 256;
   const uint64_t gy = std::min<uint64_t>(n_outer, 65535);
-  // target block count (tuning knob PGM_MARG_BLOCKS)
-  static const uint64_t target = getenv("PGM_MARG_BLOCKS") ? strtoull(getenv("PGM_MARG_BLOCKS"), nullptr, 10) : 2048;
+  // target block count
+  static constexpr uint64_t target = 2048;
   const uint64_t gx = std::min<uint64_t>(xb, std::max<uint64_t>(1, target / gy));
   // too few blocks to fill the chip: the two-kernel path (product_n + contract) was faster for a lone
   // launch below 512 blocks, but inside a levelled schedule it costs a second dependency level.  C4
   // (r03ae, two runs each): floor 512 / 256 / 128 / 64 -> 0.87-0.88 / 0.92 / 0.95 / 0.85 M
-  // calibrations/s at 1,000 rows, 1.20-1.21 / 1.25 / 1.24-1.25 / 1.24-1.25 M at 4,000.  Knob
-  // PGM_MARG_MIN_BLOCKS.  Once small steps are specialised and merged into their level's launch
+  // calibrations/s at 1,000 rows, 1.20-1.21 / 1.25 / 1.24-1.25 / 1.24-1.25 M at 4,000.  Once small steps are specialised and merged into their level's launch
   // (PGM_PM_JIT_MIN 2^14, r03ag) a small fused pass costs no launch of its own: floor 128 -> 32 gives
   // 1.03 -> 1.09 M at 1,000 rows, 4,000 rows unchanged at 1.29-1.30 M (r03ah); 32 / 8 / 2 -> 1.08 / 1.08
   // / 1.09-1.10 M (r03ai): no floor by default.
-  static const uint64_t min_blocks = getenv("PGM_MARG_MIN_BLOCKS") ? strtoull(getenv("PGM_MARG_MIN_BLOCKS"), nullptr, 10)
-                                                                   : 1;
+  static constexpr uint64_t min_blocks = 1;
   // (also accepting short reductions on 16+ blocks was slower at 1,000 rows, 0.95 -> 0.87 M: each such
   // pass is a launch of its own, where the two-kernel path's jobs join the level's batch launch; r03af)
   if (gx * gy < min_blocks) return 0;
@@ -1506,58 +1339,11 @@ __global__ __launch_bounds__(256) void k_batch(const BatchJob *__restrict__ jobs
   batch_block(jobs, block_job, blockIdx.x);
 }
 
-// Grid-wide barrier of a persistent launch whose G workgroups are all resident (the host sizes the grid
-// from the occupancy).  bar[0] counts arrivals, bar[1] is the generation (monotonic over launches, so
-// nothing is reset between runs), bar[2] the timeout status.  Workgroup stores are made visible at
-// agent scope before arriving (release) and other workgroups' stores after leaving (acquire).
-__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned G, unsigned long long deadline) {
-  __shared__ int ok_s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned a = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    if (a == G - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(bar + 1, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        if (wall_clock64() > deadline) {
-          ok = 0;
-          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    ok_s = ok;
-  }
-  __syncthreads();
-  return ok_s != 0;
-}
-
-// Several dependency levels of batch jobs in ONE launch: G resident workgroups stride over each level's
-// blocks (level_off[l] .. level_off[l+1] of the block map), then meet at a grid barrier before the next
-// level.  Replaces one launch per level (C2's 29-level plan) with one launch + 28 barriers.
-__global__ __launch_bounds__(256) void k_batch_levels(const BatchJob *__restrict__ jobs,
-                                                      const uint32_t *__restrict__ block_job,
-                                                      const uint32_t *__restrict__ level_off, uint32_t n_levels,
-                                                      unsigned *bar, unsigned long long timeout) {
-  const unsigned G = gridDim.x;
-  const unsigned long long deadline = wall_clock64() + timeout;
-  for (uint32_t l = 0; l < n_levels; ++l) {
-    const uint32_t e = level_off[l + 1];
-    for (uint32_t b = level_off[l] + blockIdx.x; b < e; b += G) batch_block(jobs, block_job, b);
-    if (l + 1 < n_levels && !grid_barrier(bar, G, deadline)) return;
-  }
-}
-
 // A single-workgroup levelled batch of contractions only (the tail of a contraction path, C1 / C2): the
 // job descriptors (contraction part only), the block map and the level table are copied into LDS once at
 // the start — every load of them independent, issued together — so each level's blocks read their
 // descriptor from LDS instead of a block-map load followed by a dependent descriptor load from memory
-// (two round trips per level).  Same per-job code as k_batch_wg, so the same results bit for bit.
+// (two round trips per level).  Same per-job code as k_batch_c, so the same results bit for bit.
 struct alignas(16) ChainJob {
   int32_t cmb, red;
   uint32_t block0, nblocks;
@@ -1620,26 +1406,10 @@ __global__ __launch_bounds__(256 * kChainVB) void k_batch_wg_c(const ChainJob *_
   }
 }
 
-// Several tiny dependent levels in ONE workgroup: each level's blocks run one after another on the same
-// 256 threads, a workgroup barrier after each (the block bodies may use LDS; the next level reads what
-// this workgroup wrote, which a workgroup-scope release/acquire makes visible).  Replaces one launch per
-// level for the last levels of a contraction path (C1 / C2), where every launch is latency only.
-__global__ __launch_bounds__(256) void k_batch_wg(const BatchJob *__restrict__ jobs,
-                                                  const uint32_t *__restrict__ block_job,
-                                                  const uint32_t *__restrict__ level_off, uint32_t n_levels) {
-  for (uint32_t l = 0; l < n_levels; ++l) {
-    const uint32_t e = level_off[l + 1];
-    for (uint32_t b = level_off[l]; b < e; ++b) {
-      batch_block(jobs, block_job, b);
-      __syncthreads();
-    }
-  }
-}
-
 // A batch whose jobs are all contractions with one (combine, reduce) pair — every C2 / C1 path level —
 // runs this instead of k_batch: k_batch carries every job kind's code (167 KB of instructions, 123
-// VGPRs), this one only the two contraction bodies.  Same per-job code, so bit-identical results.  A/B
-// knob PGM_BATCH_SPECIALISE=0.
+// VGPRs), this one only the two contraction bodies.  Same per-job code, so bit-identical results
+// (r04: C2 0.175 / 0.178 against 0.179 / 0.180 ms with k_batch, profiles/r04k/).
 template <int CMB, int RED>
 __global__ __launch_bounds__(256) void k_batch_c(const BatchJob *__restrict__ jobs,
                                                  const uint32_t *__restrict__ block_job) {
@@ -2744,56 +2514,26 @@ void pgmi_appendf(std::string &o, const char *fmt, ...) {
 // 100 k-row launch keep more CUs streaming than 98 x 1,024 once the outputs go to HBM instead of the
 // Infinity Cache; three interleaved repeats, 20 steps: 26.6 / 26.7 / 27.9 G rows/s against 27.3 / 25.1 /
 // 25.3 G at 512 (192: 27.0 / 26.7 / 26.0; 128: 25.7 / 25.6 / 26.6; 1,024: 25.5 / 24.7 / 25.5)
-static int jit_wg() {
-  static const int wg = [] {
-    const char *e = getenv("PGM_ROWS_JIT_WG");
-    const int v = e ? atoi(e) : 320;
-    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 320;
-  }();
-  return wg;
-}
+static constexpr int jit_wg() { return 320; }
 
-// output store form of the specialised kernels (knob PGM_ROWS_JIT_STORE): 0 "plain" (write-back L2),
-// 1 "nt" (nontemporal, one-row kernel), 2 "wt" = default: write-through — 8-B relaxed agent-scope
-// atomic stores / 16-B buffer stores with the sc1 bit — so every output line goes past the XCD's L2
-// in the dispatch that writes it (no dirty output left for an end-of-dispatch release to write
-// back; measured MI355X, 100k rows: HIP launch 4.7 -> 3.8 us, direct queue 6.2 -> 4.0 us with the
-// per-dispatch release dropped, WRITE_SIZE 13.28 MB per launch either way)
-static int jit_store() {
-  static const int m = [] {
-    const char *e = getenv("PGM_ROWS_JIT_STORE");
-    if (!e) return 2;
-    if (strcmp(e, "nt") == 0) return 1;
-    if (strcmp(e, "plain") == 0) return 0;
-    return 2;
-  }();
-  return m;
-}
+// output store form of the specialised kernels: write-through — 8-B relaxed agent-scope atomic stores /
+// 16-B buffer stores with the sc1 bit — so every output line goes past the XCD's L2 in the dispatch that
+// writes it (no dirty output left for an end-of-dispatch release to write back; measured MI355X, 100k
+// rows: HIP launch 4.7 -> 3.8 us, direct queue 6.2 -> 4.0 us with the per-dispatch release dropped,
+// WRITE_SIZE 13.28 MB per launch either way; r02 also measured plain (write-back) and nontemporal forms)
+static constexpr int jit_store() { return 2; }
 
-// workgroup size of the ring kernel (knob PGM_RING_WG, a multiple of 64 <= 1024): 256 = one wave per
+// workgroup size of the ring kernel: 256 = one wave per
 // SIMD per workgroup; the loop around the two-row body takes ~147 VGPRs (3 waves per SIMD), so three
 // workgroups are resident per CU (a 1,024-thread bound caps it at 128 VGPRs and spills to scratch;
 // 512 threads fit one workgroup per CU)
-static int ring_wg() {
-  static const int wg = [] {
-    const char *e = getenv("PGM_RING_WG");
-    const int v = e ? atoi(e) : 256;
-    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 256;
-  }();
-  return wg;
-}
+static constexpr int ring_wg() { return 256; }
 
-// the ring's waiting waves back off (knob PGM_RING_BACKOFF, default 1): the workgroup's token wave reads the
-// chip-wide poll token before trying to take it, and sleeps longer the longer it has waited (4 -> 12 -> 32
-// x 64 clocks).  768 token waves retrying one atomic every ~0.1 us while the ring idles saturate that
-// address and delay the one wave that reads the host counter
-static bool ring_backoff() {
-  static const bool on = [] {
-    const char *e = getenv("PGM_RING_BACKOFF");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  return on;
-}
+// the ring's waiting waves back off: the workgroup's token wave reads the chip-wide poll token before
+// trying to take it, and sleeps longer the longer it has waited (4 -> 12 -> 32 x 64 clocks).  768 token
+// waves retrying one atomic every ~0.1 us while the ring idles saturate that address and delay the one
+// wave that reads the host counter (r03: ring-ready 20 steps 17.1 -> 29.5-30.8 G rows/s)
+static constexpr bool ring_backoff() { return true; }
 
 static std::vector<int> rows_cols(const pgm_rows_plan *pl);
 static void emit_rows_code_loads(std::string &o, const std::vector<int> &cols, int R, bool coherent = false);
@@ -2803,10 +2543,8 @@ static void emit_rows_compute(std::string &o, const pgm_rows_plan *pl, int R, co
 // R rows per thread (1, or 2 with 16-B marginal stores / 2-byte code loads); names carry the row's suffix
 static void emit_rows_kernel(std::string &o, const pgm_rows_plan *pl, int R) {
   const int NV = pl->n_values + 1;  // + trailing 1.0
-  // CPT values staged in LDS (default) or gathered straight from global memory (knob
-  // PGM_ROWS_JIT_LDS=0: no staging barrier; the values come from L1/L2)
-  static const bool lds_knob = !(getenv("PGM_ROWS_JIT_LDS") && atoi(getenv("PGM_ROWS_JIT_LDS")) == 0);
-  const bool lds = lds_knob && NV * 8 <= 48 * 1024;
+  // CPT values staged in LDS when they fit (else gathered straight from global memory through L1/L2)
+  const bool lds = NV * 8 <= 48 * 1024;
   const int WG = jit_wg();
   pgmi_appendf(o, "extern \"C\" __global__ void __launch_bounds__(%d) pgm_rows_jit%s(const double *__restrict__ V, "
              "const unsigned char *__restrict__ C, long long ldc, long long row0, long long n, "
@@ -3169,12 +2907,11 @@ static bool rows2_aligned(int32_t mode, const uint8_t *codes, int64_t ld_codes, 
 // (else the one-row kernel runs)
 static bool rows_jit2_ok(int32_t mode, const uint8_t *codes, int64_t ld_codes, int64_t row0, int64_t n_rows,
                          const double *marg, int64_t ld_out, const int32_t *map, const double *gap, int n_marg) {
-  static const bool off = getenv("PGM_NO_JIT2") != nullptr;  // testing / tuning
   // measured (MI355X): two rows with 16-B stores once the launch is HBM-bound (4M rows: 110 vs 126 us)
   // and, since the 512-thread workgroups and concurrent queues, at 100k rows too (one queue: equal,
   // 3.9 us; four queues: 2.7 -> 2.1 us per launch of GPU span, r02br); one row below 50k rows
-  static const int64_t min_rows = getenv("PGM_JIT2_MIN_ROWS") ? atoll(getenv("PGM_JIT2_MIN_ROWS")) : 50000;
-  if (off || n_rows < min_rows) return false;
+  static constexpr int64_t min_rows = 50000;
+  if (n_rows < min_rows) return false;
   return rows2_aligned(mode, codes, ld_codes, row0, n_rows, marg, ld_out, map, gap, n_marg);
 }
 
@@ -3544,14 +3281,11 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
                             "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
   hipStream_t s = S(stream);
   const bool two = k.n_ops <= 2;
-  // j-outer form (tuning knob PGM_MARG_JX = row pairs per lane: 1, 2 or 4; 0 = the j-inner kernel)
-  // default (-1): j-outer with 2 row pairs per lane from 1,024 row pairs up, else 1 (MI355X, pathfinder's
-  // largest clique: collect 413 -> 272 us at 4,000 rows, 94 -> 80 us at 1,000)
-  static const int JX = getenv("PGM_MARG_JX") ? atoi(getenv("PGM_MARG_JX")) : -1;
-  if (JX != 0) {
-    const int XI = JX < 0 ? (k.NP >= 1024 ? 2 : 1) : JX >= 4 ? 4 : JX == 2 ? 2 : 1;
-    const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
-    const dim3 gj((unsigned)gxj, g.y, 1);
+  // j-outer form: 2 row pairs per lane from 1,024 row pairs up, else 1 (MI355X, pathfinder's largest
+  // clique: collect 413 -> 272 us at 4,000 rows, 94 -> 80 us at 1,000, against r02's j-inner kernel)
+  const int XI = k.NP >= 1024 ? 2 : 1;
+  const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
+  const dim3 gj((unsigned)gxj, g.y, 1);
 #define PGM_MARGJ_LAUNCH(XX)                                                                                 \
   if (reduce == PGM_RED_SUM) {                                                                               \
     if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);      \
@@ -3560,24 +3294,12 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);      \
     else hipLaunchKernelGGL((k_productn_marg_jx<MOPS, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);       \
   }
-    if (XI == 4) {
-      PGM_MARGJ_LAUNCH(4)
-    } else if (XI == 2) {
-      PGM_MARGJ_LAUNCH(2)
-    } else {
-      PGM_MARGJ_LAUNCH(1)
-    }
-#undef PGM_MARGJ_LAUNCH
-    HIP_TRY(hipGetLastError());
-    return PGM_OK;
-  }
-  if (reduce == PGM_RED_SUM) {
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_SUM>), g, dim3(256), 0, s, k, C, M);
+  if (XI == 2) {
+    PGM_MARGJ_LAUNCH(2)
   } else {
-    if (two) hipLaunchKernelGGL((k_productn_marg2<2, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
-    else hipLaunchKernelGGL((k_productn_marg2<MOPS, PGM_RED_MAX>), g, dim3(256), 0, s, k, C, M);
+    PGM_MARGJ_LAUNCH(1)
   }
+#undef PGM_MARGJ_LAUNCH
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }
@@ -3651,51 +3373,20 @@ static int plan_gather(const pgm_gather_desc *d, GatherK &k) {
 struct BatchHandle {
   std::vector<BatchJob> jobs;
   std::vector<uint32_t> block_job;
-  std::vector<uint32_t> level_off{0};  // levelled batch: first block of each level (+ the end)
+  std::vector<uint32_t> level_off{0};  // single-workgroup levelled batch: first block of each level (+ the end)
   BatchJob *d_jobs = nullptr;
   uint32_t *d_map = nullptr;
   uint32_t *d_level = nullptr;
-  unsigned *d_bar = nullptr;  // grid barrier: arrivals, generation, timeout status
-  unsigned grid = 0;          // persistent grid (levelled batch)
-  unsigned long long timeout_ticks = 0;
-  int32_t mode = PGM_BATCH_GRID;  // PGM_BATCH_ONE_WORKGROUP: k_batch_wg
+  int32_t mode = PGM_BATCH_GRID;  // PGM_BATCH_ONE_WORKGROUP: k_batch_wg_c
   int32_t spec = -1;  // every job a contraction with one (combine, reduce): combine * 3 + reduce; products: 100
-  ChainJob *d_chain = nullptr;  // ONE_WORKGROUP batch of contractions only: descriptors staged in LDS
+  ChainJob *d_chain = nullptr;  // ONE_WORKGROUP batch (contractions only): descriptors staged in LDS
   size_t chain_lds = 0;         // dynamic LDS bytes of k_batch_wg_c
 };
 
-// workgroups of k_batch_levels that are resident at once (the grid barrier needs all of them),
-// capped by PGM_BATCH_LEVELS_GRID (A/B knob)
-static unsigned batch_levels_cap() {
-  static unsigned cap = 0;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_batch_levels, 256, 0) == hipSuccess)
-      cap = (unsigned)std::max(0, cus * per);
-    (void)hipGetLastError();
-    if (const char *e = getenv("PGM_BATCH_LEVELS_GRID")) {
-      const long v = atol(e);
-      if (v > 0 && cap) cap = std::min<unsigned>(cap, (unsigned)v);
-    }
-  });
-  return cap;
-}
-
 static const int32_t kBatchSpecProducts = 100;  // BatchHandle::spec of a products-only batch
-// single-workgroup chains of contractions: descriptors staged in LDS (k_batch_wg_c) up to this many bytes
-// of tables; A/B knob PGM_CHAIN_LDS=0 for k_batch_wg
+// single-workgroup chains of contractions: descriptors, block map and level table staged in LDS
+// (k_batch_wg_c) up to this many bytes
 static const size_t kChainLdsMax = 48 * 1024;
-static const bool g_chain_lds = [] {
-  const char *e = getenv("PGM_CHAIN_LDS");
-  return !(e && e[0] == '0');
-}();
-static const bool g_batch_specialise = [] {
-  const char *e = getenv("PGM_BATCH_SPECIALISE");
-  return !(e && e[0] == '0');
-}();
 
 template <int CMB>
 static void launch_batch_cr(int red, dim3 g, hipStream_t s, const BatchJob *jobs, const uint32_t *map) {
@@ -3718,26 +3409,17 @@ static void launch_batch_c(int spec, dim3 g, hipStream_t s, const BatchJob *jobs
 }
 
 // a batch contraction job with a reduction takes G lanes per output (G a power of two up to the innermost
-// reduction extent) while its outputs x G stay under this many lanes; A/B knob PGM_BATCH_LANES
-static uint64_t batch_lanes_cap() {
-  static const uint64_t cap = [] {
-    const char *e = getenv("PGM_BATCH_LANES");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint64_t)v : (uint64_t)4096;
-  }();
-  return cap;
-}
-
-// workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that); A/B
-// knob PGM_BATCH_MAX_BLOCKS (1,024 / 4,096: no change on C1 / C2 / C4, profiles/r04j/)
-static uint64_t batch_max_blocks() {
-  static const uint64_t cap = [] {
-    const char *e = getenv("PGM_BATCH_MAX_BLOCKS");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint64_t)std::min(v, 1L << 20) : (uint64_t)256;
-  }();
-  return cap;
-}
+// reduction extent) while its outputs x G stay under this many lanes (r04: 32 K / 128 K slower on C2,
+// profiles/r04p/)
+static constexpr uint64_t kBatchLanesCap = 4096;
+// workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that; r04:
+// 1,024 / 4,096 no faster on C1 / C2 / C4, profiles/r04j/)
+static constexpr uint64_t kBatchMaxBlocks = 256;
+// a batch contraction without a reduction (a broadcast product or a copy: one load per operand per output)
+// may take more workgroups than one that reduces: its lanes otherwise walk several outputs one after
+// another, a full memory round trip each (C2's 448,000-output product level: 11.7 -> 8.9 us at 1,024
+// blocks, profiles/r04t/), while the reducing jobs of a level were measured slower with more
+static constexpr uint64_t kBatchMaxBlocksProduct = 1024;
 
 extern "C" {
 
@@ -3763,23 +3445,9 @@ int pgm_batch_create(void **handle) {
   return *handle ? PGM_OK : fail(PGM_ENOMEM, "batch_create: host allocation");
 }
 
-// a batch contraction without a reduction (a broadcast product or a copy: one load per operand per output)
-// may take more workgroups than one that reduces: its lanes otherwise walk several outputs one after
-// another, a full memory round trip each (C2's 448,000-output product level: 11.7 -> 8.9 us at 1,024
-// blocks, profiles/r04t/), while the reducing jobs of a level were measured slower with more; A/B knob
-// PGM_BATCH_MAX_BLOCKS_PRODUCT
-static uint64_t batch_max_blocks_product() {
-  static const uint64_t cap = [] {
-    const char *e = getenv("PGM_BATCH_MAX_BLOCKS_PRODUCT");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint64_t)std::min(v, 1L << 20) : (uint64_t)1024;
-  }();
-  return cap;
-}
-
 static int batch_append(BatchHandle *h, BatchJob &J, uint64_t threads, uint64_t cap = 0) {
   if (h->d_jobs) return fail(PGM_EINVAL, "batch: already finalized");
-  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), cap ? cap : batch_max_blocks());
+  const uint64_t nb = std::min<uint64_t>(std::max<uint64_t>((threads + 255) / 256, 1), cap ? cap : kBatchMaxBlocks);
   if (h->block_job.size() + nb > 0x7fffffffull) return fail(PGM_EINVAL, "batch: too many blocks");
   J.block0 = (uint32_t)h->block_job.size();
   J.nblocks = (uint32_t)nb;
@@ -3813,7 +3481,7 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   k.red_chunk = k.n_ro;
   // (a single-workgroup levelled batch runs its blocks one after another: spread a job over at most
   // one block's lanes there)
-  const uint64_t lanes_cap = h->mode == PGM_BATCH_ONE_WORKGROUP ? 256 : batch_lanes_cap();
+  const uint64_t lanes_cap = h->mode == PGM_BATCH_ONE_WORKGROUP ? 256 : kBatchLanesCap;
   int g = 0;
   if (d->reduce != PGM_RED_NONE && (uint64_t)k.n_ro * k.ri_card > 1)
     while (g < 6 && ((uint64_t)k.n_out << g) < lanes_cap && (1u << (g + 1)) <= k.ri_card) ++g;
@@ -3830,9 +3498,9 @@ int pgm_batch_add_contract(void *handle, const pgm_contract_desc *d, const doubl
   if (pairs) pairs = (!va || (k.ri_sa % 2 == 0 && ((uintptr_t)A & 15) == 0)) && (!vb || (k.ri_sb % 2 == 0 && ((uintptr_t)B & 15) == 0));
   if (pairs) {
     k.row_mode = 2;
-    return batch_append(h, J, (uint64_t)k.n_out / 2, k.n_red <= 1 ? batch_max_blocks_product() : 0);
+    return batch_append(h, J, (uint64_t)k.n_out / 2, k.n_red <= 1 ? kBatchMaxBlocksProduct : 0);
   }
-  return batch_append(h, J, (uint64_t)k.n_out << g, k.n_red <= 1 ? batch_max_blocks_product() : 0);
+  return batch_append(h, J, (uint64_t)k.n_out << g, k.n_red <= 1 ? kBatchMaxBlocksProduct : 0);
 }
 
 int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A, const uint8_t *codes, double *C,
@@ -3920,6 +3588,7 @@ int pgm_batch_add_level(void *handle) {
   BatchHandle *h = (BatchHandle *)handle;
   if (!h) return fail(PGM_EINVAL, "batch_add_level: null handle");
   if (h->d_jobs) return fail(PGM_EINVAL, "batch_add_level: already finalized");
+  if (h->mode != PGM_BATCH_ONE_WORKGROUP) return fail(PGM_EINVAL, "batch_add_level: levels need PGM_BATCH_ONE_WORKGROUP");
   if (h->block_job.size() > h->level_off.back()) h->level_off.push_back((uint32_t)h->block_job.size());
   return PGM_OK;
 }
@@ -3928,14 +3597,12 @@ static void batch_free(BatchHandle *h) {
   if (h->d_jobs) (void)hipFree(h->d_jobs);
   if (h->d_map) (void)hipFree(h->d_map);
   if (h->d_level) (void)hipFree(h->d_level);
-  if (h->d_bar) (void)hipFree(h->d_bar);
   if (h->d_chain) (void)hipFree(h->d_chain);
   h->d_chain = nullptr;
   h->chain_lds = 0;
   h->d_jobs = nullptr;
   h->d_map = nullptr;
   h->d_level = nullptr;
-  h->d_bar = nullptr;
 }
 
 int pgm_batch_finalize(void *handle) {
@@ -3944,64 +3611,47 @@ int pgm_batch_finalize(void *handle) {
   if (!h) return fail(PGM_EINVAL, "batch_finalize: null handle");
   if (h->d_jobs || h->jobs.empty()) return PGM_OK;
   if (h->level_off.back() < h->block_job.size()) h->level_off.push_back((uint32_t)h->block_job.size());
-  const size_t n_levels = h->level_off.size() - 1;
   h->spec = -1;
-  if (g_batch_specialise) {
-    bool uni = true;
-    for (const BatchJob &J : h->jobs)
-      uni = uni && J.kind == 0 && J.cmb == h->jobs[0].cmb && J.red == h->jobs[0].red;
-    if (uni) h->spec = h->jobs[0].cmb * 3 + h->jobs[0].red;
-    bool prod = true;
-    for (const BatchJob &J : h->jobs) prod = prod && J.kind == 2;
-    if (prod) h->spec = kBatchSpecProducts;
+  bool uni = true, prod = true, contract_only = true;
+  for (const BatchJob &J : h->jobs) {
+    uni = uni && J.kind == 0 && J.cmb == h->jobs[0].cmb && J.red == h->jobs[0].red;
+    prod = prod && J.kind == 2;
+    contract_only = contract_only && J.kind == 0;
   }
+  if (uni) h->spec = h->jobs[0].cmb * 3 + h->jobs[0].red;
+  if (prod) h->spec = kBatchSpecProducts;
+  const size_t lds = h->jobs.size() * sizeof(ChainJob) + 4 * (h->block_job.size() + h->level_off.size());
+  if (h->mode == PGM_BATCH_ONE_WORKGROUP && !contract_only)
+    return fail(PGM_EINVAL, "batch_finalize: a single-workgroup batch takes contractions only");
+  if (h->mode == PGM_BATCH_ONE_WORKGROUP && lds > kChainLdsMax)
+    return fail(PGM_EINVAL, "batch_finalize: single-workgroup tables of %zu bytes exceed the LDS budget", lds);
   hipError_t e = hipMalloc((void **)&h->d_jobs, sizeof(BatchJob) * h->jobs.size());
   if (e == hipSuccess) e = hipMalloc((void **)&h->d_map, sizeof(uint32_t) * h->block_job.size());
   if (e == hipSuccess)
     e = hipMemcpy(h->d_jobs, h->jobs.data(), sizeof(BatchJob) * h->jobs.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipMemcpy(h->d_map, h->block_job.data(), sizeof(uint32_t) * h->block_job.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess && h->mode == PGM_BATCH_ONE_WORKGROUP) {  // level table only, no grid barrier
+  if (e == hipSuccess && h->mode == PGM_BATCH_ONE_WORKGROUP) {  // k_batch_wg_c: staged descriptors + level table
     e = hipMalloc((void **)&h->d_level, sizeof(uint32_t) * h->level_off.size());
     if (e == hipSuccess)
       e = hipMemcpy(h->d_level, h->level_off.data(), sizeof(uint32_t) * h->level_off.size(), hipMemcpyHostToDevice);
-    // contractions only, and the staged tables fit the LDS budget: k_batch_wg_c
-    bool contract_only = g_chain_lds;
-    for (const BatchJob &J : h->jobs) contract_only = contract_only && J.kind == 0;
-    const size_t lds = h->jobs.size() * sizeof(ChainJob) + 4 * (h->block_job.size() + h->level_off.size());
-    if (e == hipSuccess && contract_only && lds <= kChainLdsMax) {
-      std::vector<ChainJob> cj(h->jobs.size());
-      for (size_t i = 0; i < h->jobs.size(); ++i) {
-        const BatchJob &J = h->jobs[i];
-        ChainJob &c = cj[i];
-        memset(&c, 0, sizeof c);
-        c.cmb = J.cmb;
-        c.red = J.red;
-        c.block0 = J.block0;
-        c.nblocks = J.nblocks;
-        c.A = J.A;
-        c.B = J.B;
-        c.C = J.C;
-        c.c = J.c;
-      }
-      e = hipMalloc((void **)&h->d_chain, sizeof(ChainJob) * cj.size());
-      if (e == hipSuccess) e = hipMemcpy(h->d_chain, cj.data(), sizeof(ChainJob) * cj.size(), hipMemcpyHostToDevice);
-      if (e == hipSuccess) h->chain_lds = lds;
+    std::vector<ChainJob> cj(h->jobs.size());
+    for (size_t i = 0; i < h->jobs.size(); ++i) {
+      const BatchJob &J = h->jobs[i];
+      ChainJob &c = cj[i];
+      memset(&c, 0, sizeof c);
+      c.cmb = J.cmb;
+      c.red = J.red;
+      c.block0 = J.block0;
+      c.nblocks = J.nblocks;
+      c.A = J.A;
+      c.B = J.B;
+      c.C = J.C;
+      c.c = J.c;
     }
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-  } else if (e == hipSuccess && n_levels > 1) {
-    uint32_t widest = 0;
-    for (size_t l = 0; l < n_levels; ++l) widest = std::max(widest, h->level_off[l + 1] - h->level_off[l]);
-    h->grid = std::min(widest, batch_levels_cap());
-    int dev = 0, khz = 100000;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    (void)hipGetLastError();
-    h->timeout_ticks = (unsigned long long)std::max(khz, 1) * 1000ull * 2ull;  // 2 s per launch
-    e = hipMalloc((void **)&h->d_level, sizeof(uint32_t) * h->level_off.size());
-    if (e == hipSuccess)
-      e = hipMemcpy(h->d_level, h->level_off.data(), sizeof(uint32_t) * h->level_off.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc((void **)&h->d_bar, 4 * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemset(h->d_bar, 0, 4 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMalloc((void **)&h->d_chain, sizeof(ChainJob) * cj.size());
+    if (e == hipSuccess) e = hipMemcpy(h->d_chain, cj.data(), sizeof(ChainJob) * cj.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) h->chain_lds = lds;
     if (e == hipSuccess) e = hipDeviceSynchronize();
   }
   if (e != hipSuccess) {
@@ -4018,19 +3668,10 @@ int pgm_batch_run(void *handle, void *stream) {
   if (!h) return fail(PGM_EINVAL, "batch_run: null handle");
   if (h->jobs.empty()) return PGM_OK;
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
-  const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
-  if (h->mode == PGM_BATCH_ONE_WORKGROUP && h->d_chain) {
+  if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
+    const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
     hipLaunchKernelGGL(k_batch_wg_c, dim3(1), dim3(256 * kChainVB), h->chain_lds, S(stream), (const ChainJob *)h->d_chain,
                        h->d_map, h->d_level, n_levels, (uint32_t)h->jobs.size(), (uint32_t)h->block_job.size());
-  } else if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
-    hipLaunchKernelGGL(k_batch_wg, dim3(1), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level, n_levels);
-  } else if (n_levels > 1 && h->grid > 0) {
-    hipLaunchKernelGGL(k_batch_levels, dim3(h->grid), dim3(256), 0, S(stream), h->d_jobs, h->d_map, h->d_level,
-                       n_levels, h->d_bar, h->timeout_ticks);
-  } else if (n_levels > 1) {  // no occupancy figure: one launch per level, in order on the stream
-    for (uint32_t l = 0; l < n_levels; ++l)
-      hipLaunchKernelGGL(k_batch, dim3(h->level_off[l + 1] - h->level_off[l]), dim3(256), 0, S(stream), h->d_jobs,
-                         h->d_map + h->level_off[l]);
   } else if (h->spec == kBatchSpecProducts) {
     hipLaunchKernelGGL(k_batch_p, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
   } else if (h->spec >= 0) {
@@ -4039,28 +3680,6 @@ int pgm_batch_run(void *handle, void *stream) {
     hipLaunchKernelGGL(k_batch, dim3((unsigned)h->block_job.size()), dim3(256), 0, S(stream), h->d_jobs, h->d_map);
   }
   HIP_TRY(hipGetLastError());
-  return PGM_OK;
-}
-
-int pgm_batch_info(void *handle, int32_t *n_levels, int32_t *grid, int32_t *timed_out) {
-  STALE_PROBE();
-  BatchHandle *h = (BatchHandle *)handle;
-  if (!h) return fail(PGM_EINVAL, "batch_info: null handle");
-  if (n_levels) *n_levels = (int32_t)h->level_off.size() - 1;
-  if (grid) *grid = (int32_t)h->grid;
-  if (timed_out) {
-    *timed_out = 0;
-    if (h->d_bar) {  // after the launches completed: a barrier that timed out leaves its words reset
-      unsigned w[4] = {0, 0, 0, 0};
-      HIP_TRY(hipDeviceSynchronize());
-      HIP_TRY(hipMemcpy(w, h->d_bar, sizeof w, hipMemcpyDeviceToHost));
-      if (w[2]) {
-        *timed_out = 1;
-        HIP_TRY(hipMemset(h->d_bar, 0, sizeof w));
-        HIP_TRY(hipDeviceSynchronize());
-      }
-    }
-  }
   return PGM_OK;
 }
 
@@ -4131,24 +3750,21 @@ int pgm_gemm(const pgm_gemm_desc *d, const double *A, const double *B, double *C
   k.s_bk = d->stride[6];
   k.s_bn = d->stride[7];
   k.s_cn = d->stride[8];
-  // block tile by M (knob PGM_GEMM_TILE=64: always 64x64)
-  static const bool tile64 = getenv("PGM_GEMM_TILE") && atoi(getenv("PGM_GEMM_TILE")) == 64;
+  // block tile by M
   // 128-row tile only while it still gives >= 4 blocks per CU (it halves the blocks of a 65..128-row
   // step; it pays when B is large and would be read twice: C2's 500 x (100 x 576 x 125) step 495 -> 396 us)
   const bool tall_ok = d->m > 64 && d->m <= 128 && (uint64_t)d->batch * (((uint64_t)d->n + 63) / 64) >= 1024;
-  const int cfg = tile64 ? 0 : d->m <= 16 ? 1 : tall_ok ? 2 : 0;
+  const int cfg = d->m <= 16 ? 1 : tall_ok ? 2 : 0;
   const uint64_t BM = cfg == 1 ? 16 : cfg == 2 ? 128 : 64, BN = cfg == 1 ? 128 : 64;
   const uint64_t tn = ((uint64_t)d->n + BN - 1) / BN, tm = ((uint64_t)d->m + BM - 1) / BM;
   if (tn * tm > 0x7fffffffull || d->batch > 65535ll * 65535ll) return fail(PGM_EINVAL, "gemm: grid too large");
   k.tiles_n = (uint32_t)tn;
   if (d->k == 0) return fail(PGM_EINVAL, "gemm: k == 0 (nothing to sum; use the generic contraction)");
-  // tile-load lane order along each operand's unit-stride axis (knob PGM_GEMM_FIXED_ORDER: k-fast A,
-  // n-fast B always, the original mapping)
-  static const bool fixed_order = getenv("PGM_GEMM_FIXED_ORDER") != nullptr;
+  // tile-load lane order along each operand's unit-stride axis (r01: 28.7 -> 32.6 TF/s on plain layouts)
   const bool am_unit = d->stride[3] == 1 || (d->stride[3] < 0 && (d->lane_order & 1));
   const bool bk_unit = d->stride[6] == 1 || (d->stride[6] < 0 && (d->lane_order & 2));
-  k.a_mfast = (!fixed_order && am_unit && d->stride[5] != 1) ? 1u : 0u;
-  k.b_kfast = (!fixed_order && bk_unit && d->stride[7] != 1) ? 1u : 0u;
+  k.a_mfast = (am_unit && d->stride[5] != 1) ? 1u : 0u;
+  k.b_kfast = (bk_unit && d->stride[7] != 1) ? 1u : 0u;
   const bool ta = d->stride[0] < 0 || d->stride[3] < 0 || d->stride[5] < 0;
   const bool tb = d->stride[1] < 0 || d->stride[6] < 0 || d->stride[7] < 0;
   const bool tc = d->stride[2] < 0 || d->stride[4] < 0 || d->stride[8] < 0;
@@ -4719,14 +4335,7 @@ int pgm_rows_bound_destroy(void *bound) {
 // the plan's pass, its outputs out to the caller's host arrays at the chunk's columns.  Each side's
 // stream orders its own chunks, so chunk c + 2 reuses the buffer only after chunk c's copy-out; with
 // pinned host arrays (pgm_host_alloc / hipHostRegister) the two sides' DMA and kernels overlap.
-static int64_t shard_chunk_rows() {
-  static const int64_t v = [] {
-    const char *e = getenv("PGM_SHARD_CHUNK");
-    const long long x = e ? atoll(e) : 0;
-    return (int64_t)(x >= 16 ? x & ~15LL : 262144);  // 256 K rows: 36 MB of marginals per chunk
-  }();
-  return v;
-}
+static constexpr int64_t shard_chunk_rows() { return 262144; }  // 256 K rows: 36 MB of marginals per chunk
 
 static int shard_side_ready(RowsHandle::ShardSide &sd, size_t need) {
   if (!sd.s) HIP_TRY(hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking));

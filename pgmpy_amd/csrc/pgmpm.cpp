@@ -175,7 +175,6 @@ struct PMSpec {  // one fused step's specialisation
   ProdMK k;
   int red = PGM_RED_SUM, XI = 1, unroll = 8;
   bool store = true, xcd = false, nt = false;
-  bool wt = false;    // write-through (sc1) 16-B product stores: no dirty lines left for the kernel's end
   bool has_m = true;  // false: the product alone (pgm_product_n_bind), no marginal
   unsigned gx = 1;
   uint64_t total = 0;  // blocks
@@ -198,22 +197,18 @@ static int pm_knob(const char *name, int dflt) {
 }
 
 // Decode order of a step's kept outer dims, fastest first (the last one is the slowest: with the XCD
-// grouping each XCD takes a contiguous range of it).  Default: the belief's own order (its fastest
-// dim fastest, so a block's neighbours write neighbouring addresses) — PGM_PM_XPART=0.  PGM_PM_KREV=1: reversed.
-// PGM_PM_XPART=1: the kept dim carried by the most row-operand bytes becomes the slowest, so each XCD
-// reads a disjoint slice of every operand that carries it (instead of all 8 re-reading an operand that
-// lacks the belief's slowest dim); =2: in addition the other dims vary fastest in order of the bytes
-// that carry them (least first), so consecutive blocks re-read the same operand entries while they are
-// in the XCD's L2 — the default since r04c (C4 pathfinder, 4,000 rows, with PGM_PM_XCD=2: fetch 7.75 ->
-// 6.32 GB per sweep, 1.04x the steps' own reads; profiles/r04c/).  cards[q], bytes_of(q) = row-operand
-// bytes that vary along kept dim q.
+// grouping each XCD takes a contiguous range of it).  The kept dim carried by the most row-operand bytes
+// becomes the slowest, so each XCD reads a disjoint slice of every operand that carries it (instead of
+// all 8 re-reading an operand that lacks the belief's slowest dim), and the other dims vary fastest in
+// order of the bytes that carry them (least first), so consecutive blocks re-read the same operand
+// entries while they are in the XCD's L2 (C4 pathfinder, 4,000 rows: fetch 7.75 -> 6.32 GB per sweep,
+// 1.04x the steps' own reads; r03's belief order and r04's partition-only and reversed forms measured
+// slower, profiles/r04c/).  cards[q], bytes_of(q) = row-operand bytes that vary along kept dim q.
 template <class BytesOf>
 static std::vector<int> pm_kept_order(int kx, const unsigned *cards, BytesOf bytes_of) {
-  static const int krev = pm_knob("PGM_PM_KREV", 0);
-  static const int xpart = pm_knob("PGM_PM_XPART", 2);  // r04c: 2 (fetch 7.75 -> 6.32 GB per 4,000-row sweep)
   std::vector<int> ord;
-  for (int qi = 0; qi < kx; ++qi) ord.push_back(krev ? qi : kx - 1 - qi);
-  if (!xpart || kx < 2) return ord;
+  for (int qi = 0; qi < kx; ++qi) ord.push_back(kx - 1 - qi);
+  if (kx < 2) return ord;
   int p = -1;
   double best = -1.0;
   for (int q = 0; q < kx; ++q) {
@@ -223,8 +218,7 @@ static std::vector<int> pm_kept_order(int kx, const unsigned *cards, BytesOf byt
   }
   if (p < 0) return ord;
   ord.erase(std::find(ord.begin(), ord.end(), p));
-  if (xpart == 2)
-    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return bytes_of(a) < bytes_of(b); });
+  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return bytes_of(a) < bytes_of(b); });
   ord.push_back(p);
   return ord;
 }
@@ -257,8 +251,6 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
   if (xcd) o += pm_xcd_remap(total);
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
-  if (store && sp.wt)
-    o += "  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0x7fffffff, 0x00020000);\n";
   o += "  unsigned idx = ob;\n  long long oc = 0, om = 0";
   for (int i = 0; i < k.n_ops; ++i) pgmi_appendf(o, ", f%d = 0", i);
   o += ";\n  (void)oc; (void)idx;\n";
@@ -370,14 +362,10 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     pgmi_appendf(o, "%sconst pgm_d2 w%d = {w%dx, w%dy};\n", ind.c_str(), u, u, u);
   }
   if (store) {
-    if (!sp.wt) pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
+    pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
     for (int u = 0; u < XI; ++u) {
       const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
-      if (sp.wt)  // byte offset < 2 GiB (checked at bind)
-        pgmi_appendf(o, "%s%s{ pgm_u32x4 q_; __builtin_memcpy(&q_, &w%d, 16); __builtin_amdgcn_raw_buffer_store_b128("
-                        "q_, rsC, (int)((oc + %s + 2LL * x%d) * 8LL), 0, 16); }\n",
-                     ind.c_str(), guard.c_str(), u, lin(k.rsc).c_str(), u);
-      else if (nt)
+      if (nt)
         pgmi_appendf(o, "%s%s__builtin_nontemporal_store(w%d, cj + x%d);\n", ind.c_str(), guard.c_str(), u, u);
       else
         pgmi_appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
@@ -394,12 +382,11 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     ind.resize(ind.size() - 2);
     pgmi_appendf(o, "%s}\n", ind.c_str());
   }
-  // marginal stores: plain (write-back L2), or nontemporal when the step stores no product (a
-  // marginal-only pass writes nothing else; knob PGM_PM_MNT=0 keeps them plain)
-  static const int mnt = pm_knob("PGM_PM_MNT", 1);
+  // marginal stores: nontemporal when the step stores no product (a marginal-only pass writes nothing
+  // else), plain (write-back L2) otherwise
   for (int u = 0; u < XI && has_m; ++u) {
     const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
-    if (mnt && !store)
+    if (!store)
       pgmi_appendf(o, "  %s__builtin_nontemporal_store(a%d, (pgm_d2 *)(M + om) + x%d);\n", guard.c_str(), u, u);
     else
       pgmi_appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
@@ -683,9 +670,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   if (r == 0)
     return pgmi_failf(PGM_EINVAL, "product_n_marginal: shape not supported by the fused kernel "
                             "(pgm_product_n_marginal_ok is 0: run pgm_product_n + pgm_contract)");
-  // knobs: PGM_PM_JIT=0 keeps the generic kernel; PGM_PM_JIT_MIN = smallest clique (entries incl.
-  // rows) specialised; PGM_PM_XI row pairs per lane; PGM_PM_UNROLL entries unrolled; PGM_PM_XCD
-  // block order grouped by XCD; PGM_PM_NT nontemporal belief stores
+  // PGM_PM_JIT=0 keeps the generic kernel (the specialised steps' reference path)
   static const int on = pm_knob("PGM_PM_JIT", 1);
   // defaults measured on MI355X, pathfinder C4 (4,000 / 1,000 rows: generic 781K / 515K calibrations/s;
   // specialised above 2M entries 911K / 601K; + one row pair per lane, nontemporal belief stores and
@@ -693,16 +678,17 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // r03ag, after the schedule changes (direct collect operands, 128-block fused floor): 2^18 / 2^16 / 2^14
   // -> 0.96-0.97 / 1.024-1.026 / 1.026-1.028 M calibrations/s at 1,000 rows, 1.27-1.28 / 1.28-1.29 /
   // 1.29 M at 4,000 (small steps specialised join their level's merged launch instead of launching alone)
-  static const int64_t min_entries = getenv("PGM_PM_JIT_MIN") ? atoll(getenv("PGM_PM_JIT_MIN")) : (1ll << 14);
-  static const int xi_knob = pm_knob("PGM_PM_XI", 0);  // 0: per step (below); 1 / 2 / 4 / 8: forced
-  // per step, at least this many row pairs per lane (1 / 2 / 4) when the rows fill them: 2 measured
-  // (MI355X, C4 4,000 rows: 1.146 -> 1.18 M calibrations/s; 1,000 rows unchanged, too few rows;
-  // forced 2 / 4 for every step, or a minimum of 4: slower, profiles/r02bw_c4_xi.txt)
-  static const int xi_min = pm_knob("PGM_PM_XI_MIN", 2);
-  static const int unroll = pm_knob("PGM_PM_UNROLL", 8);
-  static const int xcd_knob = pm_knob("PGM_PM_XCD", 2);  // r04c: 2 (with XPART 2: +1.9 % / +3 % at 4,000 / 1,000 rows)
-  static const int nt = pm_knob("PGM_PM_NT", 1);
-  static const int wt = pm_knob("PGM_PM_WT", 0);  // write-through product stores (A/B knob)
+  static constexpr int64_t min_entries = 1ll << 14;
+  // per step, at least this many row pairs per lane when the rows fill them: 2 measured (MI355X, C4
+  // 4,000 rows: 1.146 -> 1.18 M calibrations/s; 1,000 rows unchanged, too few rows; forced 2 / 4 for
+  // every step, or a minimum of 4: slower, profiles/r02bw_c4_xi.txt)
+  static constexpr int xi_min = 2;
+  // reduced entries unrolled (4 / 16: -2 % / -10 % at 4,000 rows, profiles/r04v/; 16 on the steps of few
+  // blocks only: +1.7 % at 1,000 rows, -3 to -5 % at 4,000, profiles/r04z/)
+  static constexpr int unroll = 8;
+  // nontemporal belief stores (default-policy stores: -5 % / -9 % at 4,000 / 1,000 rows; write-through
+  // product stores: -4 % / -8 %; profiles/r04v/)
+  static constexpr bool nt = true;
   static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
   const uint64_t entries = (uint64_t)k.n_outer * (uint64_t)k.n_red * 2ull * k.NP;
   if (!on || no_jit || entries < (uint64_t)min_entries) return PGM_OK;  // *bound NULL: generic kernel
@@ -710,10 +696,8 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // operands, products without a reduction) does little work per lane — one 16-B store and a few
   // loads — so its lifetime, not HBM, bounds the step; XI pairs per lane give each lane ~8 entries of
   // work while keeping >= 2,048 blocks (8 per CU) in the step
-  int XI = (xi_min == 2 || xi_min == 4) && (uint64_t)k.NP >= 256ull * xi_min ? xi_min : 1;
-  if (xi_knob == 1 || xi_knob == 2 || xi_knob == 4 || xi_knob == 8) {
-    XI = xi_knob;
-  } else {
+  int XI = (uint64_t)k.NP >= 256ull * xi_min ? xi_min : 1;
+  {
     const uint64_t red = std::max<uint64_t>(1, (uint64_t)k.n_red);
     while (XI < 8 && red * (uint64_t)XI < 8) {
       const int nx = XI * 2;
@@ -731,18 +715,10 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.red = reduce;
   sp.XI = XI;
   sp.unroll = unroll;
-  // a step of few blocks (C4 at 1,000 rows) has few waves per CU to hide its loads: a longer unroll keeps
-  // more of a lane's entries in flight.  A/B knob PGM_PM_UNROLL_SMALL = block count below which the unroll is
-  // PGM_PM_UNROLL_SMALL_N (default 16); 0 (the default) = off
-  static const int small_blocks = pm_knob("PGM_PM_UNROLL_SMALL", 0);
-  static const int small_unroll = pm_knob("PGM_PM_UNROLL_SMALL_N", 16);
-  if (small_blocks > 0 && total < (uint64_t)small_blocks) sp.unroll = small_unroll;
   sp.store = C != nullptr;
   sp.has_m = has_m;
-  // PGM_PM_XCD: 1 = XCD grouping when the block count is a multiple of 8, 2 = always (bijective remap)
-  sp.xcd = xcd_knob >= 2 || (xcd_knob == 1 && total % 8 == 0);
-  sp.nt = nt != 0;
-  sp.wt = wt != 0 && sp.store && entries * 8ull + 64ull < (1ull << 31);
+  sp.xcd = true;  // blocks grouped by XCD for any block count (bijective remap; r04c)
+  sp.nt = nt;
   sp.gx = (unsigned)gx;
   sp.total = total;
   std::vector<uint64_t> starts;
@@ -838,8 +814,8 @@ static int plan_two_marginals(const pgm_productn_desc *d, const double *const *o
       ++q.nZ;
     }
   }
-  // register accumulators: the smaller target's own states, unrolled (knob PGM_PM2_MAX_ACC, default 16)
-  static const unsigned max_acc = getenv("PGM_PM2_MAX_ACC") ? (unsigned)atoi(getenv("PGM_PM2_MAX_ACC")) : 16u;
+  // register accumulators: the smaller target's own states, unrolled (8 / 32: no better, profiles/r02bv_c4_knobs.txt)
+  static constexpr unsigned max_acc = 16u;
   (void)nu;
   if (std::min(q.n1, q.n2) > max_acc || nk >= (1ull << 31)) return 0;
   q.n_outer = (uint32_t)nk;
@@ -856,8 +832,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
   *bound = nullptr;
   if (reduce != PGM_RED_SUM && reduce != PGM_RED_MAX)
     return pgmi_failf(PGM_EINVAL, "product_n_marginals: reduce must be PGM_RED_SUM or PGM_RED_MAX");
-  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr || pm_knob("PGM_PM_JIT", 1) == 0 ||
-                             pm_knob("PGM_PM2", 1) == 0;
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr || pm_knob("PGM_PM_JIT", 1) == 0;
   if (no_jit) return PGM_OK;
   PMSpec sp;
   const int r = plan_two_marginals(d, ops, marg_s1, marg_s2, M1, M2, sp.mm);
@@ -867,7 +842,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
   sp.store = false;
   sp.gx = (sp.mm.NP + 255) / 256;
   sp.total = (uint64_t)sp.gx * sp.mm.n_outer;
-  sp.xcd = pm_knob("PGM_PM_XCD", 2) >= 2 || (pm_knob("PGM_PM_XCD", 2) == 1 && sp.total % 8 == 0);
+  sp.xcd = true;
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;
   const std::string src = pm_source({sp}, starts, &blocks);

@@ -19,8 +19,6 @@ one HIP graph.  Algorithmic bytes per calibration: 8 (sum|C| + 4 sum|S|) — eve
 every separator message and sigma' written and read once; SURVEY.md §8(d)'s 8 (4 sum|C| + 4 sum|S|)
 counts the reference's schedule, which reads and writes each belief in both passes.
 """
-import os
-
 import numpy as np
 
 from .. import _native as N
@@ -68,14 +66,6 @@ class BatchedCalibration:
         return dict(self._marg)
 
 
-DIRECT_OPS = os.environ.get("PGM_BP_DIRECT_OPS", "1") != "0"
-# _aggregate: a scope with at most this many operands hands them up unmultiplied, so the containing
-# scope's product takes them in the same pass (0: multiply at every scope first).  Measured no faster
-# (r03af: 4 vs 0 -> 0.87 vs 0.87-0.88 M at 1,000 rows, 1.27-1.28 vs 1.28 M at 4,000), so off; A/B knob
-# PGM_BP_FOLD_RAW
-FOLD_RAW = int(os.environ.get("PGM_BP_FOLD_RAW", "0"))
-
-
 def _aggregate(prog, small, clique_labels, scope_size):
     """Multiply the findings / messages entering a clique bottom-up over their scopes.
 
@@ -94,12 +84,6 @@ def _aggregate(prog, small, clique_labels, scope_size):
     for i, sc in enumerate(order):
         items = groups[sc] + folded[sc]
         bigger = [t for t in order[i + 1:] if set(sc) < set(t)]
-        if bigger and (len(items) <= FOLD_RAW or not FOLD_RAW):
-            if FOLD_RAW:
-                # a few operands go up as they are: the containing scope's product takes them in the
-                # same pass (one dependency level instead of one per nesting level of scopes)
-                folded[min(bigger, key=lambda t: (scope_size(t), len(t)))].extend(items)
-                continue
         if len(items) == 1:
             agg = items[0]
         else:
@@ -123,9 +107,7 @@ class BPSchedule:
         red = "sum" if operation == "marginalize" else "max"
         R = E.ROW
         # levelled: independent cliques' small products / separator marginals share one launch per
-        # dependency level (collect: tree height; distribute: depth)
-        if os.environ.get("PGM_BP_LEVELS") == "0":  # A/B knob: one launch per step
-            levels = False
+        # dependency level (collect: tree height; distribute: depth; r01: 408 -> 170 launches)
         prog = Program(levels=levels)
         dev = E.device()
         self.codes = torch.empty((max(1, len(self.ev_vars)), n_rows), dtype=torch.uint8, device=dev)
@@ -177,9 +159,9 @@ class BPSchedule:
                 sep = [v for v in ls if v in parent[c]]
                 # the message from the findings / child messages themselves when the fused pass takes
                 # them all: the aggregates (distribute's operands) are then off collect's critical path
-                # (one dependency level less per clique whose inputs share a scope; PGM_BP_DIRECT_OPS=0: A/B)
+                # (one dependency level less per clique whose inputs share a scope; +1-2 %, r03ad)
                 mops = ops
-                if DIRECT_OPS and len(ops) - 1 < len(small) and 1 + len(small) <= 4:
+                if len(ops) - 1 < len(small) and 1 + len(small) <= 4:
                     mops = [(t, ls)] + list(small)
                 bt, m, _ = prog.product_n_marginal(mops, ls + [R], sep + [R], reduce=red, store=False)
                 beliefs[c] = (bt, ls)  # the buffer distribute writes (the fallback path filled it already)
@@ -297,32 +279,12 @@ class BatchedJunctionTree:
         self.pot = {}
         self.card = {}
         self.states = {}
-        # clique layout: the variables most of the clique's separators share come first (slowest), e.g.
-        # pathfinder's Fault in all 57 separators of the root.  A fused clique pass walks its kept states
-        # in layout order and hands each XCD a contiguous range of them, so the shared variables split
-        # the work between XCDs — every separator-sized operand slice is then read by one XCD only —
-        # while the belief is still written in address order.  A/B knob PGM_BP_LAYOUT=1 (default: the
-        # factor's own order — the rule shortened the root levels but slowed the schedule as a whole).
-        shared = {}
-        # only the large cliques (measured: the uniform rule slowed the 8-12 K-state cliques' level,
-        # profiles/r03m_*): PGM_BP_LAYOUT_MIN states and up
-        layout_min = int(os.environ.get("PGM_BP_LAYOUT_MIN", 16384))
-        if os.environ.get("PGM_BP_LAYOUT", "0") == "1":  # measured slower overall (r03m/r03n): off
-            for a, b in jt.edges():
-                for v in set(a) & set(b):
-                    shared[(a, v)] = shared.get((a, v), 0) + 1
-                    shared[(b, v)] = shared.get((b, v), 0) + 1
+        # (r03 also tried a clique layout with the variables most separators share first: slower overall,
+        # profiles/r03m_*, r03n_*)
         for c in self.cliques:
             f = jt.get_factors(c)
             labels = list(f.variables)
-            t = f._d()
-            if shared and int(np.prod([int(k) for k in f.cardinality])) >= layout_min:
-                pos = {v: i for i, v in enumerate(labels)}
-                order = sorted(labels, key=lambda v: (-shared.get((c, v), 0), pos[v]))
-                if order != labels:
-                    t = E.contract(t, labels, None, None, order, combine="copy")
-                    labels = order
-            self.pot[c] = (t, labels)
+            self.pot[c] = (f._d(), labels)
             for v, k in zip(f.variables, f.cardinality):
                 self.card[v] = int(k)
             self.states.update({v: list(s) for v, s in f.state_names.items()})

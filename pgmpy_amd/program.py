@@ -7,50 +7,37 @@ them into a HIP graph (pgm_graph_capture_*) so a whole compiled schedule — a
 batched BP calibration, a fixed-shape contraction plan — is one launch.
 """
 import ctypes
-import os
 
 from . import _native as N
 from . import engine as E
 from . import hazard as H
 
 
-# index-space size (outputs x reduction) up to which a step joins a batch (knob PGM_BATCH_MAX_WORK)
-BATCH_MAX_WORK = int(os.environ.get("PGM_BATCH_MAX_WORK", 1 << 22))
-# a step the planner would split (few outputs, long reduction) joins only this small (PGM_BATCH_SPLIT_WORK)
-BATCH_SPLIT_WORK = int(os.environ.get("PGM_BATCH_SPLIT_WORK", 1 << 16))
+# index-space size (outputs x reduction) up to which a step joins a batch
+BATCH_MAX_WORK = 1 << 22
+# a step the planner would split (few outputs, long reduction) joins only this small
+BATCH_SPLIT_WORK = 1 << 16
 # the same for a plain Program's batches (the levels of a contraction path, C1 / C2): a split step costs two
 # launches (partials + final) at ~4.5 us each, more than the unsplit job takes inside the level's batch — C2
 # 0.218 -> 0.204 ms/query (profiles/r03w/)
-PLAIN_SPLIT_WORK = int(os.environ.get("PGM_PLAIN_SPLIT_WORK", 1 << 22))
+PLAIN_SPLIT_WORK = 1 << 22
 # outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
-# their own row-mode launch (16-B two-rows-per-lane).  Tuning knob: PGM_PRODN_BATCH_MAX.
-PRODN_BATCH_MAX = int(os.environ.get("PGM_PRODN_BATCH_MAX", 1 << 21))
+# their own row-mode launch (16-B two-rows-per-lane).  2 M best of 64 K / 512 K / 2 M / 4 M / 8 M
+# (profiles/r01i_c4_variants.txt); 256 K / 64 K within noise (r03ak)
+PRODN_BATCH_MAX = 1 << 21
 # levelled programs: n-ary products / separator marginals at least this large (entries) become
 # specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
-# take or that are below the engine's own threshold, PGM_PM_JIT_MIN)
-PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 14))  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
-# consecutive dependency levels made only of batch jobs run as ONE persistent launch with a grid barrier
-# between levels (pgm_batch_add_level) instead of one launch each.  A/B knob: PGM_BATCH_LEVELS=1.
-# Measured slower on C2 (r03f: 0.58-1.69 ms/query against 0.27 with one launch per level; a grid barrier
-# with its agent-scope write-back / invalidate costs more than a kernel boundary), so off by default.
-LEVEL_CHAIN = os.environ.get("PGM_BATCH_LEVELS", "0") == "1"
-# plain programs: consecutive dependency levels of at most this many 256-thread blocks each run in ONE
-# single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP: a level's blocks four at a time in a
-# 1,024-thread workgroup, a workgroup barrier between levels) instead of one launch each — the tail of a
-# contraction path (C1 / C2: the last levels down to the query marginal, then its normalisation).  r03
-# measured it no faster with the generic batch kernel, one 256-thread block at a time (C2 0.215-0.221
-# ms/query against 0.208-0.210); r04's contraction-only chain kernel stages the descriptors in LDS
-# (k_batch_wg_c): C2 0.173-0.174 against 0.179 ms, C1 0.067 against 0.069-0.071 (profiles/r04o/; 8 or
-# more blocks per level: C1 slower).  0 = one launch per level.
-WG_CHAIN_BLOCKS = int(os.environ.get("PGM_WG_CHAIN_BLOCKS", 4))
-# a plain Program's batch of ONE job: the job's own launch (pgm_contract / pgm_gather: the planner may
-# split a long reduction; the descriptor travels by value in the kernel arguments) or, with
-# PGM_ONE_JOB_AS_BATCH=1 (A/B knob), a one-job pgm_batch launch (descriptor in device memory)
-ONE_JOB_AS_BATCH = os.environ.get("PGM_ONE_JOB_AS_BATCH", "0") == "1"
-# n-ary products with more operands than one kernel takes: balanced tree (default) or sequential fold
-# (PGM_PRODN_TREE=0, A/B knob)
-TREE_PRODUCTS = os.environ.get("PGM_PRODN_TREE", "1") != "0"
-
+# take or that are below the engine's own threshold)
+PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
+# plain programs: consecutive dependency levels of at most this many 256-thread blocks each, all of their
+# jobs contractions, run in ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP, k_batch_wg_c:
+# descriptors staged in LDS, a level's blocks four at a time in a 1,024-thread workgroup, a workgroup
+# barrier between levels) instead of one launch each — the tail of a contraction path (C1 / C2: the last
+# levels down to the query marginal, then its normalisation).  C2 0.173-0.174 against 0.179 ms, C1 0.067
+# against 0.069-0.071 (profiles/r04o/; 8 or more blocks per level: C1 slower).  0 = one launch per level.
+# (r03's persistent grid-barrier form of several levels and its one-block-at-a-time generic chain were
+# measured slower and removed in r05.)
+WG_CHAIN_BLOCKS = 4
 
 
 def _key(t):
@@ -102,7 +89,6 @@ class Program:
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
         self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
-        self._chains = []  # levelled batch handles (several dependency levels in one launch)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
         self.merged_parts = {}  # step index -> full notes of the specialised steps merged into it
         self._plain_recs = []  # plain Program: one record per launch / batch job (check_hazards only)
@@ -163,7 +149,7 @@ class Program:
 
     def _batch_step(self, b):
         L = N.lib()
-        if len(b.jobs) == 1 and not ONE_JOB_AS_BATCH:  # a batch of one is just the job (its own planner's launch)
+        if len(b.jobs) == 1:  # a batch of one is just the job (its own planner's launch)
             kind, _, args = b.jobs[0]
             if kind == "contract":
                 return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), f"{kind} (batch of one)"
@@ -172,6 +158,27 @@ class Program:
         self._add_batch_jobs(h, b.jobs)
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
         return (lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")), f"batch of {len(b.jobs)}"
+
+    def _chain_batch(self, group):
+        """A single-workgroup levelled batch of `group`'s levels (contractions only), or None when its
+        staged tables exceed the kernel's LDS budget (pgm_batch_finalize: PGM_EINVAL)."""
+        L = N.lib()
+        h = ctypes.c_void_p()
+        N.check(L.pgm_batch_create(ctypes.byref(h)), "batch_create")
+        try:
+            N.check(L.pgm_batch_set_mode(h, N.BATCH_ONE_WORKGROUP), "batch_set_mode")
+            for m, b in enumerate(group):
+                if m:
+                    N.check(L.pgm_batch_add_level(h), "batch_add_level")
+                self._add_batch_jobs(h, b.jobs)
+            if L.pgm_batch_finalize(h) != 0:
+                L.pgm_batch_destroy(h)
+                return None
+        except Exception:
+            L.pgm_batch_destroy(h)
+            raise
+        self._handles.append(h)
+        return h
 
     def _lower_batches(self):
         """Plain Program: closed batches -> launches (see end_batch)."""
@@ -190,42 +197,29 @@ class Program:
             while j < n and isinstance(self._steps[j], _Batch):
                 j += 1
             group = self._steps[i:j]
-            if WG_CHAIN_BLOCKS > 0 and not LEVEL_CHAIN and len(group) >= 2:
-                # runs of consecutive tiny levels (each at most WG_CHAIN_BLOCKS blocks) -> one
-                # single-workgroup launch; the other levels keep one launch each
-                blocks = [self._batch_blocks(b) for b in group]
+            if WG_CHAIN_BLOCKS > 0 and len(group) >= 2:
+                # runs of consecutive tiny levels of contractions (each at most WG_CHAIN_BLOCKS blocks) ->
+                # one single-workgroup launch; the other levels keep one launch each
+                blocks = [self._batch_blocks(b) if all(kind == "contract" for kind, _, _ in b.jobs) else None
+                          for b in group]
                 k = 0
                 while k < len(group):
                     e = k
-                    while e < len(group) and blocks[e] <= WG_CHAIN_BLOCKS:
+                    while e < len(group) and blocks[e] is not None and blocks[e] <= WG_CHAIN_BLOCKS:
                         e += 1
                     if e - k >= 2:
-                        h = self._new_batch()
-                        N.check(L.pgm_batch_set_mode(h, N.BATCH_ONE_WORKGROUP), "batch_set_mode")
-                        for m, b in enumerate(group[k:e]):
-                            if m:
-                                N.check(L.pgm_batch_add_level(h), "batch_add_level")
-                            self._add_batch_jobs(h, b.jobs)
-                        N.check(L.pgm_batch_finalize(h), "batch_finalize")
-                        steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
-                        notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
-                                     f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
-                        k = e
-                        continue
+                        h = self._chain_batch(group[k:e])
+                        if h is not None:
+                            steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+                            notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
+                                         f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
+                            k = e
+                            continue
+                        e = k + 1  # tables over the LDS budget: one launch per level
                     fn, note = self._batch_step(group[k])
                     steps.append(fn)
                     notes.append(note)
                     k += 1
-            elif LEVEL_CHAIN and len(group) >= 2:
-                h = self._new_batch()
-                for k, b in enumerate(group):
-                    if k:
-                        N.check(L.pgm_batch_add_level(h), "batch_add_level")
-                    self._add_batch_jobs(h, b.jobs)
-                N.check(L.pgm_batch_finalize(h), "batch_finalize")
-                self._chains.append(h)
-                steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
-                notes.append(f"{len(group)} levels as one levelled batch of {sum(len(b.jobs) for b in group)} jobs")
             else:
                 for b in group:
                     fn, note = self._batch_step(b)
@@ -315,15 +309,8 @@ class Program:
         by_level = [[] for _ in range(n_lv)]
         for r in self._recs:
             by_level[r.level].append(r)
-        chain = []  # consecutive levels of batch jobs only, run as ONE levelled batch launch
         for lv, recs in enumerate(by_level):
-            if LEVEL_CHAIN and recs and all(r.job is not None for r in recs):
-                chain.append((lv, recs))
-                continue
-            self._flush_chain(chain)
-            chain = []
             self._emit_level(lv, recs)
-        self._flush_chain(chain)
 
     @staticmethod
     def _add_jobs(h, recs):
@@ -344,27 +331,6 @@ class Program:
         N.check(N.lib().pgm_batch_create(ctypes.byref(h)), "batch_create")
         self._handles.append(h)
         return h
-
-    def _flush_chain(self, chain):
-        """Consecutive levels made only of batch jobs: one levelled batch (pgm_batch_add_level between
-        levels; one persistent launch with a grid barrier per level boundary)."""
-        if len(chain) < 2:
-            for lv, recs in chain:
-                self._emit_level(lv, recs)
-            return
-        L = N.lib()
-        h = self._new_batch()
-        for i, (_, recs) in enumerate(chain):
-            if i:
-                N.check(L.pgm_batch_add_level(h), "batch_add_level")
-            self._add_jobs(h, recs)
-        N.check(L.pgm_batch_finalize(h), "batch_finalize")
-        self._steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
-        self._chains.append(h)
-        n_jobs = sum(len(recs) for _, recs in chain)
-        self.notes.append(f"levels {chain[0][0]}-{chain[-1][0]} as one levelled batch of {n_jobs} jobs")
-        self.step_bytes.append(sum(r.nbytes for _, recs in chain for r in recs))
-        self.step_levels.append(chain[0][0])
 
     def _emit_level(self, lv, recs):
         """One dependency level: its unbatched launches, then one batch launch of its small jobs."""
@@ -392,30 +358,11 @@ class Program:
         self.step_bytes.append(sum(r.nbytes for r in small))
         self.step_levels.extend([lv] * (len(self._steps) - n0))
 
-    def barrier_timed_out(self):
-        """Whether a levelled batch's grid barrier gave up since the last check (synchronises)."""
-        L = N.lib()
-        out = False
-        for h in self._chains:
-            t = ctypes.c_int32()
-            N.check(L.pgm_batch_info(h, None, None, ctypes.byref(t)), "batch_info")
-            out = out or bool(t.value)
-        return out
-
-    def chain_info(self):
-        """[(levels, persistent grid)] of the levelled batches (profiling aid)."""
-        L = N.lib()
-        res = []
-        for h in self._chains:
-            nl, g = ctypes.c_int32(), ctypes.c_int32()
-            N.check(L.pgm_batch_info(h, ctypes.byref(nl), ctypes.byref(g), None), "batch_info")
-            res.append((nl.value, g.value))
-        return res
-
     def _merge_pm(self, recs):
         """A level's specialised product+marginal steps as one launch per 64 (pgm_pm_merge); returns
-        the records merged (their launches are emitted here).  PGM_PM_MERGE=0 keeps them apart."""
-        if len(recs) < 2 or os.environ.get("PGM_PM_MERGE", "1") == "0":
+        the records merged (their launches are emitted here; one launch per step: -21 % / -35 % at
+        4,000 / 1,000 rows of C4, profiles/r04v/)."""
+        if len(recs) < 2:
             return set()
         L = N.lib()
         done = set()
@@ -500,7 +447,7 @@ class Program:
         ops = list(operands)
         kinds = list(kinds) if kinds is not None else [N.PRODN_MUL] * len(ops)
         L = N.lib()
-        if len(ops) > N.PRODN_MAX_OPS and all(k == N.PRODN_MUL for k in kinds) and TREE_PRODUCTS:
+        if len(ops) > N.PRODN_MAX_OPS and all(k == N.PRODN_MUL for k in kinds):
             # more operands than one kernel takes: a balanced tree of products (independent groups of
             # up to PRODN_MAX_OPS, then their partial products) instead of a sequential fold, so a
             # levelled program runs the groups in one level — pathfinder's root folds 46 one-variable
@@ -691,12 +638,6 @@ class Program:
         else:
             for step in self._steps:
                 step(s)
-        if self._chains and self.barrier_timed_out():
-            # a levelled batch's grid barrier (A/B knob PGM_BATCH_LEVELS=1) needs every workgroup of its
-            # persistent grid resident at once; when other work held CUs it gave up after its deadline and
-            # the later levels did not run (barrier_timed_out has reset its words for the next replay)
-            raise RuntimeError("levelled batch: the grid barrier timed out (workgroups not co-resident); "
-                               "the outputs of this run are incomplete")
 
     @E.exclusive
     def capture(self):

@@ -629,73 +629,13 @@ def test_batch_product_n_jobs(gpu):
     e_ = rng.random((3, 7))
     o4 = prog.product_n([(E.to_device(e_), ["x", "q"]), (c, ["x"])], ["x", "q"])
     assert prog.n_levels == 2
-    from pgmpy_amd.program import LEVEL_CHAIN
-
-    if LEVEL_CHAIN:  # both levels are batch jobs only: one levelled launch
-        assert len(prog) == 1 and prog.notes[0].startswith("levels 0-1 as one levelled batch of 4")
-    else:
-        assert len(prog) == 2 and prog.notes[0].startswith("level batch of 3")
+    assert len(prog) == 2 and prog.notes[0].startswith("level batch of 3")
     prog.run()
     np.testing.assert_array_equal(E.to_host(o4), e_ * E.to_host(c)[:, None])
     np.testing.assert_array_equal(E.to_host(o1), ref1)
     np.testing.assert_array_equal(E.to_host(x), ref2)
     np.testing.assert_array_equal(E.to_host(o3), np.transpose(ref1, (1, 0, 2)) * E.to_host(c)[:, None, None])
     assert not np.array_equal(x_before, ref2)
-
-
-def test_levelled_batch_chain_matches_numpy(gpu, monkeypatch):
-    """Twelve dependent levels of batch jobs (two independent chains of contractions, each level
-    reading the previous level's outputs) run as ONE persistent launch with a grid barrier between
-    levels (pgm_batch_add_level / k_batch_levels): every level's output equals numpy's, on repeated
-    runs (the barrier's generation carries over) and through a captured HIP graph; no barrier timed out."""
-    import torch
-
-    import pgmpy_amd.program as P
-    from pgmpy_amd.program import Program
-
-    monkeypatch.setattr(P, "LEVEL_CHAIN", True)  # off by default (slower on C2), tested here
-    E = _e()
-    rng = np.random.default_rng(5)
-    n_lv = 12
-    xs = [rng.random((16, 256)) for _ in range(2)]  # 64 K-entry index space per step: a batch job
-    Ws = [[rng.random((16, 16)) / 8 for _ in range(n_lv)] for _ in range(2)]
-    prog = Program(levels=True)
-    outs = [[], []]
-    for c in range(2):
-        cur = E.to_device(xs[c])
-        for lv in range(n_lv):
-            cur = prog.contract(E.to_device(Ws[c][lv]), ["b", "a"], cur, ["a", "r"], ["b", "r"], reduce="sum")
-            outs[c].append(cur)
-    assert prog.n_levels == n_lv
-    assert len(prog) == 1, prog.notes
-    (levels, grid), = prog.chain_info()
-    assert levels == n_lv and grid > 0
-    want = [[None] * n_lv for _ in range(2)]
-    for c in range(2):
-        h = xs[c]
-        for lv in range(n_lv):
-            h = Ws[c][lv] @ h
-            want[c][lv] = h
-
-    def check():
-        torch.cuda.synchronize()
-        assert not prog.barrier_timed_out()
-        for c in range(2):
-            for lv in range(n_lv):
-                np.testing.assert_allclose(E.to_host(outs[c][lv]), want[c][lv], rtol=1e-12)
-
-    prog.run()
-    check()
-    for o in outs[0] + outs[1]:
-        o.zero_()
-    prog.run()
-    prog.run()
-    check()
-    prog.capture()
-    for o in outs[0] + outs[1]:
-        o.zero_()
-    prog.run()
-    check()
 
 
 def test_single_workgroup_level_chain_matches_numpy(gpu, monkeypatch):
@@ -942,28 +882,3 @@ def test_two_marginals_one_pass(gpu, rows, red, ratio):
     np.testing.assert_allclose(E.to_host(Ms[1]), f(full, axis=(0, 1)), rtol=1e-13)
 
 
-@pytest.mark.parametrize("env", [{"PGM_PM_XCD": "1", "PGM_PM_XPART": "0"}, {"PGM_PM_XPART": "1"}, {"PGM_PM_XCD": "0"},
-                                 {"PGM_PM_KREV": "1", "PGM_PM_XPART": "0"}])
-def test_bp_block_order_knobs_bit_exact(gpu, tmp_path, env):
-    """The block-to-tile order knobs of the specialised batched-BP steps (bijective XCD grouping of any
-    block count, the XCD partition along the kept dim the row operands carry, the reversed decode)
-    only change which block computes which output: every clique belief of a 1,002-row pathfinder
-    calibration is bit-identical to the default order's (r04 default: XCD grouping of any block count,
-    XPART 2; against r03's order, the XPART 1 form, no grouping, the reversed decode; separate processes:
-    the knobs are read once)."""
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    worker = os.path.join(root, "tests", "workers", "c4_variant.py")
-    outs = []
-    for e in ({}, env):
-        out = str(tmp_path / f"c4_{len(outs)}.npz")
-        r = subprocess.run([sys.executable, worker, out], cwd=root, env={**os.environ, **e}, timeout=240,
-                           capture_output=True, text=True)
-        assert r.returncode == 0, r.stderr[-3000:]
-        outs.append(np.load(out))
-    a, b = outs
-    assert sorted(a.files) == sorted(b.files) and len(a.files) == 103
-    for k in a.files:
-        assert np.array_equal(a[k], b[k], equal_nan=True), k
