@@ -63,6 +63,7 @@ class ContractDesc(ctypes.Structure):
 
 
 PRODN_MAX_OPS = 8
+PM_MAX_OPS = 8  # operands of a fused product + marginal step (pgm_internal.h MOPS)
 
 
 PRODN_MUL, PRODN_RATIO, PRODN_DEN = 0, 1, 2

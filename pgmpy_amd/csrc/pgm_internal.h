@@ -31,7 +31,8 @@ int pgmi_failf(int code, const char *fmt, ...);  // printf-style pgmi_fail
 #include "pgmhip.h"
 
 #define KMAX 12  // dims of a contraction / fused-step index space (incl. the row dim)
-#define MOPS 4   // operands of a fused product + marginal step
+#define MOPS 8   // operands of a fused product + marginal step (r05: 4 -> 8, so a clique's pass reads its
+                 // child messages directly instead of pre-multiplied aggregates)
 
 // n / d for n < 2^31 with one mul-hi and one shift (Granlund-Montgomery round-up method)
 struct FDiv {

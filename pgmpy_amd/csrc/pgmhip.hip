@@ -3286,13 +3286,16 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
   const int XI = k.NP >= 1024 ? 2 : 1;
   const uint64_t gxj = (k.NP + 256ull * XI - 1) / (256ull * XI);
   const dim3 gj((unsigned)gxj, g.y, 1);
+#define PGM_MARGJ_NOPS(NO, XX)                                                                               \
+  if (reduce == PGM_RED_SUM) hipLaunchKernelGGL((k_productn_marg_jx<NO, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M); \
+  else hipLaunchKernelGGL((k_productn_marg_jx<NO, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);
 #define PGM_MARGJ_LAUNCH(XX)                                                                                 \
-  if (reduce == PGM_RED_SUM) {                                                                               \
-    if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);      \
-    else hipLaunchKernelGGL((k_productn_marg_jx<MOPS, PGM_RED_SUM, XX>), gj, dim3(256), 0, s, k, C, M);       \
+  if (two) {                                                                                                 \
+    PGM_MARGJ_NOPS(2, XX)                                                                                    \
+  } else if (k.n_ops <= 4) {                                                                                 \
+    PGM_MARGJ_NOPS(4, XX)                                                                                    \
   } else {                                                                                                   \
-    if (two) hipLaunchKernelGGL((k_productn_marg_jx<2, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);      \
-    else hipLaunchKernelGGL((k_productn_marg_jx<MOPS, PGM_RED_MAX, XX>), gj, dim3(256), 0, s, k, C, M);       \
+    PGM_MARGJ_NOPS(MOPS, XX)                                                                                 \
   }
   if (XI == 2) {
     PGM_MARGJ_LAUNCH(2)
@@ -3300,6 +3303,7 @@ int pgm_product_n_marginal(const pgm_productn_desc *d, const double *const *ops,
     PGM_MARGJ_LAUNCH(1)
   }
 #undef PGM_MARGJ_LAUNCH
+#undef PGM_MARGJ_NOPS
   HIP_TRY(hipGetLastError());
   return PGM_OK;
 }

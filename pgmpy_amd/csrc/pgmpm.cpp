@@ -188,7 +188,7 @@ struct PMBound {
   std::string src;
   unsigned blocks = 0;
   std::vector<PMSpec> specs;
-  std::vector<const double *> ptrs;  // 6 per body: o0..o3, C, M
+  std::vector<const double *> ptrs;  // per body: its n_ops operands, then C, M
 };
 
 static int pm_knob(const char *name, int dflt) {
@@ -237,6 +237,17 @@ static std::string pm_xcd_remap(uint64_t total) {
   return o;
 }
 
+// a body's signature: its block index, its n operands, then the product (C) and marginal (M) outputs
+static std::string pm_signature(const std::string &name, int n) {
+  std::string o = "__device__ __forceinline__ void " + name + "(unsigned b";
+  for (int i = 0; i < n; ++i) o += ", const double *__restrict__ o" + std::to_string(i);
+  o += ", double *__restrict__ C, double *__restrict__ M) {\n  (void)C; (void)M;\n";
+  return o;
+}
+
+// operand pointers a body takes (its PMBound::ptrs are these, then C and M)
+static int pm_nops(const PMSpec &sp) { return sp.multi ? sp.mm.n_ops : sp.k.n_ops; }
+
 // body `name` of one step: a device function of its block index within the step
 static std::string pm_body(const PMSpec &sp, const std::string &name) {
   const ProdMK &k = sp.k;
@@ -245,10 +256,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   const unsigned gx = sp.gx;
   const uint64_t total = sp.total;
   std::string o;
-  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
-             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
-             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
-  o += "  (void)o1; (void)o2; (void)o3; (void)C;\n";
+  o += pm_signature(name, k.n_ops);
   if (xcd) o += pm_xcd_remap(total);
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", gx, gx);
   o += "  unsigned idx = ob;\n  long long oc = 0, om = 0";
@@ -409,10 +417,7 @@ static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
   const char *mreg = treg == 0 ? "m1" : "m2", *mstr = treg == 0 ? "m2" : "m1";
   const unsigned nreg = treg == 0 ? q.n1 : q.n2;
   std::string o;
-  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned b, const double *__restrict__ o0, "
-             "const double *__restrict__ o1, const double *__restrict__ o2, const double *__restrict__ o3, "
-             "double *__restrict__ C, double *__restrict__ M) {\n", name.c_str());
-  o += "  (void)o1; (void)o2; (void)o3;\n";
+  o += pm_signature(name, q.n_ops);
   if (sp.xcd) o += pm_xcd_remap(sp.total);
   pgmi_appendf(o, "  const unsigned xb = b %% %uu, ob = b / %uu;\n", sp.gx, sp.gx);
   o += "  unsigned idx = ob;\n  long long m1 = 0, m2 = 0";
@@ -548,7 +553,7 @@ static std::string pm_multi_body(const PMSpec &sp, const std::string &name) {
   return o;
 }
 
-// kernel pgm_pm over the bodies (kernel argument: 6 pointers per body); starts[i] = first block of
+// kernel pgm_pm over the bodies (kernel argument: each body's operand pointers, then C and M); starts[i] = first block of
 // body i, returns the grid size through *blocks
 static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint64_t> &starts, uint64_t *blocks) {
   std::string o =
@@ -568,18 +573,24 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
     o += specs[i].multi ? pm_multi_body(specs[i], "pm" + std::to_string(i)) : pm_body(specs[i], "pm" + std::to_string(i));
   }
   *blocks = at;
-  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%zu][6]; };\n", n);
+  size_t nptr = 0;
+  for (const PMSpec &sp : specs) nptr += (size_t)pm_nops(sp) + 2;
+  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%zu]; };\n", nptr);
   o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const pgm_pm_args a) {\n"
        "  const unsigned b = blockIdx.x;\n";
+  size_t base = 0;
   for (size_t i = 0; i < n; ++i) {
+    const int no = pm_nops(specs[i]);
+    std::string call = "pm" + std::to_string(i) + "(b - " + std::to_string((unsigned long long)starts[i]) + "u";
+    for (int t = 0; t < no; ++t) call += ", a.p[" + std::to_string(base + t) + "]";
+    call += ", (double *)a.p[" + std::to_string(base + no) + "], (double *)a.p[" + std::to_string(base + no + 1) + "])";
+    base += (size_t)no + 2;
     if (n == 1) {
-      o += "  pm0(b, a.p[0][0], a.p[0][1], a.p[0][2], a.p[0][3], (double *)a.p[0][4], (double *)a.p[0][5]);\n";
+      o += "  " + call + ";\n";
       break;
     }
-    pgmi_appendf(o, "  if (b >= %lluu && b < %lluu) { pm%zu(b - %lluu, a.p[%zu][0], a.p[%zu][1], a.p[%zu][2], "
-               "a.p[%zu][3], (double *)a.p[%zu][4], (double *)a.p[%zu][5]); return; }\n",
-            (unsigned long long)starts[i], (unsigned long long)(starts[i] + specs[i].total), i,
-            (unsigned long long)starts[i], i, i, i, i, i, i);
+    pgmi_appendf(o, "  if (b >= %lluu && b < %lluu) { %s; return; }\n", (unsigned long long)starts[i],
+                 (unsigned long long)(starts[i] + specs[i].total), call.c_str());
   }
   o += "}\n";
   return o;
@@ -714,7 +725,11 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.k = k;
   sp.red = reduce;
   sp.XI = XI;
-  sp.unroll = unroll;
+  // entries unrolled: `unroll`, fewer when many row operands vary over the reduced entries (each unrolled
+  // entry keeps XI 16-B loads per such operand in flight: at most ~48, the 3-operand steps' budget)
+  int nvj = 0;
+  for (int t = 0; t < k.n_ops; ++t) nvj += k.vec[t] && k.jvar[t];
+  sp.unroll = std::max(1, std::min(unroll, 48 / std::max(1, nvj * XI)));
   sp.store = C != nullptr;
   sp.has_m = has_m;
   sp.xcd = true;  // blocks grouped by XCD for any block count (bijective remap; r04c)
@@ -733,7 +748,7 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   b->src = src;
   b->blocks = (unsigned)blocks;
   b->specs.push_back(sp);
-  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(k.ops[t]);
+  for (int t = 0; t < k.n_ops; ++t) b->ptrs.push_back(k.ops[t]);
   b->ptrs.push_back(C);
   b->ptrs.push_back(M);
   *bound = b;
@@ -851,7 +866,7 @@ int pgm_product_n_marginals_bind(const pgm_productn_desc *d, const double *const
   b->src = src;
   b->blocks = (unsigned)blocks;
   b->specs.push_back(sp);
-  for (int t = 0; t < MOPS; ++t) b->ptrs.push_back(t < d->n_ops ? ops[t] : ops[0]);
+  for (int t = 0; t < d->n_ops; ++t) b->ptrs.push_back(ops[t]);
   b->ptrs.push_back(M1);  // the C slot
   b->ptrs.push_back(M2);  // the M slot
   *bound = b;
@@ -887,6 +902,9 @@ int pgm_pm_bound_run(void *bound, void *stream) {
   return PGM_OK;
 }
 
+// a merged launch's kernel arguments stay within 4 KB (512 pointers)
+static constexpr size_t kPmMaxArgPtrs = 512;
+
 int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
   STALE_PROBE();
   if (!bounds || !merged || n < 1 || n > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: 1..64 bound steps");
@@ -900,6 +918,7 @@ int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
     ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
   }
   if (specs.size() > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: more than 64 bodies");
+  if (ptrs.size() > kPmMaxArgPtrs) return PGM_OK;  // kernel arguments over 4 KB: keep the separate launches
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;
   const std::string src = pm_source(specs, starts, &blocks);

@@ -151,7 +151,13 @@ class BPSchedule:
                 small.append((prog.indicator(self.codes[j], bjt.card[v], n_rows, err=self.err), [v, R]))
             for k in children[c]:
                 small.append(msgs[k])
-            ops = [(t, ls)] + _aggregate(prog, small, ls, scope_size)
+            # the clique's passes read its findings and child messages directly when one fused pass takes
+            # them all (and, below the root, sigma' / mu as well in distribute): no pre-multiplied
+            # aggregate is written and read again (r05: 530 MB written + 743 MB read per 4,000-row
+            # sweep of pathfinder went to aggregates); more operands than that are multiplied bottom-up
+            # over their scopes first (_aggregate)
+            direct = 1 + len(small) + (2 if c in parent else 0) <= N.PM_MAX_OPS
+            ops = [(t, ls)] + (list(small) if direct else _aggregate(prog, small, ls, scope_size))
             if len(ops) == 1:
                 ops.append((E.to_device(np.ones(n_rows)), [R]))  # broadcast psi over the rows
             operands[c] = ops
@@ -161,7 +167,7 @@ class BPSchedule:
                 # them all: the aggregates (distribute's operands) are then off collect's critical path
                 # (one dependency level less per clique whose inputs share a scope; +1-2 %, r03ad)
                 mops = ops
-                if len(ops) - 1 < len(small) and 1 + len(small) <= 4:
+                if len(ops) - 1 < len(small) and 1 + len(small) <= N.PM_MAX_OPS:
                     mops = [(t, ls)] + list(small)
                 bt, m, _ = prog.product_n_marginal(mops, ls + [R], sep + [R], reduce=red, store=False)
                 beliefs[c] = (bt, ls)  # the buffer distribute writes (the fallback path filled it already)
@@ -222,7 +228,7 @@ class BPSchedule:
                 for c in scopes[sc]:
                     tc, lc = beliefs[c]
                     mu, sl = msgs[c]
-                    if len(operands[c]) + 2 <= 4:  # sigma' / mu enter as a ratio operand pair (0/0 -> 0)
+                    if len(operands[c]) + 2 <= N.PM_MAX_OPS:  # sigma' / mu as a ratio operand pair (0/0 -> 0)
                         ops_c = operands[c] + [(sigma, sl), (mu, sl)]
                         kinds = [N.PRODN_MUL] * len(operands[c]) + [N.PRODN_RATIO, N.PRODN_DEN]
                     else:  # the separator-sized ratio folded into the aggregates

@@ -91,6 +91,7 @@ class Program:
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
         self.notes = []  # one short description per step (profiling aid: tools/program_steps.py)
         self.merged_parts = {}  # step index -> full notes of the specialised steps merged into it
+        self.merged_handles = {}  # step index -> the merged steps' own bound handles (profiling aid)
         self._plain_recs = []  # plain Program: one record per launch / batch job (check_hazards only)
         self._unit = 0  # plain Program: launch counter behind _Rec.step
         self._plain_lowered = -1  # plain Program: len(_steps) right after the last lowering
@@ -336,6 +337,8 @@ class Program:
         """One dependency level: its unbatched launches, then one batch launch of its small jobs."""
         small = [r for r in recs if r.job is not None]
         n0 = len(self._steps)
+        # (r05: launching the large steps alone, or ordering the merged bodies by size, measured slower:
+        # -6 to -18 % at 4,000 rows, profiles/r05g/)
         merged = self._merge_pm([r for r in recs if r.job is None and r.pm is not None])
         for r in recs:
             if r in merged:
@@ -366,8 +369,16 @@ class Program:
             return set()
         L = N.lib()
         done = set()
-        for i in range(0, len(recs), 64):
-            part = recs[i:i + 64]
+        parts, cur, n_ptr = [], [], 0
+        for r in recs:  # <= 64 bodies and <= 512 kernel-argument pointers (operands + C + M each) per launch
+            k = len(r.reads) + 2
+            if cur and (len(cur) == 64 or n_ptr + k > 512):
+                parts.append(cur)
+                cur, n_ptr = [], 0
+            cur.append(r)
+            n_ptr += k
+        parts.append(cur)
+        for part in parts:
             if len(part) < 2:
                 continue
             arr = (ctypes.c_void_p * len(part))(*[r.pm.value for r in part])
@@ -378,6 +389,7 @@ class Program:
             self._pm_bound.append(m)
             self._pm_launch.append(m)
             self.merged_parts[len(self._steps)] = [r.note for r in part]
+            self.merged_handles[len(self._steps)] = [r.pm for r in part]
             self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
             self.step_bytes.append(sum(r.nbytes for r in part))
@@ -468,7 +480,7 @@ class Program:
         args = (ctypes.byref(d), ptrs, N.ptr(out))
         job = ("product_n", args) if out.numel() <= PRODN_BATCH_MAX else None
         fn, pm = (lambda s, a=args: N.check(L.pgm_product_n(*a, s), "product_n")), None
-        if (job is None or out.numel() >= PM_PREFER_MIN) and self._levels and len(ops) <= 4:
+        if (job is None or out.numel() >= PM_PREFER_MIN) and self._levels and len(ops) <= N.PM_MAX_OPS:
             # a specialised step, merged with its level's
             bound = ctypes.c_void_p()
             N.check(L.pgm_product_n_bind(*args, ctypes.byref(bound)), "product_n_bind")
@@ -487,7 +499,7 @@ class Program:
         store=False asks for M alone: the fused kernel then writes nothing to C (the fallback
         still materialises C).  Returns (C, M, stored)."""
         ops = list(operands)
-        if len(ops) <= 4:
+        if len(ops) <= N.PM_MAX_OPS:
             d, ptrs, out2, ms, M, ok = E.prepare_product_n_marginal(ops, out_labels, marg_labels, out, kinds, store)
             if ok:
                 L = N.lib()
@@ -518,7 +530,7 @@ class Program:
         pass that stores nothing else (pgm_product_n_marginals_bind), or None when the pass does not
         take the shapes.  `out` (not written) only describes the product's index space."""
         ops = list(operands)
-        if len(ops) > 4 or not self._levels:
+        if len(ops) > N.PM_MAX_OPS or not self._levels:
             return None
         L = N.lib()
         d, ptrs, C = E.prepare_product_n(ops, out_labels, out, kinds)

@@ -14,6 +14,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _time_bound(L, N, h, reps=20):
+    """us per launch of one bound specialised step, replayed alone on the current stream."""
+    import torch
+
+    s = N.stream_handle()
+    N.check(L.pgm_pm_bound_run(h, s), "pm_bound_run")
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    N.check(L.pgm_event_create(ctypes.byref(a)))
+    N.check(L.pgm_event_create(ctypes.byref(b)))
+    N.check(L.pgm_event_record(a, s))
+    for _ in range(reps):
+        N.check(L.pgm_pm_bound_run(h, s), "pm_bound_run")
+    N.check(L.pgm_event_record(b, s))
+    torch.cuda.synchronize()
+    ms = ctypes.c_float()
+    N.check(L.pgm_event_elapsed_ms(a, b, ctypes.byref(ms)))
+    L.pgm_event_destroy(a)
+    L.pgm_event_destroy(b)
+    return ms.value * 1e3 / reps
+
+
 def main():
     import torch
 
@@ -41,6 +62,11 @@ def main():
         rec = {"i": i, "level": prog.step_levels[i] if i < len(prog.step_levels) else None, "us": us,
                "MB": prog.step_bytes[i] / 1e6 if i < len(prog.step_bytes) else None, "note": note,
                "parts": prog.merged_parts.get(i)}
+        hs = prog.merged_handles.get(i)
+        if hs and os.environ.get("PARTS", "1") == "1":  # each merged step alone, unmerged
+            arr = (ctypes.c_void_p * len(hs))(*[h.value for h in hs])
+            N.check(L.pgm_pm_prepare(arr, len(hs)), "pm_prepare")
+            rec["part_us"] = [_time_bound(L, N, h) for h in hs]
         b = (fn.__defaults__ or (None,))[0]
         if isinstance(b, ctypes.c_void_p) and b.value in pm:
             n = L.pgm_pm_bound_source(b, buf, len(buf))
