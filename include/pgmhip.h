@@ -332,6 +332,14 @@ int pgm_batch_set_mode(void *handle, int32_t mode);
 int pgm_batch_blocks(void *handle, int64_t *blocks);
 int pgm_batch_finalize(void *handle);
 int pgm_batch_run(void *handle, void *stream);
+/* The finalized batch (contraction jobs only, either mode) as ONE plan-specialised kernel (hipRTC,
+ * cached by source like the fused BP steps): each job's output decode, strides, reduction walk and
+ * lanes per output are literals and a block finds its job from literal block ranges, so no block map
+ * or descriptor is read (C1 / C2's path levels).  *bound = NULL when a job is not a contraction the
+ * generator takes (the generic pgm_batch_run stays); else prepare / run / destroy it with
+ * pgm_pm_prepare, pgm_pm_bound_run, pgm_pm_bound_destroy (not pgm_pm_merge).  The batch's pointers
+ * must stay valid; the batch handle itself may be destroyed. */
+int pgm_batch_specialise(void *handle, void **bound);
 int pgm_batch_destroy(void *handle);
 
 

@@ -187,6 +187,7 @@ _SIGS = {
     "pgm_batch_finalize": ([_P], ctypes.c_int),
     "pgm_batch_run": ([_P, _P], ctypes.c_int),
     "pgm_batch_destroy": ([_P], ctypes.c_int),
+    "pgm_batch_specialise": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
     "pgm_codes_select": ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int32, ctypes.c_int64, _P, _P],
                          ctypes.c_int),
     "pgm_graph_capture_begin": ([_P], ctypes.c_int),

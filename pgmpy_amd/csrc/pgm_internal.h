@@ -39,6 +39,36 @@ struct FDiv {
   uint32_t d, m, s;
 };
 
+// a planned contraction (pgmhip.hip plan_contract; the generic kernels read it, pgmpm.cpp compiles a
+// batch of them into a specialised kernel)
+struct ContractK {
+  int32_t nk, nr, g_log2, n_split;
+  uint32_t n_out, n_red, red_chunk, row_mode;  // red_chunk: reduction-OUTER indices per split
+  uint32_t n_ro, ri_card;                       // reduction = n_ro outer x ri_card innermost
+  int64_t ri_sa, ri_sb;                         // strides of the innermost reduction dim
+  uint32_t ri_chunk, ri_nb;                     // row mode: innermost dim cut in ri_nb chunks of ri_chunk
+  uint32_t n_v, _pad2;                          // row mode: virtual reduction-outer count n_ro * ri_nb
+  FDiv kdiv[KMAX];
+  int64_t ksa[KMAX], ksb[KMAX], ksc[KMAX];
+  FDiv rdiv[KMAX];
+  int64_t rsa[KMAX], rsb[KMAX];
+};
+
+// one contraction job of a batch (pgm_batch_*) as the specialiser sees it: blocks [block0, block0 +
+// nblocks) of the batch's 256-thread blocks, C[keep] = reduce(combine(A, B))
+struct pgmi_cs_job {
+  int32_t cmb, red;
+  uint32_t block0, nblocks;
+  const double *A, *B;
+  double *C;
+  ContractK k;
+};
+
+// a plan-specialised kernel for a batch of contraction jobs (pgmpm.cpp): one_wg = 0: one launch of
+// the batch's blocks (one level); 1: the single-workgroup levelled form (level_off: first block of
+// each level + the end).  *bound = NULL when a job is not one it takes (the generic kernel runs).
+int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int n_levels, int one_wg, void **bound);
+
 // the fused product + marginal step's plan (pgmhip.hip plans it and runs the generic kernels;
 // pgmpm.cpp compiles it into specialised kernels)
 struct ProdMK {

@@ -35,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 20  // 20: pgm_batch_info and the grid-barrier levelled batch removed (levels: single-workgroup mode only); 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 21  // 21: pgm_batch_specialise; 20: pgm_batch_info and the grid-barrier levelled batch removed (levels: single-workgroup mode only); 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;
@@ -92,18 +92,7 @@ __device__ __forceinline__ double max_nan(double a, double b) {
 
 // ----------------------------------------------------------------------------- contract
 
-struct ContractK {
-  int32_t nk, nr, g_log2, n_split;
-  uint32_t n_out, n_red, red_chunk, row_mode;  // red_chunk: reduction-OUTER indices per split
-  uint32_t n_ro, ri_card;                       // reduction = n_ro outer x ri_card innermost
-  int64_t ri_sa, ri_sb;                         // strides of the innermost reduction dim
-  uint32_t ri_chunk, ri_nb;                     // row mode: innermost dim cut in ri_nb chunks of ri_chunk
-  uint32_t n_v, _pad2;                          // row mode: virtual reduction-outer count n_ro * ri_nb
-  FDiv kdiv[KMAX];
-  int64_t ksa[KMAX], ksb[KMAX], ksc[KMAX];
-  FDiv rdiv[KMAX];
-  int64_t rsa[KMAX], rsb[KMAX];
-};
+// ContractK (the planned flat / row-mode contraction): pgm_internal.h
 
 template <int CMB>
 __device__ __forceinline__ double combine(double a, double b) {
@@ -3685,6 +3674,31 @@ int pgm_batch_run(void *handle, void *stream) {
   }
   HIP_TRY(hipGetLastError());
   return PGM_OK;
+}
+
+int pgm_batch_specialise(void *handle, void **bound) {
+  STALE_PROBE();
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !bound) return fail(PGM_EINVAL, "batch_specialise: null argument");
+  *bound = nullptr;
+  if (!h->d_jobs) return fail(PGM_EINVAL, "batch_specialise: not finalized");
+  std::vector<pgmi_cs_job> jobs;
+  for (const BatchJob &J : h->jobs) {
+    if (J.kind != 0 || J.c.n_split != 1) return PGM_OK;  // contractions only (no split-K partials)
+    pgmi_cs_job c;
+    c.cmb = J.cmb;
+    c.red = J.red;
+    c.block0 = J.block0;
+    c.nblocks = J.nblocks;
+    c.A = J.A;
+    c.B = J.B;
+    c.C = J.C;
+    c.k = J.c;
+    jobs.push_back(c);
+  }
+  if (jobs.empty()) return PGM_OK;
+  return pgmi_cs_bind(jobs.data(), (int)jobs.size(), h->level_off.data(), (int)h->level_off.size() - 1,
+                      h->mode == PGM_BATCH_ONE_WORKGROUP ? 1 : 0, bound);
 }
 
 int pgm_batch_destroy(void *handle) {

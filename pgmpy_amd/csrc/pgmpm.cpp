@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <functional>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -189,6 +190,7 @@ struct PMBound {
   unsigned blocks = 0;
   std::vector<PMSpec> specs;
   std::vector<const double *> ptrs;  // per body: its n_ops operands, then C, M
+  unsigned threads = 256;  // workitems per workgroup (a specialised contraction chain: 1,024)
 };
 
 static int pm_knob(const char *name, int dflt) {
@@ -898,7 +900,7 @@ int pgm_pm_bound_run(void *bound, void *stream) {
   size_t sz = b->ptrs.size() * sizeof(void *);
   void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, (void *)b->ptrs.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
-  HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, 256, 1, 1, 0, S(stream), nullptr, extra));
+  HIP_TRY(hipModuleLaunchKernel(b->fn, b->blocks, 1, 1, b->threads, 1, 1, 0, S(stream), nullptr, extra));
   return PGM_OK;
 }
 
@@ -914,6 +916,7 @@ int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
   for (int i = 0; i < n; ++i) {
     const PMBound *b = (const PMBound *)bounds[i];
     if (!b) return pgmi_failf(PGM_EINVAL, "pm_merge: null bound %d", i);
+    if (b->specs.empty()) return pgmi_failf(PGM_EINVAL, "pm_merge: bound %d is a specialised contraction batch", i);
     specs.insert(specs.end(), b->specs.begin(), b->specs.end());
     ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
   }
@@ -956,3 +959,219 @@ int pgm_pm_bound_destroy(void *bound) {
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------------------------- specialised contraction batches
+// A batch of contraction jobs (one dependency level of a compiled contraction path, C1 / C2; or the
+// single-workgroup chain of its tiny last levels) as ONE generated kernel: each job's output decode
+// (literal divisors), operand strides, reduction walk (literal nested loops, the generic kernels' entry
+// order: reduction-outer dims slowest first, the innermost dim last) and lanes per output are
+// literals, and a block finds its job by comparing its index with literal ranges — no block map, no
+// descriptor loads (the generic k_batch_c reads a block map entry, then ~600 B of descriptor, before
+// its first operand load; k_batch_wg_c reads its descriptors field by field from LDS).
+
+static std::string cs_combine(int cmb, const std::string &a, const std::string &b) {
+  switch (cmb) {
+    case PGM_COMBINE_MUL: return "(" + a + " * " + b + ")";
+    case PGM_COMBINE_ADD: return "(" + a + " + " + b + ")";
+    case PGM_COMBINE_DIV: return "pgm_div0(" + a + ", " + b + ")";
+    case PGM_COMBINE_DIV_RAW: return "(" + a + " / " + b + ")";
+    default: return a;  // COPY
+  }
+}
+
+static std::string cs_red(int red, const std::string &acc, const std::string &v) {
+  if (red == PGM_RED_SUM) return acc + " = " + acc + " + " + v + ";";
+  if (red == PGM_RED_MAX) return acc + " = pgm_maxn(" + acc + ", " + v + ");";
+  return acc + " = " + v + ";";
+}
+
+// the job's output index decode: oa / ob / oc from idx (the kept dims, the last one fastest)
+static void cs_decode(std::string &o, const ContractK &k, int nk, bool use_b, const char *ind) {
+  for (int i = nk - 1; i >= 0; --i) {
+    const unsigned d = k.kdiv[i].d;
+    if (i == 0)
+      pgmi_appendf(o, "%s{ const unsigned g_ = idx;", ind);
+    else
+      pgmi_appendf(o, "%s{ const unsigned q_ = idx / %uu, g_ = idx - q_ * %uu; idx = q_;", ind, d, d);
+    if (k.ksa[i]) pgmi_appendf(o, " oa += (long long)g_ * %lldLL;", (long long)k.ksa[i]);
+    if (use_b && k.ksb[i]) pgmi_appendf(o, " ob += (long long)g_ * %lldLL;", (long long)k.ksb[i]);
+    if (k.ksc[i]) pgmi_appendf(o, " oc += (long long)g_ * %lldLL;", (long long)k.ksc[i]);
+    o += " }\n";
+  }
+}
+
+// nested loops over the reduction-outer dims (dim 0 outermost) opening; returns the offset expressions
+static void cs_red_loops_open(std::string &o, const ContractK &k, std::string &ind, uint64_t inner_trip) {
+  uint64_t prod = inner_trip;
+  int first_unrolled = k.nr - 1;
+  for (int r = k.nr - 2; r >= 0; --r) {
+    prod *= k.rdiv[r].d;
+    if (prod > 16) break;
+    first_unrolled = r;
+  }
+  for (int r = 0; r < k.nr - 1; ++r) {
+    pgmi_appendf(o, "%s#pragma unroll%s\n", ind.c_str(), r >= first_unrolled ? "" : " 1");
+    pgmi_appendf(o, "%sfor (unsigned r%d = 0; r%d < %uu; ++r%d) {\n", ind.c_str(), r, r, k.rdiv[r].d, r);
+    ind += "  ";
+  }
+}
+
+static void cs_red_loops_close(std::string &o, const ContractK &k, std::string &ind) {
+  for (int r = 0; r < k.nr - 1; ++r) {
+    ind.resize(ind.size() - 2);
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+  }
+}
+
+static std::string cs_ro_off(const ContractK &k, bool a) {
+  std::string e = "0LL";
+  for (int r = 0; r < k.nr - 1; ++r) {
+    const long long s = a ? (long long)k.rsa[r] : (long long)k.rsb[r];
+    if (s) e += " + (long long)r" + std::to_string(r) + " * " + std::to_string(s) + "LL";
+  }
+  return e;
+}
+
+static std::string cs_job_body(const pgmi_cs_job &J, const std::string &name) {
+  const ContractK &k = J.k;
+  const bool use_b = J.cmb != PGM_COMBINE_COPY;
+  const char *init = J.red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
+  std::string o;
+  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned tid, unsigned nth, const double *__restrict__ A, "
+                  "const double *__restrict__ B, double *__restrict__ C) {\n  (void)B;\n", name.c_str());
+  const std::string ra = cs_ro_off(k, true), rb = cs_ro_off(k, false);
+  const unsigned RI = k.ri_card;
+  if (k.row_mode == 2) {  // output pairs along the innermost kept dim, 16-B accesses (contract_flat2)
+    const int kx = k.nk - 1;
+    const bool va = k.ksa[kx] != 0, vb = use_b && k.ksb[kx] != 0;
+    pgmi_appendf(o, "  for (unsigned q = tid; q < %uu; q += nth) {\n", k.n_out >> 1);
+    o += "    unsigned idx = q << 1;\n    long long oa = 0, ob = 0, oc = 0; (void)ob;\n";
+    cs_decode(o, k, k.nk, use_b, "    ");
+    pgmi_appendf(o, "    double lo = %s, hi = %s;\n", init, init);
+    std::string ind = "    ";
+    cs_red_loops_open(o, k, ind, RI);
+    pgmi_appendf(o, "%s#pragma unroll%s\n", ind.c_str(), RI <= 16 ? "" : " 4");
+    pgmi_appendf(o, "%sfor (unsigned ri = 0; ri < %uu; ++ri) {\n", ind.c_str(), RI);
+    const std::string in = ind + "  ";
+    pgmi_appendf(o, "%sconst double *a_ = A + oa + %s + (long long)ri * %lldLL;\n", in.c_str(), ra.c_str(), (long long)k.ri_sa);
+    if (va) pgmi_appendf(o, "%sconst pgm_d2 xa = *(const pgm_d2 *)a_;\n", in.c_str());
+    else pgmi_appendf(o, "%sconst double xs_ = *a_; const pgm_d2 xa = {xs_, xs_};\n", in.c_str());
+    if (use_b) {
+      pgmi_appendf(o, "%sconst double *b_ = B + ob + %s + (long long)ri * %lldLL;\n", in.c_str(), rb.c_str(), (long long)k.ri_sb);
+      if (vb) pgmi_appendf(o, "%sconst pgm_d2 xb = *(const pgm_d2 *)b_;\n", in.c_str());
+      else pgmi_appendf(o, "%sconst double ys_ = *b_; const pgm_d2 xb = {ys_, ys_};\n", in.c_str());
+    }
+    pgmi_appendf(o, "%s%s\n", in.c_str(), cs_red(J.red, "lo", cs_combine(J.cmb, "xa.x", "xb.x")).c_str());
+    pgmi_appendf(o, "%s%s\n", in.c_str(), cs_red(J.red, "hi", cs_combine(J.cmb, "xa.y", "xb.y")).c_str());
+    pgmi_appendf(o, "%s}\n", ind.c_str());
+    cs_red_loops_close(o, k, ind);
+    o += "    *(pgm_d2 *)(C + oc) = (pgm_d2){lo, hi};\n  }\n}\n";
+    return o;
+  }
+  const unsigned G = 1u << k.g_log2;
+  if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
+  pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  o += "    unsigned idx = out;\n    long long oa = 0, ob = 0, oc = 0; (void)ob;\n";
+  cs_decode(o, k, k.nk, use_b, "    ");
+  pgmi_appendf(o, "    double acc = %s;\n", init);
+  std::string ind = "    ";
+  cs_red_loops_open(o, k, ind, G > 1 ? (RI + G - 1) / G : RI);
+  if (G > 1) {
+    pgmi_appendf(o, "%sfor (unsigned ri = lane_g; ri < %uu; ri += %uu) {\n", ind.c_str(), RI, G);
+  } else {
+    pgmi_appendf(o, "%s#pragma unroll%s\n", ind.c_str(), RI <= 16 ? "" : " 8");
+    pgmi_appendf(o, "%sfor (unsigned ri = 0; ri < %uu; ++ri) {\n", ind.c_str(), RI);
+  }
+  const std::string in = ind + "  ";
+  std::string va = "A[oa + " + ra + " + (long long)ri * " + std::to_string((long long)k.ri_sa) + "LL]";
+  std::string vb = "B[ob + " + rb + " + (long long)ri * " + std::to_string((long long)k.ri_sb) + "LL]";
+  pgmi_appendf(o, "%s%s\n", in.c_str(), cs_red(J.red, "acc", cs_combine(J.cmb, va, vb)).c_str());
+  pgmi_appendf(o, "%s}\n", ind.c_str());
+  cs_red_loops_close(o, k, ind);
+  if (G > 1 && J.red != PGM_RED_NONE)
+    for (unsigned off = G >> 1; off > 0; off >>= 1)
+      pgmi_appendf(o, "    %s\n", cs_red(J.red, "acc", "__shfl_xor(acc, " + std::to_string(off) + ", 64)").c_str());
+  pgmi_appendf(o, "    %sC[oc] = acc;\n  }\n}\n", G > 1 ? "if (lane_g == 0) " : "");
+  return o;
+}
+
+int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int n_levels, int one_wg, void **bound) {
+  *bound = nullptr;
+  static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
+  // (a block finds its job through a balanced tree of literal comparisons: with a linear chain the
+  // 130 / 87 / 64-job C2 levels ran 3-4x slower than the generic kernel; with the tree every level is
+  // faster specialised, r05i: C2 0.148 ms/query with 24 jobs at most per specialised level, 0.129 with
+  // no limit but the kernel-argument budget of 170 jobs)
+  if (no_jit || n < 1 || 3 * n > (int)kPmMaxArgPtrs) return PGM_OK;
+  for (int j = 0; j < n; ++j) {
+    const ContractK &k = jobs[j].k;
+    if (k.n_split != 1 || (k.row_mode != 0 && k.row_mode != 2) || k.nk < 1 || k.nk > KMAX || k.nr > KMAX)
+      return PGM_OK;
+  }
+  std::string o =
+      "#pragma clang fp contract(off)\n"  // products rounded before they are summed, as numpy does
+      "typedef double pgm_d2 __attribute__((ext_vector_type(2)));\n"
+      "__device__ __forceinline__ double pgm_div0(double a, double b) { const double r = a / b; "
+      "return r != r ? 0.0 : r; }\n"
+      "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
+  for (int j = 0; j < n; ++j) o += cs_job_body(jobs[j], "cj" + std::to_string(j));
+  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", 3 * n);
+  // jobs [j0, j1) by block b: a balanced tree of literal comparisons (the jobs' block ranges ascend)
+  std::function<void(std::string &, int, int, std::string)> dispatch = [&](std::string &s, int j0, int j1,
+                                                                            std::string ind) {
+    if (j1 - j0 == 1) {
+      const pgmi_cs_job &J = jobs[j0];
+      pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], a.p[%d], (double *)a.p[%d]);\n", ind.c_str(), j0,
+                   J.block0, J.nblocks * 256u, 3 * j0, 3 * j0 + 1, 3 * j0 + 2);
+      return;
+    }
+    const int m = (j0 + j1) / 2;
+    pgmi_appendf(s, "%sif (b < %uu) {\n", ind.c_str(), jobs[m].block0);
+    dispatch(s, j0, m, ind + "  ");
+    pgmi_appendf(s, "%s} else {\n", ind.c_str());
+    dispatch(s, m, j1, ind + "  ");
+    pgmi_appendf(s, "%s}\n", ind.c_str());
+  };
+  unsigned blocks = 0, threads = 256;
+  if (!one_wg) {
+    uint64_t nb = 0;
+    for (int j = 0; j < n; ++j) nb = std::max<uint64_t>(nb, (uint64_t)jobs[j].block0 + jobs[j].nblocks);
+    if (nb == 0 || nb >= (1ull << 31)) return PGM_OK;
+    blocks = (unsigned)nb;
+    o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const pgm_pm_args a) {\n"
+         "  const unsigned b = blockIdx.x, lt = threadIdx.x;\n";
+    dispatch(o, 0, n, "  ");
+    o += "}\n";
+  } else {
+    // one 1,024-thread workgroup: each level's blocks four at a time (virtual 256-thread blocks), a
+    // workgroup barrier after each level (the next level reads what this workgroup wrote)
+    blocks = 1;
+    threads = 1024;
+    o += "extern \"C\" __global__ void __launch_bounds__(1024) pgm_pm(const pgm_pm_args a) {\n"
+         "  const unsigned vb = threadIdx.x / 256u, lt = threadIdx.x % 256u;\n";
+    int j = 0;
+    for (int l = 0; l < n_levels; ++l) {
+      const uint32_t b0 = level_off[l], b1 = level_off[l + 1];
+      int j1 = j;
+      while (j1 < n && jobs[j1].block0 < b1) ++j1;
+      pgmi_appendf(o, "  for (unsigned b = %uu + vb; b < %uu; b += 4u) {\n", b0, b1);
+      if (j1 > j) dispatch(o, j, j1, "    ");
+      o += "  }\n  __syncthreads();\n";
+      j = j1;
+    }
+    if (j != n) return PGM_OK;  // jobs outside the level table: not a shape this form takes
+    o += "}\n";
+  }
+  PMBound *b = new (std::nothrow) PMBound;
+  if (!b) return pgmi_failf(PGM_ENOMEM, "batch_specialise: out of host memory");
+  b->src = o;
+  b->blocks = blocks;
+  b->threads = threads;
+  for (int q = 0; q < n; ++q) {
+    b->ptrs.push_back(jobs[q].A);
+    b->ptrs.push_back(jobs[q].B);
+    b->ptrs.push_back(jobs[q].C);
+  }
+  *bound = b;
+  return PGM_OK;
+}

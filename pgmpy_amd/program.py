@@ -7,6 +7,7 @@ them into a HIP graph (pgm_graph_capture_*) so a whole compiled schedule — a
 batched BP calibration, a fixed-shape contraction plan — is one launch.
 """
 import ctypes
+import os
 
 from . import _native as N
 from . import engine as E
@@ -38,6 +39,10 @@ PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
 # (r03's persistent grid-barrier form of several levels and its one-block-at-a-time generic chain were
 # measured slower and removed in r05.)
 WG_CHAIN_BLOCKS = 4
+# plain programs: every level batch of contractions (and the single-workgroup chain) runs as ONE
+# plan-specialised kernel (pgm_batch_specialise) instead of the descriptor-driven k_batch_c /
+# k_batch_wg_c (r05).  A/B knob PGM_BATCH_RTC=0
+BATCH_SPECIALISE = os.environ.get("PGM_BATCH_RTC", "1") != "0"
 
 
 def _key(t):
@@ -86,6 +91,7 @@ class Program:
         self._batch = None
         self._handles = []
         self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
+        self._pm_prepared = 0  # plain Program: _pm_bound[:n] compiled by _ready
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
         self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
@@ -148,16 +154,33 @@ class Program:
         finally:
             L.pgm_batch_destroy(h)
 
+    def _specialise(self, h):
+        """The finalized batch h as one plan-specialised kernel (pgm_batch_specialise: literal shapes,
+        strides and block ranges, no descriptor reads), or None when it does not take the batch."""
+        if not BATCH_SPECIALISE:
+            return None
+        b = ctypes.c_void_p()
+        N.check(N.lib().pgm_batch_specialise(h, ctypes.byref(b)), "batch_specialise")
+        if not b.value:
+            return None
+        self._pm_bound.append(b)
+        return b
+
     def _batch_step(self, b):
         L = N.lib()
-        if len(b.jobs) == 1:  # a batch of one is just the job (its own planner's launch)
-            kind, _, args = b.jobs[0]
-            if kind == "contract":
-                return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), f"{kind} (batch of one)"
-            return (lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather")), f"{kind} (batch of one)"
+        if len(b.jobs) == 1 and b.jobs[0][0] != "contract":  # one gather: its own planner's launch
+            args = b.jobs[0][2]
+            return (lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather")), "gather (batch of one)"
         h = self._new_batch()
         self._add_batch_jobs(h, b.jobs)
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
+        sb = self._specialise(h)
+        if sb is not None:
+            return ((lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run")),
+                    f"specialised batch of {len(b.jobs)}")
+        if len(b.jobs) == 1:  # a contraction the generator does not take: its own planner's launch
+            args = b.jobs[0][2]
+            return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), "contract (batch of one)"
         return (lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")), f"batch of {len(b.jobs)}"
 
     def _chain_batch(self, group):
@@ -211,7 +234,11 @@ class Program:
                     if e - k >= 2:
                         h = self._chain_batch(group[k:e])
                         if h is not None:
-                            steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+                            sb = self._specialise(h)
+                            if sb is not None:
+                                steps.append(lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run"))
+                            else:
+                                steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
                             notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
                                          f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
                             k = e
@@ -275,8 +302,9 @@ class Program:
         """Lower, then compile every specialised kernel the steps launch (in parallel, before any
         run or capture)."""
         self._lower()
-        if self._pm_launch is None:
-            self._pm_launch = list(self._pm_bound)  # plain Program: every bound step is launched
+        if self._pm_launch is None or not self._levels:  # plain Program: every bound step not yet prepared
+            self._pm_launch = self._pm_bound[self._pm_prepared:]
+            self._pm_prepared = len(self._pm_bound)
         if self._pm_launch:
             arr = (ctypes.c_void_p * len(self._pm_launch))(*[h.value for h in self._pm_launch])
             N.check(N.lib().pgm_pm_prepare(arr, len(self._pm_launch)), "pm_prepare")
