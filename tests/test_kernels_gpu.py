@@ -882,3 +882,49 @@ def test_two_marginals_one_pass(gpu, rows, red, ratio):
     np.testing.assert_allclose(E.to_host(Ms[1]), f(full, axis=(0, 1)), rtol=1e-13)
 
 
+
+
+@pytest.mark.parametrize("spec", [True, False])
+def test_specialised_contraction_batch_matches_numpy(gpu, monkeypatch, spec):
+    """A plain Program's level batch of contractions through the plan-specialised kernel
+    (pgm_batch_specialise, r05) and through the generic k_batch_c: one-lane-per-output jobs, lanes
+    per output on a long reduction, output pairs with 16-B accesses, every combine (mul / add / div
+    with 0/0 -> 0 / div_raw / copy) and reduce (sum / max / none) — each equals numpy, rtol 1e-12."""
+    import pgmpy_amd.program as P
+    from pgmpy_amd.program import Program
+
+    monkeypatch.setattr(P, "BATCH_SPECIALISE", spec)
+    E = _e()
+    rng = np.random.default_rng(21)
+    A1, B1 = rng.random((7, 5, 6)), rng.random((6, 9))
+    A2, B2 = rng.random((3, 2000)), rng.random((2000,))
+    A3, B3 = rng.random((4, 5, 8)), rng.random((4, 8))
+    A4, B4 = rng.random((6, 64)), rng.random((6,))
+    A5, B5 = rng.random((5, 6, 4)), rng.random((6, 4))
+    A5[0, :3, :] = 0.0
+    B5[:2, :] = 0.0
+    A6 = rng.random((3, 4, 5, 2))
+    A7, B7 = rng.random((8, 16)), rng.random((16,)) + 0.5
+    prog = Program()
+    prog.begin_batch()
+    o1 = prog.contract(E.to_device(A1), ["a", "b", "r"], E.to_device(B1), ["r", "c"], ["a", "b", "c"], reduce="sum")
+    o2 = prog.contract(E.to_device(A2), ["a", "r"], E.to_device(B2), ["r"], ["a"], reduce="sum")
+    o3 = prog.contract(E.to_device(A3), ["a", "r", "x"], E.to_device(B3), ["a", "x"], ["a", "x"], reduce="max",
+                       combine="add")
+    o4 = prog.contract(E.to_device(A4), ["a", "x"], E.to_device(B4), ["a"], ["a", "x"], combine="mul")
+    o5 = prog.contract(E.to_device(A5), ["q", "a", "x"], E.to_device(B5), ["a", "x"], ["q", "a", "x"], combine="div")
+    o6 = prog.contract(E.to_device(A6), ["a", "b", "c", "d"], None, None, ["d", "b"], reduce="sum", combine="copy")
+    o7 = prog.contract(E.to_device(A7), ["a", "x"], E.to_device(B7), ["x"], ["x", "a"], combine="div_raw")
+    prog.end_batch()
+    prog.run()
+    import torch
+
+    torch.cuda.synchronize()
+    assert any(("specialised" in n) == spec for n in prog.notes), prog.notes
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r5 = A5 / B5[None]
+    r5[np.isnan(r5)] = 0.0
+    checks = [(o1, np.einsum("abr,rc->abc", A1, B1)), (o2, A2 @ B2), (o3, (A3 + B3[:, None, :]).max(axis=1)),
+              (o4, A4 * B4[:, None]), (o5, r5), (o6, A6.sum(axis=(0, 2)).T), (o7, (A7 / B7[None]).T)]
+    for got, want in checks:
+        np.testing.assert_allclose(E.to_host(got), want, rtol=1e-12, atol=0)
