@@ -54,14 +54,28 @@ struct ContractK {
   int64_t rsa[KMAX], rsb[KMAX];
 };
 
-// one contraction job of a batch (pgm_batch_*) as the specialiser sees it: blocks [block0, block0 +
-// nblocks) of the batch's 256-thread blocks, C[keep] = reduce(combine(A, B))
+// a planned per-row evidence gather (pgm_gather: C[out] = A[out's offset + sum of codes x strides])
+struct GatherK {
+  int32_t nk, n_ev, batch_dim, _pad;
+  uint32_t n_out, _pad2;
+  int64_t ld, row0;
+  FDiv kdiv[KMAX];
+  int64_t ksa[KMAX], ksc[KMAX];
+  int64_t ev_col[PGM_MAX_DIMS], ev_stride[PGM_MAX_DIMS];
+  int32_t ev_card[PGM_MAX_DIMS];
+};
+
+// one job of a batch (pgm_batch_*) as the specialiser sees it: blocks [block0, block0 + nblocks) of
+// the batch's 256-thread blocks; kind 0: C[keep] = reduce(combine(A, B)) (k), 1: an evidence gather (g)
 struct pgmi_cs_job {
-  int32_t cmb, red;
+  int32_t kind, cmb, red;
   uint32_t block0, nblocks;
   const double *A, *B;
   double *C;
+  const uint8_t *codes;
+  int32_t *err;
   ContractK k;
+  GatherK g;
 };
 
 // a plan-specialised kernel for a batch of contraction jobs (pgmpm.cpp): one_wg = 0: one launch of

@@ -1224,15 +1224,7 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
 }
 
 // ----------------------------------------------------------------------------- gather
-struct GatherK {
-  int32_t nk, n_ev, batch_dim, _pad;
-  uint32_t n_out, _pad2;
-  int64_t ld, row0;
-  FDiv kdiv[KMAX];
-  int64_t ksa[KMAX], ksc[KMAX];
-  int64_t ev_col[PGM_MAX_DIMS], ev_stride[PGM_MAX_DIMS];
-  int32_t ev_card[PGM_MAX_DIMS];
-};
+// GatherK (a planned per-row evidence gather): pgm_internal.h
 
 __device__ __forceinline__ void gather_body(const GatherK &p, const double *__restrict__ A,
                                             const uint8_t *__restrict__ codes, double *__restrict__ C,
@@ -3684,8 +3676,10 @@ int pgm_batch_specialise(void *handle, void **bound) {
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_specialise: not finalized");
   std::vector<pgmi_cs_job> jobs;
   for (const BatchJob &J : h->jobs) {
-    if (J.kind != 0 || J.c.n_split != 1) return PGM_OK;  // contractions only (no split-K partials)
+    if (J.kind > 1 || (J.kind == 0 && J.c.n_split != 1)) return PGM_OK;  // contractions and gathers only
     pgmi_cs_job c;
+    memset(&c, 0, sizeof c);
+    c.kind = J.kind;
     c.cmb = J.cmb;
     c.red = J.red;
     c.block0 = J.block0;
@@ -3693,7 +3687,10 @@ int pgm_batch_specialise(void *handle, void **bound) {
     c.A = J.A;
     c.B = J.B;
     c.C = J.C;
-    c.k = J.c;
+    c.codes = J.codes;
+    c.err = J.err;
+    if (J.kind == 0) c.k = J.c;
+    else c.g = J.g;
     jobs.push_back(c);
   }
   if (jobs.empty()) return PGM_OK;

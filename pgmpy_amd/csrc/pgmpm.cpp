@@ -1095,6 +1095,36 @@ static std::string cs_job_body(const pgmi_cs_job &J, const std::string &name) {
   return o;
 }
 
+// an evidence gather job (gather_body): C[out] = A[kept offset + sum_j code_j x stride_j], a code out of its
+// variable's range raises the error flag and reads state 0
+static std::string cs_gather_body(const pgmi_cs_job &J, const std::string &name) {
+  const GatherK &g = J.g;
+  std::string o;
+  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned tid, unsigned nth, const double *__restrict__ A, "
+                  "const unsigned char *__restrict__ K, double *__restrict__ C, int *__restrict__ E) {\n"
+                  "  (void)K; (void)E;\n", name.c_str());
+  pgmi_appendf(o, "  for (unsigned out = tid; out < %uu; out += nth) {\n", g.n_out);
+  o += "    unsigned idx = out, row = 0;\n    long long oa = 0, oc = 0;\n    (void)row;\n";
+  for (int i = g.nk - 1; i >= 0; --i) {
+    const unsigned d = g.kdiv[i].d;
+    if (i == 0) o += "    { const unsigned g_ = idx;";
+    else pgmi_appendf(o, "    { const unsigned q_ = idx / %uu, g_ = idx - q_ * %uu; idx = q_;", d, d);
+    if (g.ksa[i]) pgmi_appendf(o, " oa += (long long)g_ * %lldLL;", (long long)g.ksa[i]);
+    if (g.ksc[i]) pgmi_appendf(o, " oc += (long long)g_ * %lldLL;", (long long)g.ksc[i]);
+    if (i == g.batch_dim) o += " row = g_;";
+    o += " }\n";
+  }
+  for (int j = 0; j < g.n_ev; ++j) {
+    pgmi_appendf(o, "    { unsigned c_ = K[%lldLL + (long long)row];", (long long)(g.ev_col[j] * g.ld + g.row0));
+    pgmi_appendf(o, " if (c_ >= %uu) { if (E) atomicOr(E, 1); c_ = 0; }", (unsigned)g.ev_card[j]);
+    pgmi_appendf(o, " oa += (long long)c_ * %lldLL; }\n", (long long)g.ev_stride[j]);
+  }
+  o += "    C[oc] = A[oa];\n  }\n}\n";
+  return o;
+}
+
+static int cs_nptrs(const pgmi_cs_job &J) { return J.kind == 1 ? 4 : 3; }
+
 int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int n_levels, int one_wg, void **bound) {
   *bound = nullptr;
   static const bool no_jit = getenv("PGM_NO_JIT") != nullptr;
@@ -1102,8 +1132,15 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
   // 130 / 87 / 64-job C2 levels ran 3-4x slower than the generic kernel; with the tree every level is
   // faster specialised, r05i: C2 0.148 ms/query with 24 jobs at most per specialised level, 0.129 with
   // no limit but the kernel-argument budget of 170 jobs)
-  if (no_jit || n < 1 || 3 * n > (int)kPmMaxArgPtrs) return PGM_OK;
+  std::vector<int> base(n + 1, 0);
+  for (int j = 0; j < n; ++j) base[j + 1] = base[j] + cs_nptrs(jobs[j]);
+  if (no_jit || n < 1 || base[n] > (int)kPmMaxArgPtrs) return PGM_OK;
   for (int j = 0; j < n; ++j) {
+    if (jobs[j].kind == 1) {
+      const GatherK &g = jobs[j].g;
+      if (g.nk < 1 || g.nk > KMAX || g.n_ev < 0 || g.n_ev > PGM_MAX_DIMS) return PGM_OK;
+      continue;
+    }
     const ContractK &k = jobs[j].k;
     if (k.n_split != 1 || (k.row_mode != 0 && k.row_mode != 2) || k.nk < 1 || k.nk > KMAX || k.nr > KMAX)
       return PGM_OK;
@@ -1114,15 +1151,21 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
       "__device__ __forceinline__ double pgm_div0(double a, double b) { const double r = a / b; "
       "return r != r ? 0.0 : r; }\n"
       "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
-  for (int j = 0; j < n; ++j) o += cs_job_body(jobs[j], "cj" + std::to_string(j));
-  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", 3 * n);
+  for (int j = 0; j < n; ++j)
+    o += jobs[j].kind == 1 ? cs_gather_body(jobs[j], "cj" + std::to_string(j)) : cs_job_body(jobs[j], "cj" + std::to_string(j));
+  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", base[n]);
   // jobs [j0, j1) by block b: a balanced tree of literal comparisons (the jobs' block ranges ascend)
   std::function<void(std::string &, int, int, std::string)> dispatch = [&](std::string &s, int j0, int j1,
                                                                             std::string ind) {
     if (j1 - j0 == 1) {
       const pgmi_cs_job &J = jobs[j0];
-      pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], a.p[%d], (double *)a.p[%d]);\n", ind.c_str(), j0,
-                   J.block0, J.nblocks * 256u, 3 * j0, 3 * j0 + 1, 3 * j0 + 2);
+      const int p0 = base[j0];
+      if (J.kind == 1)
+        pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], (const unsigned char *)a.p[%d], (double *)a.p[%d], "
+                        "(int *)a.p[%d]);\n", ind.c_str(), j0, J.block0, J.nblocks * 256u, p0, p0 + 1, p0 + 2, p0 + 3);
+      else
+        pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], a.p[%d], (double *)a.p[%d]);\n", ind.c_str(), j0,
+                     J.block0, J.nblocks * 256u, p0, p0 + 1, p0 + 2);
       return;
     }
     const int m = (j0 + j1) / 2;
@@ -1169,8 +1212,14 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
   b->threads = threads;
   for (int q = 0; q < n; ++q) {
     b->ptrs.push_back(jobs[q].A);
-    b->ptrs.push_back(jobs[q].B);
-    b->ptrs.push_back(jobs[q].C);
+    if (jobs[q].kind == 1) {
+      b->ptrs.push_back((const double *)jobs[q].codes);
+      b->ptrs.push_back(jobs[q].C);
+      b->ptrs.push_back((const double *)jobs[q].err);
+    } else {
+      b->ptrs.push_back(jobs[q].B);
+      b->ptrs.push_back(jobs[q].C);
+    }
   }
   *bound = b;
   return PGM_OK;

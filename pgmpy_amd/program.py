@@ -168,9 +168,6 @@ class Program:
 
     def _batch_step(self, b):
         L = N.lib()
-        if len(b.jobs) == 1 and b.jobs[0][0] != "contract":  # one gather: its own planner's launch
-            args = b.jobs[0][2]
-            return (lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather")), "gather (batch of one)"
         h = self._new_batch()
         self._add_batch_jobs(h, b.jobs)
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
@@ -178,9 +175,11 @@ class Program:
         if sb is not None:
             return ((lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run")),
                     f"specialised batch of {len(b.jobs)}")
-        if len(b.jobs) == 1:  # a contraction the generator does not take: its own planner's launch
-            args = b.jobs[0][2]
-            return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), "contract (batch of one)"
+        if len(b.jobs) == 1:  # a job the generator does not take: its own planner's launch
+            kind, _, args = b.jobs[0]
+            if kind == "contract":
+                return (lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract")), "contract (batch of one)"
+            return (lambda s, a=args: N.check(L.pgm_gather(*a, s), "gather")), "gather (batch of one)"
         return (lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")), f"batch of {len(b.jobs)}"
 
     def _chain_batch(self, group):
