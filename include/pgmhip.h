@@ -124,7 +124,12 @@ int pgm_contract(const pgm_contract_desc *d, const double *A, const double *B, d
 enum pgm_prodn_kind {
   PGM_PRODN_MUL = 0,   /* prod *= X_i                                                    */
   PGM_PRODN_RATIO = 1, /* prod *= X_i / X_{i+1}, NaN -> 0 (sepset update sigma / mu,     */
-  PGM_PRODN_DEN = 2    /*   ExactInference.py:798-802 + DiscreteFactor.py:859-863)       */
+  PGM_PRODN_DEN = 2,   /*   ExactInference.py:798-802 + DiscreteFactor.py:859-863)       */
+  PGM_PRODN_MDIV = 3   /* pgm_product_n_marginal only: prod *= X_i like MUL, and the marginal M is
+                          stored divided by X_i (0/0 -> 0) — X_i must not vary over the entries M sums
+                          (a child's message mu on its separator: M = sigma' / mu, the child's update
+                          ratio, ExactInference.py:798-802).  At most one per call; other calls:
+                          PGM_EINVAL */
 };
 typedef struct {
   int32_t n_ops;

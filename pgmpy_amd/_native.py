@@ -66,7 +66,7 @@ PRODN_MAX_OPS = 8
 PM_MAX_OPS = 8  # operands of a fused product + marginal step (pgm_internal.h MOPS)
 
 
-PRODN_MUL, PRODN_RATIO, PRODN_DEN = 0, 1, 2
+PRODN_MUL, PRODN_RATIO, PRODN_DEN, PRODN_MDIV = 0, 1, 2, 3
 
 
 class ProductNDesc(ctypes.Structure):

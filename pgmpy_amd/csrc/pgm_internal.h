@@ -87,6 +87,7 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
 // pgmpm.cpp compiles it into specialised kernels)
 struct ProdMK {
   int32_t n_ops, nk, nr, n_red;  // nk: kept outer dims + the row dim (last); nr: reduced dims
+  int32_t mdiv;                  // >= 0: the marginal is stored divided by this operand (0/0 -> 0; PGM_PRODN_MDIV)
   int32_t kind[MOPS];
   int32_t vec[MOPS];             // operand has the row axis (stride 1) / is broadcast over rows
   int32_t jvar[MOPS];            // operand varies over the reduced entries (else loaded once per outer)

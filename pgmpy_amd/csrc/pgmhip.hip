@@ -1106,8 +1106,17 @@ __global__ __launch_bounds__(256) void k_productn_marg_jx(const ProdMK p, double
       }
     }
 #pragma unroll
-    for (int u = 0; u < XI; ++u)
+    for (int u = 0; u < XI; ++u) {
+      if (p.mdiv >= 0) {  // the marginal over the operand that does not vary over the summed entries
+        double2 dv = h[u][0];
+#pragma unroll
+        for (int i = 1; i < NOPS; ++i)
+          if (i == p.mdiv) dv = h[u][i];
+        const double rx = acc[u].x / dv.x, ry = acc[u].y / dv.y;
+        acc[u] = make_double2(rx != rx ? 0.0 : rx, ry != ry ? 0.0 : ry);
+      }
       if (x0 + 256u * u < p.NP) ((double2 *)(M + om))[x0 + 256u * u] = acc[u];
+    }
   }
 }
 
@@ -1124,12 +1133,18 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
   if (NX < 64 || NX % 2 || d->keep_sc[last] != 1 || marg_s[last] != 1) return 0;
   if (((uintptr_t)C & 15) || ((uintptr_t)M & 15)) return 0;
   k.n_ops = d->n_ops;
+  k.mdiv = -1;
   for (int t = 0; t < MOPS; ++t) {
     const bool real = t < d->n_ops;
     k.ops[t] = real ? ops[t] : ops[0];
     k.kind[t] = real ? d->op_kind[t] : PGM_PRODN_MUL;
-    if (real && (!ops[t] || d->op_kind[t] < 0 || d->op_kind[t] > 2))
+    if (real && (!ops[t] || d->op_kind[t] < 0 || d->op_kind[t] > PGM_PRODN_MDIV))
       return fail(PGM_EINVAL, "product_n_marginal: operand %d", t);
+    if (real && d->op_kind[t] == PGM_PRODN_MDIV) {  // a factor of the product, and the marginal's divisor
+      if (k.mdiv >= 0) return fail(PGM_EINVAL, "product_n_marginal: more than one PGM_PRODN_MDIV operand");
+      k.mdiv = t;
+      k.kind[t] = PGM_PRODN_MUL;
+    }
     const int64_t sx = real ? d->keep_s[t][last] : 0;
     if (sx != 0 && sx != 1) return 0;
     if (sx == 1 && ((uintptr_t)ops[t] & 15)) return 0;
@@ -1198,6 +1213,7 @@ int pgmi_plan_product_marg(const pgm_productn_desc *d, const double *const *ops,
     k.jvar[t] = 0;
     for (int r = 0; t < d->n_ops && r < k.nr; ++r) k.jvar[t] |= k.rs[t][r] != 0;
   }
+  if (k.mdiv >= 0 && k.jvar[k.mdiv]) return 0;  // the divisor varies over the summed entries: not this kernel
   k.kdiv[k.nk] = make_fdiv((uint32_t)NX);  // the row dim, last
   ++k.nk;
   k.n_red = (int32_t)n_red;

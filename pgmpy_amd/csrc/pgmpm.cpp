@@ -392,6 +392,16 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     ind.resize(ind.size() - 2);
     pgmi_appendf(o, "%s}\n", ind.c_str());
   }
+  // a marginal divided by an operand constant over the summed entries (PGM_PRODN_MDIV: sigma' / mu)
+  if (has_m && k.mdiv >= 0) {
+    const int i = k.mdiv;
+    for (int u = 0; u < XI; ++u) {
+      if (k.vec[i])
+        pgmi_appendf(o, "  a%d = (pgm_d2){pgm_ratio(a%d.x, h%d_%d.x), pgm_ratio(a%d.y, h%d_%d.y)};\n", u, u, i, u, u, i, u);
+      else
+        pgmi_appendf(o, "  a%d = (pgm_d2){pgm_ratio(a%d.x, h%d), pgm_ratio(a%d.y, h%d)};\n", u, u, i, u, i);
+    }
+  }
   // marginal stores: nontemporal when the step stores no product (a marginal-only pass writes nothing
   // else), plain (write-back L2) otherwise
   for (int u = 0; u < XI && has_m; ++u) {

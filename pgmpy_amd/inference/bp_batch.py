@@ -19,6 +19,8 @@ one HIP graph.  Algorithmic bytes per calibration: 8 (sum|C| + 4 sum|S|) — eve
 every separator message and sigma' written and read once; SURVEY.md §8(d)'s 8 (4 sum|C| + 4 sum|S|)
 counts the reference's schedule, which reads and writes each belief in both passes.
 """
+import os
+
 import numpy as np
 
 from .. import _native as N
@@ -64,6 +66,29 @@ class BatchedCalibration:
 
     def marginals_device(self):
         return dict(self._marg)
+
+
+# a clique's finalising pass stores its child's update ratio sigma'/mu instead of sigma' where it can
+# (BPSchedule.premarginal); A/B knob PGM_BP_RATIO=0
+RATIO_PREMARG = os.environ.get("PGM_BP_RATIO", "1") != "0"
+
+
+class _SepFromRatio:
+    """A sepset belief sigma' the schedule did not store: the child's update ratio r = sigma'/mu and its
+    message mu; sigma' = r x mu (exact where mu = 0: the parent's belief then holds the factor mu, so
+    sigma' = 0 = r x mu), made on first use (outside the compiled program)."""
+
+    def __init__(self, ratio, mu, sl):
+        self.ratio, self.mu, self.sl = ratio, mu, sl
+        self._t = None
+
+    def __getitem__(self, i):
+        if self._t is None:
+            self._t = E.product_n([(self.ratio, self.sl), (self.mu, self.sl)], self.sl)
+        return (self._t, self.sl[:-1])[i]
+
+    def __iter__(self):
+        return iter((self[0], self[1]))
 
 
 def _aggregate(prog, small, clique_labels, scope_size):
@@ -137,7 +162,36 @@ class BPSchedule:
             scs = {tuple(v for v in lc if v in k) for k in kids[c]}
             return max(scs, key=lambda x: (scope_size(x), len(x)))
 
-        premarg = {}  # clique -> (scope, marginal of its final belief) made in the finalising pass
+        def premarginal(c, ops, labels, out=None, kinds=None):
+            """c's finalising pass: its belief (into `out`) with the marginal onto its largest child scope S.
+            When exactly one child k has scope S, k's message mu_k is one of the pass's operands and no other
+            child scope needs sigma'(S) to be derived from, the pass stores k's update ratio sigma'(S) / mu_k
+            instead (PGM_PRODN_MDIV, 0/0 -> 0): k's own pass then reads one separator-sized operand instead of
+            sigma' and mu_k (r05).  Returns (belief, (S, marginal, k or None))."""
+            sc = largest_kid_scope(c)
+            base = list(kinds) if kinds is not None else [N.PRODN_MUL] * len(ops)
+            ks = [k for k in kids[c] if set(msgs[k][1][:-1]) == set(sc)]
+            idx = None
+            if RATIO_PREMARG and len(ks) == 1:
+                idx = next((i for i, (t_, _) in enumerate(ops) if t_ is msgs[ks[0]][0] and base[i] == N.PRODN_MUL), None)
+                other = {frozenset(msgs[q][1][:-1]) for q in kids[c]} - {frozenset(sc)}
+                for s_ in other:  # every other child scope inside S still finds a sigma' to come from
+                    if s_ <= set(sc) and not any(s_ < t_ for t_ in other):
+                        idx = None
+                if idx is not None:
+                    if out is None:
+                        out = E.empty([bjt.card[v] for v in labels] + [n_rows])
+                    mk = list(base)
+                    mk[idx] = N.PRODN_MDIV
+                    ok = E.prepare_product_n_marginal(ops, labels + [R], list(sc) + [R], out, mk)[5]
+                    if ok:
+                        bt, m, _ = prog.product_n_marginal(ops, labels + [R], list(sc) + [R], out=out, kinds=mk,
+                                                           reduce=red)
+                        return bt, (sc, m, ks[0])
+            bt, m, _ = prog.product_n_marginal(ops, labels + [R], list(sc) + [R], out=out, kinds=kinds, reduce=red)
+            return bt, (sc, m, None)
+
+        premarg = {}  # clique -> (scope, marginal of its final belief or a child's update ratio, that child)
         operands = {}  # clique -> its collect operands: [psi_c] + aggregated findings / child messages
         # collect: post-order (children before parents).  A clique's message to its parent is the
         # marginal of psi_c x aggregates computed WITHOUT writing the clique-sized product (the
@@ -173,10 +227,8 @@ class BPSchedule:
                 beliefs[c] = (bt, ls)  # the buffer distribute writes (the fallback path filled it already)
                 msgs[c] = (m, sep + [R])
             elif c in kids:
-                sc = largest_kid_scope(c)
-                bt, m, _ = prog.product_n_marginal(ops, ls + [R], list(sc) + [R], reduce=red)
+                bt, premarg[c] = premarginal(c, ops, ls)
                 beliefs[c] = (bt, ls)
-                premarg[c] = (sc, m)
             else:
                 beliefs[c] = (prog.product_n(ops, ls + [R]), ls)
         # distribute: root -> leaves; one sigma' per distinct separator scope of a parent, each
@@ -186,6 +238,31 @@ class BPSchedule:
         # child-scope marginal in the same pass — the reference's beta_c *= sigma'/mu
         # (ExactInference.py:798-802) on a belief that was never materialised before.
         final = {bjt.root: (operands[bjt.root], None)}  # clique -> (operands, kinds) its belief is the product of
+
+        def finalise(p, c, sigma=None, ratio=None):
+            """c's final belief psi_c x operands x sigma'/mu_c in one pass (with its own premarginal when it
+            has children); `ratio` = sigma'/mu_c already made by the parent's pass."""
+            tc, lc = beliefs[c]
+            mu, sl = msgs[c]
+            if ratio is not None and len(operands[c]) + 1 <= N.PM_MAX_OPS:
+                ops_c = operands[c] + [(ratio, sl)]
+                kinds = None
+            elif ratio is not None:  # folded into the aggregates
+                ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(ratio, sl)], lc, scope_size)
+                kinds = None
+            elif len(operands[c]) + 2 <= N.PM_MAX_OPS:  # sigma' / mu as a ratio operand pair (0/0 -> 0)
+                ops_c = operands[c] + [(sigma, sl), (mu, sl)]
+                kinds = [N.PRODN_MUL] * len(operands[c]) + [N.PRODN_RATIO, N.PRODN_DEN]
+            else:  # the separator-sized ratio folded into the aggregates
+                r_ = prog.product_n([(sigma, sl), (mu, sl)], sl, kinds=[N.PRODN_RATIO, N.PRODN_DEN])
+                ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(r_, sl)], lc, scope_size)
+                kinds = None
+            final[c] = (ops_c, kinds)
+            if c in kids:
+                _, premarg[c] = premarginal(c, ops_c, lc, out=tc, kinds=kinds)
+            else:
+                prog.product_n(ops_c, lc + [R], out=tc, kinds=kinds)
+            seps[(p, c)] = (sigma, sl[:-1]) if ratio is None else _SepFromRatio(ratio, mu, sl)
         for p in [bjt.root] + [c for _, c in bjt.order]:
             if p not in kids:
                 continue
@@ -194,11 +271,16 @@ class BPSchedule:
             for c in kids[p]:
                 scopes.setdefault(tuple(msgs[c][1][:-1]), []).append(c)
             have = {tuple(lp): tp}
+            ratio_kid = None
             if p in premarg:
-                sc0, m0 = premarg[p]
-                have[tuple(sc0)] = m0
+                sc0, m0, ratio_kid = premarg[p]
+                if ratio_kid is None:
+                    have[tuple(sc0)] = m0
             ordered = sorted(scopes, key=lambda x: -scope_size(x))
             for si, sc in enumerate(ordered):
+                if ratio_kid is not None and scopes[sc] == [ratio_kid]:
+                    finalise(p, ratio_kid, ratio=premarg[p][1])
+                    continue
                 if sc in have:
                     sigma = have[sc]
                 else:
@@ -226,24 +308,7 @@ class BPSchedule:
                                               combine="copy")
                     have[sc] = sigma
                 for c in scopes[sc]:
-                    tc, lc = beliefs[c]
-                    mu, sl = msgs[c]
-                    if len(operands[c]) + 2 <= N.PM_MAX_OPS:  # sigma' / mu as a ratio operand pair (0/0 -> 0)
-                        ops_c = operands[c] + [(sigma, sl), (mu, sl)]
-                        kinds = [N.PRODN_MUL] * len(operands[c]) + [N.PRODN_RATIO, N.PRODN_DEN]
-                    else:  # the separator-sized ratio folded into the aggregates
-                        ratio = prog.product_n([(sigma, sl), (mu, sl)], sl, kinds=[N.PRODN_RATIO, N.PRODN_DEN])
-                        ops_c = [operands[c][0]] + _aggregate(prog, operands[c][1:] + [(ratio, sl)], lc, scope_size)
-                        kinds = None
-                    final[c] = (ops_c, kinds)
-                    if c in kids:
-                        sc_c = largest_kid_scope(c)
-                        _, m, _ = prog.product_n_marginal(ops_c, lc + [R], list(sc_c) + [R], out=tc, kinds=kinds,
-                                                          reduce=red)
-                        premarg[c] = (sc_c, m)
-                    else:
-                        prog.product_n(ops_c, lc + [R], out=tc, kinds=kinds)
-                    seps[(p, c)] = (sigma, sl[:-1])
+                    finalise(p, c, sigma=sigma)
         marg = {}
         if marginals:
             for var in bjt.variables:
