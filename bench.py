@@ -1330,6 +1330,7 @@ def bench_c2(args):
     return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
             "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
             "plan": {"kind": plan.kind, **ps},
+            "chain_tuning": [getattr(h[0], "chain_tuning", None) for h in plan.__dict__.get("_progs", {}).values()],
             "achieved": {"GB/s": ps["bytes"] / dt / 1e9, "TFLOP/s": ps["flops"] / dt / 1e12,
                          "note": "algorithmic bytes / flops of the executed plan (contraction.choose_path; SURVEY §8(d) C2) per query"},
             "reference": {"value": 52.7, "unit": "s/query", "note": "pgmpy numpy path, survey container (not this host)"},
@@ -1374,8 +1375,13 @@ def bench_c1(args):
             r = ve.query(q, e, show_progress=False)
     torch.cuda.synchronize()
     warm = (time.perf_counter() - t0) / (reps * len(pats))
+    tuned = [getattr(h[0], "chain_tuning", None) for rn in ve._compiled.values()
+             for h in rn.plan.__dict__.get("_progs", {}).values()]
+    tuned = [t for t in tuned if t]
     out = {"metric": "alarm single-row query latency (C1)", "value": warm, "unit": "s/query",
            "higher_is_better": False, "patterns": len(pats), "first_query_s": cold,
+           "chain_tuning": {"programs": len(tuned),
+                            "kept_chain": sum(t["chained_us"] <= t["per_level_us"] for t in tuned)},
            "note": "value: compiled pattern plans cached (same query/evidence variables, new values)"}
     if not args.no_cpu_baseline:
         from oracle import ve as OVE

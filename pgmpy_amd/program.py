@@ -37,8 +37,11 @@ PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
 # levels down to the query marginal, then its normalisation).  C2 0.173-0.174 against 0.179 ms, C1 0.067
 # against 0.069-0.071 (profiles/r04o/; 8 or more blocks per level: C1 slower).  0 = one launch per level.
 # (r03's persistent grid-barrier form of several levels and its one-block-at-a-time generic chain were
-# measured slower and removed in r05.)
+# measured slower and removed in r05.)  r05: with every level a specialised kernel the chain wins on C1
+# (0.062 -> 0.056 ms/query) and loses on C2 (0.123 -> 0.128 ms), so a program times both forms once before
+# its first run / capture and keeps the faster (_tune_chains; CHAIN_TUNE = False keeps the chain).
 WG_CHAIN_BLOCKS = 4
+CHAIN_TUNE = True
 # plain programs: every level batch of contractions (and the single-workgroup chain) runs as ONE
 # plan-specialised kernel (pgm_batch_specialise) instead of the descriptor-driven k_batch_c /
 # k_batch_wg_c (r05).  A/B knob PGM_BATCH_RTC=0
@@ -92,6 +95,7 @@ class Program:
         self._handles = []
         self._pm_bound = []  # specialised product+marginal kernels (pgm_product_n_marginal_bind)
         self._pm_prepared = 0  # plain Program: _pm_bound[:n] compiled by _ready
+        self._chain_alts = []  # plain Program: (single-workgroup chain step, [(fn, note) per level]) not yet tuned
         self.step_levels = []  # levelled Program: the dependency level of each lowered step
         self.step_bytes = []  # levelled Program: algorithmic bytes of each lowered step (profiling aid)
         self._pm_launch = None  # the specialised steps actually launched (compiled by _ready)
@@ -235,11 +239,14 @@ class Program:
                         if h is not None:
                             sb = self._specialise(h)
                             if sb is not None:
-                                steps.append(lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run"))
+                                fn = lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run")
                             else:
-                                steps.append(lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run"))
+                                fn = lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")
+                            steps.append(fn)
                             notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
                                          f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
+                            # the same levels one launch each: _tune_chains keeps whichever form is faster
+                            self._chain_alts.append((fn, [self._batch_step(b) for b in group[k:e]]))
                             k = e
                             continue
                         e = k + 1  # tables over the LDS budget: one launch per level
@@ -308,6 +315,72 @@ class Program:
             arr = (ctypes.c_void_p * len(self._pm_launch))(*[h.value for h in self._pm_launch])
             N.check(N.lib().pgm_pm_prepare(arr, len(self._pm_launch)), "pm_prepare")
             self._pm_launch = []
+        if self._chain_alts:
+            if CHAIN_TUNE:
+                self._tune_chains()
+            else:
+                self._chain_alts = []
+
+    def _tune_chains(self, reps=20):
+        """A run of tiny dependent levels goes faster as one single-workgroup launch on some programs (C1:
+        0.062 -> 0.056 ms/query) and slower on others (C2: 0.123 -> 0.128 ms): capture the whole program
+        both ways as HIP graphs (how compiled queries replay it), time `reps` replays of each, alternately,
+        best of two, and keep the faster.  The steps recompute the same outputs from the same inputs, so
+        the extra replays change nothing."""
+        import torch
+
+        alts, self._chain_alts = self._chain_alts, []
+        chained = (list(self._steps), list(self.notes))
+        swap = {id(fn): lv for fn, lv in alts}
+        flat = ([], [])
+        for fn, note in zip(*chained):
+            for f, n in swap.get(id(fn), [(fn, note)]):
+                flat[0].append(f)
+                flat[1].append(n)
+        L = N.lib()
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        graphs = []
+        with E.device_lock.exclusive():
+            torch.cuda.current_stream().synchronize()
+            st = torch.cuda.Stream()
+            s = N.stream_handle(st)
+            N.check(L.pgm_event_create(ctypes.byref(a)))
+            N.check(L.pgm_event_create(ctypes.byref(b)))
+            try:
+                for steps in (chained[0], flat[0]):
+                    g = ctypes.c_void_p()
+                    N.check(L.pgm_graph_capture_begin(s), "graph_capture_begin")
+                    try:
+                        for step in steps:
+                            step(s)
+                    finally:
+                        N.check(L.pgm_graph_capture_end(s, ctypes.byref(g)), "graph_capture_end")
+                    graphs.append(g)
+
+                def timed(g):
+                    N.check(L.pgm_graph_launch(g, s), "graph_launch")
+                    N.check(L.pgm_event_record(a, s))
+                    for _ in range(reps):
+                        N.check(L.pgm_graph_launch(g, s), "graph_launch")
+                    N.check(L.pgm_event_record(b, s))
+                    ms = ctypes.c_float()
+                    N.check(L.pgm_event_elapsed_ms(a, b, ctypes.byref(ms)))
+                    return ms.value
+
+                t_chain = t_flat = float("inf")
+                for _ in range(2):
+                    t_chain = min(t_chain, timed(graphs[0]))
+                    t_flat = min(t_flat, timed(graphs[1]))
+                st.synchronize()
+            finally:
+                for g in graphs:
+                    L.pgm_graph_destroy(g)
+                L.pgm_event_destroy(a)
+                L.pgm_event_destroy(b)
+        self.chain_tuning = {"chained_us": t_chain * 1e3 / reps, "per_level_us": t_flat * 1e3 / reps}
+        if t_flat < t_chain:
+            self._steps, self.notes = flat
+            self._plain_lowered = len(self._steps)
 
     def _lower(self):
         """Levelled Program -> steps: per level, its unbatched launches then one batch launch."""

@@ -649,6 +649,7 @@ def test_single_workgroup_level_chain_matches_numpy(gpu, monkeypatch):
     from pgmpy_amd.program import Program
 
     monkeypatch.setattr(P, "WG_CHAIN_BLOCKS", 4)  # the default since r04; pinned here
+    monkeypatch.setattr(P, "CHAIN_TUNE", False)  # keep the chain whatever the timing (tested below)
     E = _e()
     rng = np.random.default_rng(11)
     n_a, n_b = 6, 5  # tiny levels before / after the wide one
@@ -928,3 +929,52 @@ def test_specialised_contraction_batch_matches_numpy(gpu, monkeypatch, spec):
               (o4, A4 * B4[:, None]), (o5, r5), (o6, A6.sum(axis=(0, 2)).T), (o7, (A7 / B7[None]).T)]
     for got, want in checks:
         np.testing.assert_allclose(E.to_host(got), want, rtol=1e-12, atol=0)
+
+
+
+def test_chain_tuning_keeps_results(gpu, monkeypatch):
+    """_tune_chains (r05): the same two-chain program with CHAIN_TUNE on times the single-workgroup chain
+    against one launch per level before its first run, records both times and keeps the faster form;
+    whichever it kept, every level equals numpy on repeated runs and through a captured graph."""
+    import torch
+
+    import pgmpy_amd.program as P
+    from pgmpy_amd.program import Program
+
+    monkeypatch.setattr(P, "WG_CHAIN_BLOCKS", 4)
+    monkeypatch.setattr(P, "CHAIN_TUNE", True)
+    E = _e()
+    rng = np.random.default_rng(12)
+    n = 7
+    x = rng.random((16, 8))
+    Ws = [rng.random((16, 16)) / 8 for _ in range(n)]
+    prog = Program()
+    cur, h, outs, want = E.to_device(x), x.copy(), [], []
+    for lv in range(n):
+        prog.begin_batch()
+        cur = prog.contract(E.to_device(Ws[lv]), ["b", "a"], cur, ["a", "r"], ["b", "r"], reduce="sum")
+        prog.end_batch()
+        h = Ws[lv] @ h
+        outs.append(cur)
+        want.append(h)
+    prog.run()
+    t = prog.chain_tuning
+    assert t["chained_us"] > 0 and t["per_level_us"] > 0, t
+    chained = any("in one workgroup" in nt for nt in prog.notes)
+    assert chained == (t["chained_us"] <= t["per_level_us"]), (t, list(prog.notes))
+
+    def check():
+        torch.cuda.synchronize()
+        for lv in range(n):
+            np.testing.assert_allclose(E.to_host(outs[lv]), want[lv], rtol=1e-12)
+
+    check()
+    for o in outs:
+        o.zero_()
+    prog.run()
+    check()
+    prog.capture()
+    for o in outs:
+        o.zero_()
+    prog.run()
+    check()
