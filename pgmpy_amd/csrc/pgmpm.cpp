@@ -590,6 +590,7 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
   pgmi_appendf(o, "struct pgm_pm_args { const double *p[%zu]; };\n", nptr);
   o += "extern \"C\" __global__ void __launch_bounds__(256) pgm_pm(const pgm_pm_args a) {\n"
        "  const unsigned b = blockIdx.x;\n";
+  std::vector<std::string> calls(n);
   size_t base = 0;
   for (size_t i = 0; i < n; ++i) {
     const int no = pm_nops(specs[i]);
@@ -597,12 +598,29 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
     for (int t = 0; t < no; ++t) call += ", a.p[" + std::to_string(base + t) + "]";
     call += ", (double *)a.p[" + std::to_string(base + no) + "], (double *)a.p[" + std::to_string(base + no + 1) + "])";
     base += (size_t)no + 2;
-    if (n == 1) {
-      o += "  " + call + ";\n";
-      break;
-    }
-    pgmi_appendf(o, "  if (b >= %lluu && b < %lluu) { %s; return; }\n", (unsigned long long)starts[i],
-                 (unsigned long long)(starts[i] + specs[i].total), call.c_str());
+    calls[i] = call;
+  }
+  if (n == 1) {
+    o += "  " + calls[0] + ";\n";
+  } else {
+    // a block finds its body through a balanced tree of literal block-range comparisons (log2 of the bodies
+    // instead of up to one compare per body; C4 rate unchanged, r05p); blocks in the padding between bodies
+    // fall out at the leaf's upper bound
+    std::function<void(size_t, size_t, int)> tree = [&](size_t lo, size_t hi, int depth) {
+      const std::string ind(2 * (size_t)depth, ' ');
+      if (hi - lo == 1) {
+        pgmi_appendf(o, "%sif (b < %lluu) %s;\n", ind.c_str(), (unsigned long long)(starts[lo] + specs[lo].total),
+                     calls[lo].c_str());
+        return;
+      }
+      const size_t mid = (lo + hi) / 2;
+      pgmi_appendf(o, "%sif (b < %lluu) {\n", ind.c_str(), (unsigned long long)starts[mid]);
+      tree(lo, mid, depth + 1);
+      o += ind + "} else {\n";
+      tree(mid, hi, depth + 1);
+      o += ind + "}\n";
+    };
+    tree(0, n, 1);
   }
   o += "}\n";
   return o;
