@@ -548,6 +548,19 @@ int pgm_dq_timer_stop_ticks(void *dq, uint64_t *start, uint64_t *end, uint64_t *
  * per-launch duration a kernel trace reports, which exceeds span / launches when queues overlap */
 int pgm_dq_timer_dispatch_stats(void *dq, uint64_t *sum_ticks, uint64_t *count);
 int pgm_dq_bound_destroy(void *dbound);
+/* r05 (ABI 22): a compiled query's steps on the queue (VariableElimination.query through a captured
+ * plain Program, pgmpy/inference/ExactInference.py:349-440, C1 / C2).  pgm_dq_bind_pm re-binds one
+ * plan-specialised launch (pgm_pm_bound_* handle: a fused product step, a merged level or a specialised
+ * contraction batch) to the queue; pgm_dq_run_chain writes the n launches as one dependent chain (each
+ * packet's barrier bit set unless independent[i] is 1 — launch i reads nothing launch i-1 writes — and
+ * agent-scope fences between them; the first acquires, the last releases at system scope; independent
+ * may be NULL), rings the doorbell once and returns when the last has completed — the outputs are then
+ * visible to the host.  Contract: no HIP work that writes the chain's inputs may be pending (the chain
+ * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.
+ * pgm_dq_profiling turns the queue's dispatch timestamps on or off (pgm_dq_timer_* need them). */
+int pgm_dq_bind_pm(void *dq, void *pm_bound, void **dbound);
+int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n);
+int pgm_dq_profiling(void *dq, int32_t on);
 
 #ifdef __cplusplus
 }

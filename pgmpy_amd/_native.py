@@ -245,6 +245,10 @@ _SIGS = {
     "pgm_dq_timer_dispatch_stats": ([_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)],
                                     ctypes.c_int),
     "pgm_dq_bound_destroy": ([_P], ctypes.c_int),
+    "pgm_dq_bind_pm": ([_P, _P, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "pgm_dq_run_chain": ([ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32],
+                         ctypes.c_int),
+    "pgm_dq_profiling": ([_P, ctypes.c_int32], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -20,6 +20,7 @@ typedef struct {
 } pgmi_jit_launch;
 
 int pgmi_rows_bound_jit(void *bound, pgmi_jit_launch *out);
+int pgmi_pm_bound_jit(void *bound, pgmi_jit_launch *out);  // pgmpm.cpp: a specialised step / batch
 int pgmi_fail(int code, const char *msg);  // set pgm_last_error, return code
 int pgmi_failf(int code, const char *fmt, ...);  // printf-style pgmi_fail
 }

@@ -626,13 +626,25 @@ static std::string pm_source(const std::vector<PMSpec> &specs, std::vector<uint6
   return o;
 }
 
+// source -> loaded kernel and its code object (process lifetime; the code object is what a direct AQL
+// dispatch loads into its own HSA executable, pgm_dq_bind_pm)
+struct PMLoaded {
+  std::string src;
+  hipFunction_t fn;
+  std::vector<char> code;
+};
 static std::mutex g_pm_mu;
-static std::vector<std::pair<std::string, hipFunction_t>> g_pm_cache;  // source -> kernel (process lifetime)
+static std::vector<PMLoaded> g_pm_cache;
+
+static const PMLoaded *pm_entry(const std::string &src) {  // caller holds g_pm_mu
+  for (auto &e : g_pm_cache)
+    if (e.src == src) return &e;
+  return nullptr;
+}
 
 static hipFunction_t pm_cached(const std::string &src) {  // caller holds g_pm_mu
-  for (auto &e : g_pm_cache)
-    if (e.first == src) return e.second;
-  return nullptr;
+  const PMLoaded *e = pm_entry(src);
+  return e ? e->fn : nullptr;
 }
 
 static hipFunction_t pm_load(const std::string &src, const std::vector<char> &code) {  // caller holds g_pm_mu
@@ -642,7 +654,7 @@ static hipFunction_t pm_load(const std::string &src, const std::vector<char> &co
     (void)hipGetLastError();
     return nullptr;
   }
-  g_pm_cache.emplace_back(src, fn);
+  g_pm_cache.push_back(PMLoaded{src, fn, code});
   return fn;
 }
 
@@ -980,6 +992,30 @@ int pgm_pm_prepare(void *const *bounds, int32_t n) {
   return pm_prepare((PMBound *const *)bounds, n);
 }
 
+// a bound specialised launch as a direct AQL dispatch sees it (pgmdq.cpp): its code object, kernel name,
+// grid and explicit argument segment (the flat pointer array)
+int pgmi_pm_bound_jit(void *bound, pgmi_jit_launch *out) {
+  PMBound *b = (PMBound *)bound;
+  if (!b || !out) return pgmi_failf(PGM_EINVAL, "pm_bound_jit: null argument");
+  if (!b->fn) {
+    const int r = pm_prepare(&b, 1);
+    if (r != PGM_OK) return r;
+  }
+  std::lock_guard<std::mutex> lk(g_pm_mu);
+  const PMLoaded *e = pm_entry(b->src);
+  if (!e || e->code.empty()) return pgmi_failf(PGM_EINVAL, "pm_bound_jit: no code object kept for this launch");
+  out->code = e->code.data();
+  out->code_size = e->code.size();
+  out->kernel = "pgm_pm";
+  out->args = b->ptrs.data();
+  out->args_size = b->ptrs.size() * sizeof(void *);
+  out->blocks = b->blocks;
+  out->wg = b->threads;
+  out->owner = b;
+  out->write_through = 0;
+  return PGM_OK;
+}
+
 int pgm_pm_bound_destroy(void *bound) {
   STALE_PROBE();
   delete (PMBound *)bound;
@@ -1166,11 +1202,12 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
   for (int j = 0; j < n; ++j) {
     if (jobs[j].kind == 1) {
       const GatherK &g = jobs[j].g;
-      if (g.nk < 1 || g.nk > KMAX || g.n_ev < 0 || g.n_ev > PGM_MAX_DIMS) return PGM_OK;
+      if (g.nk < 0 || g.nk > KMAX || g.n_ev < 0 || g.n_ev > PGM_MAX_DIMS) return PGM_OK;  // nk 0: one output
       continue;
     }
     const ContractK &k = jobs[j].k;
-    if (k.n_split != 1 || (k.row_mode != 0 && k.row_mode != 2) || k.nk < 1 || k.nk > KMAX || k.nr > KMAX)
+    if (k.n_split != 1 || (k.row_mode != 0 && k.row_mode != 2) || k.nk < 0 || k.nk > KMAX || k.nr > KMAX ||
+        (k.row_mode == 2 && k.nk < 1))
       return PGM_OK;
   }
   std::string o =

@@ -20,6 +20,7 @@ Per batch only the uint8 evidence-code columns the plan reads are touched.
 A compiled plan is immutable; run() is re-entrant on distinct outputs.
 """
 import ctypes
+import os
 import threading
 from operator import itemgetter
 
@@ -602,9 +603,15 @@ class PatternPlan:
                                       itemgetter(*idx) if idx else None)
             if sel is not None:
                 host["codes"].array[:, 0] = sel(codes)
-            s = N.stream_handle(stream)
-            prog.run(stream)
-            N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
+            dq = DirectQueue.for_queries()
+            if dq is not None and prog.bind_direct(dq):
+                # the steps as one chain of AQL packets: written and rung in ~2 us, returns when the
+                # results are in host memory (a graph launch spends ~17 us on the host first)
+                prog.run_direct()
+            else:
+                s = N.stream_handle(stream)
+                prog.run(stream)
+                N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
             return host[key].array.reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
@@ -910,6 +917,32 @@ class DirectQueue:
         if q is None:
             q = cls._default[d] = cls(d)
         return q
+
+    _queries = {}
+
+    @classmethod
+    def for_queries(cls):
+        """The current device's queue for compiled single queries (Program.bind_direct / run_direct; its
+        own queue, dispatch timestamps off), or None when PGM_QUERY_DIRECT=0 or the queue cannot be made
+        (the queries then replay their HIP graphs)."""
+        import torch
+
+        if os.environ.get("PGM_QUERY_DIRECT", "1") == "0":
+            return None
+        d = torch.cuda.current_device()
+        q = cls._queries.get(d, False)
+        if q is False:
+            try:
+                q = cls(d)
+                N.check(N.lib().pgm_dq_profiling(q._h, 0), "dq_profiling")
+            except RuntimeError:
+                q = None
+            cls._queries[d] = q
+        return q
+
+    @property
+    def handle(self):
+        return self._h
 
     def sync(self):
         N.check(N.lib().pgm_dq_sync(self._h), "dq_sync")

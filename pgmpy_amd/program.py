@@ -22,6 +22,8 @@ BATCH_SPLIT_WORK = 1 << 16
 # launches (partials + final) at ~4.5 us each, more than the unsplit job takes inside the level's batch — C2
 # 0.218 -> 0.204 ms/query (profiles/r03w/)
 PLAIN_SPLIT_WORK = 1 << 22
+# plain Program: a lone contraction up to this index space becomes a batch of one (specialised kernel)
+LONE_BATCH_WORK = 1 << 16
 # outputs up to which an n-ary product joins a level batch (flat mode, 8-B accesses); larger ones keep
 # their own row-mode launch (16-B two-rows-per-lane).  2 M best of 64 K / 512 K / 2 M / 4 M / 8 M
 # (profiles/r01i_c4_variants.txt); 256 K / 64 K within noise (r03ak)
@@ -69,6 +71,22 @@ class _Rec:
         self.step = step  # plain Program: the launch this record runs in (a batch's jobs share one)
 
 
+class _PMStep:
+    """A launch of one plan-specialised kernel (pgm_pm_bound_run: a fused product step, a merged level or
+    a specialised contraction batch), or of several independent ones (a level batch over the kernel-argument
+    budget, in parts); `bounds` are their handles, which a direct AQL chain re-binds (Program.bind_direct)."""
+
+    __slots__ = ("bounds",)
+
+    def __init__(self, *bounds):
+        self.bounds = bounds
+
+    def __call__(self, s):
+        L = N.lib()
+        for b in self.bounds:
+            N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
+
+
 class _Batch:
     """Independent small jobs collected between Program.begin_batch() and end_batch()."""
 
@@ -105,6 +123,8 @@ class Program:
         self._plain_recs = []  # plain Program: one record per launch / batch job (check_hazards only)
         self._unit = 0  # plain Program: launch counter behind _Rec.step
         self._plain_lowered = -1  # plain Program: len(_steps) right after the last lowering
+        self._direct = None  # bind_direct: the steps' direct AQL launches, () when not eligible
+        self.direct_note = None
 
     # ------------------------------------------------------------------ batching
     def begin_batch(self):
@@ -170,6 +190,35 @@ class Program:
         self._pm_bound.append(b)
         return b
 
+    def _specialise_parts(self, jobs):
+        """A level batch whose kernel arguments exceed one specialised kernel's budget (512 pointers: a
+        contraction takes 3, a gather 4; C2's 205-gather level) as consecutive parts that each fit, every
+        part specialised; None when there is nothing to split or a part is not taken."""
+        if not BATCH_SPECIALISE or len(jobs) < 2:
+            return None
+        chunks, cur, n = [], [], 0
+        for j in jobs:
+            w = 4 if j[0] == "gather" else 3
+            if cur and n + w > 512:
+                chunks.append(cur)
+                cur, n = [], 0
+            cur.append(j)
+            n += w
+        chunks.append(cur)
+        if len(chunks) < 2:
+            return None
+        L = N.lib()
+        out = []
+        for c in chunks:
+            h = self._new_batch()
+            self._add_batch_jobs(h, c)
+            N.check(L.pgm_batch_finalize(h), "batch_finalize")
+            sb = self._specialise(h)
+            if sb is None:
+                return None
+            out.append(sb)
+        return out
+
     def _batch_step(self, b):
         L = N.lib()
         h = self._new_batch()
@@ -177,8 +226,10 @@ class Program:
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
         sb = self._specialise(h)
         if sb is not None:
-            return ((lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run")),
-                    f"specialised batch of {len(b.jobs)}")
+            return _PMStep(sb), f"specialised batch of {len(b.jobs)}"
+        parts = self._specialise_parts(b.jobs)
+        if parts:
+            return _PMStep(*parts), f"specialised batch of {len(b.jobs)} in {len(parts)} parts"
         if len(b.jobs) == 1:  # a job the generator does not take: its own planner's launch
             kind, _, args = b.jobs[0]
             if kind == "contract":
@@ -239,7 +290,7 @@ class Program:
                         if h is not None:
                             sb = self._specialise(h)
                             if sb is not None:
-                                fn = lambda s, bb=sb: N.check(L.pgm_pm_bound_run(bb, s), "pm_bound_run")
+                                fn = _PMStep(sb)
                             else:
                                 fn = lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")
                             steps.append(fn)
@@ -490,7 +541,7 @@ class Program:
             self._pm_launch.append(m)
             self.merged_parts[len(self._steps)] = [r.note for r in part]
             self.merged_handles[len(self._steps)] = [r.pm for r in part]
-            self._steps.append(lambda s, b=m: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"))
+            self._steps.append(_PMStep(m))
             self.notes.append(f"merged {len(part)} specialised steps: " + "; ".join(r.note[:60] for r in part[:3]))
             self.step_bytes.append(sum(r.nbytes for r in part))
             done.update(part)
@@ -520,10 +571,18 @@ class Program:
                 bm = self._bind_marginal(A, la, out_labels, out, reduce)
                 if bm is not None:
                     pm, foot = bm
-                    fn, job = (lambda s, b=pm: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), None
+                    fn, job = _PMStep(pm), None
             self._emit(fn, note, [A, B], [out, ws], job, pm=pm, foot=foot)
             return out
-        w = _work(d) if self._batch is not None else 0
+        w = _work(d)
+        if self._batch is None and wsb == 0 and w <= LONE_BATCH_WORK:
+            # a small lone contraction (a single query's final transposing copy) as a batch of one: lowered
+            # to a plan-specialised kernel like the batched levels, so the program can run as one AQL chain
+            self.begin_batch()
+            try:
+                return self.contract(A, la, B, lb, out_labels, reduce, combine, out)
+            finally:
+                self.end_batch()
         if self._batch is not None and w <= (BATCH_MAX_WORK if wsb == 0 else PLAIN_SPLIT_WORK):
             self._batch.jobs.append(("contract", (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out)),
                                      (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)))
@@ -586,7 +645,7 @@ class Program:
             N.check(L.pgm_product_n_bind(*args, ctypes.byref(bound)), "product_n_bind")
             if bound.value:
                 self._pm_bound.append(bound)
-                fn, pm, job = (lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")), bound, None
+                fn, pm, job = _PMStep(bound), bound, None
         self._emit(fn, f"product_n {[(list(ls), tuple(t.shape), tuple(t.stride())) for t, ls in ops]} "
                        f"-> {list(out_labels)}{tuple(out.shape)}", [t for t, _ in ops], [out], job, pm=pm,
                    foot=H.product_n_foot(d, ptrs, N.ptr(out)))
@@ -611,7 +670,7 @@ class Program:
                 if bound.value:  # the plan compiled into a specialised kernel
                     self._pm_bound.append(bound)
                     pm = bound
-                    fn = lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run")
+                    fn = _PMStep(bound)
                 else:
                     fn = lambda s, a=args: N.check(L.pgm_product_n_marginal(*a, s), "product_n_marginal")
                 self._emit(fn,
@@ -649,7 +708,7 @@ class Program:
             return None
         self._keep.extend([d, ptrs, C] + strides + Ms + [t for t, _ in ops])
         self._pm_bound.append(bound)
-        self._emit(lambda s, b=bound: N.check(L.pgm_pm_bound_run(b, s), "pm_bound_run"),
+        self._emit(_PMStep(bound),
                    f"product_n_marginals {[(list(ls), tuple(t.shape)) for t, ls in ops]} -> {list(marg1)} + "
                    f"{list(marg2)}", [t for t, _ in ops], Ms, pm=bound,
                    foot=H.product_n_foot(d, ptrs, None, store=False,
@@ -773,6 +832,49 @@ class Program:
             N.check(L.pgm_graph_capture_end(s, ctypes.byref(g)), "graph_capture_end")
         self._graph = g
 
+    # ------------------------------------------------------------------ direct AQL chain (r05)
+    def bind_direct(self, dq):
+        """Re-bind every step to the user-mode queue dq (plan.DirectQueue; pgm_dq_bind_pm) so run_direct()
+        dispatches the program as one chain of AQL packets: no graph launch on the host (C2: 17.5 us of the
+        0.123 ms query before the GPU starts).  Only a plain program whose steps are all plan-specialised
+        launches qualifies (at most 128); returns whether this one does.  Bound once per program; the
+        reason a program does not qualify is kept in `direct_note`."""
+        if self._direct is not None:
+            return bool(self._direct)
+        self._ready()
+        self._direct = ()
+        steps = self._steps
+        if self._levels or not steps or len(steps) > 128:
+            self.direct_note = f"{len(steps)} steps (levelled or over 128)"
+            return False
+        other = [n for f, n in zip(steps, self.notes) if not isinstance(f, _PMStep)]
+        if other:
+            self.direct_note = "not specialised: " + "; ".join(other[:3])
+            return False
+        L = N.lib()
+        hs, indep = [], []
+        for f in steps:
+            for j, b in enumerate(f.bounds):
+                d = ctypes.c_void_p()
+                if len(hs) >= 128 or L.pgm_dq_bind_pm(dq.handle, b, ctypes.byref(d)) != 0:
+                    self.direct_note = "dq_bind_pm: " + (N.last_error() if len(hs) < 128 else "over 128 launches")
+                    for h in hs:
+                        L.pgm_dq_bound_destroy(h)
+                    return False
+                hs.append(d)
+                indep.append(1 if j else 0)  # a step's parts after its first: independent of each other
+        self._direct = hs
+        self._direct_q = dq  # the queue outlives the launches bound to it
+        self._direct_arr = (ctypes.c_void_p * len(hs))(*[h.value for h in hs])
+        self._direct_indep = (ctypes.c_uint8 * len(hs))(*indep)
+        self.direct_note = f"{len(hs)} launches as one AQL chain"
+        return True
+
+    def run_direct(self):
+        """One replay as a chain of AQL packets on the bound queue; returns when the last step has
+        completed and its outputs are visible to the host (pgm_dq_run_chain)."""
+        N.check(N.lib().pgm_dq_run_chain(self._direct_arr, self._direct_indep, len(self._direct)), "dq_run_chain")
+
     def __len__(self):
         self._lower()
         return len(self._steps)
@@ -781,6 +883,8 @@ class Program:
         g = getattr(self, "_graph", None)
         try:
             L = N.load_library()
+            for h in getattr(self, "_direct", None) or ():
+                L.pgm_dq_bound_destroy(h)
             if g is not None and g.value:
                 L.pgm_graph_destroy(g)
             for h in getattr(self, "_handles", []):

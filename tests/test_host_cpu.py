@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 21
+    assert lib.pgm_version() == 22
 
 
 def test_struct_layouts_match_header():

@@ -67,7 +67,8 @@ def main():
             arr = (ctypes.c_void_p * len(hs))(*[h.value for h in hs])
             N.check(L.pgm_pm_prepare(arr, len(hs)), "pm_prepare")
             rec["part_us"] = [_time_bound(L, N, h) for h in hs]
-        b = (fn.__defaults__ or (None,))[0]
+        bs = getattr(fn, "bounds", ())
+        b = bs[0] if len(bs) == 1 else None
         if isinstance(b, ctypes.c_void_p) and b.value in pm:
             n = L.pgm_pm_bound_source(b, buf, len(buf))
             if n > 0:
