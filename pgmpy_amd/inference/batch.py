@@ -320,8 +320,43 @@ class ColumnarEvidence:
     (1,038 columns) moves 7 of them.  Replaces the per-row state-name lookups of predict /
     predict_probability (DiscreteBayesianNetwork.py:871-878, 974-979)."""
 
-    def __init__(self, raws, luts, groups, n):
+    def __init__(self, raws, luts, groups, n, addrs=None):
         self.raws, self.luts, self.groups, self.n = raws, luts, groups, n
+        self._addrs = addrs  # column addresses while the NaN scan is pending (groups None)
+        self._scan = None
+
+    def start_scan(self):
+        """Run the pending NaN scan on a worker thread (the native scan releases the GIL), so the caller
+        can work on the device meanwhile; finish_scan() joins it and builds the groups."""
+        if self.groups is not None or self._scan is not None:
+            return
+        has_nan = np.zeros(len(self.raws), dtype=np.uint8)
+        box = {}
+
+        def work():
+            try:
+                _scan_negative(self._addrs, self.n, has_nan)
+            except BaseException as e:  # re-raised by finish_scan
+                box["error"] = e
+
+        t = threading.Thread(target=work, daemon=True)
+        self._scan = (t, has_nan, box)
+        t.start()
+
+    def finish_scan(self):
+        if self.groups is not None:
+            return
+        if self._scan is None:
+            has_nan = np.zeros(len(self.raws), dtype=np.uint8)
+            _scan_negative(self._addrs, self.n, has_nan)
+        else:
+            t, has_nan, box = self._scan
+            t.join()
+            self._scan = None
+            if "error" in box:
+                raise box["error"]
+        self.groups = _nan_groups(self.raws, has_nan, self.n)
+        self._addrs = None
 
     def host_codes_for(self, cols, rows):
         """uint8 state codes [len(cols), len(rows)] of the given frame columns and rows (host)."""
@@ -337,9 +372,11 @@ class ColumnarEvidence:
         return upload_codes(self.host_codes_for(cols, rows))
 
 
-def ingest_columnar(model, data, columns):
+def ingest_columnar(model, data, columns, defer_scan=False):
     """ColumnarEvidence of `data`, or None when a column is not a (small) pandas Categorical.
-    Raises the reference's KeyError when a cell holds a category that is not a state name."""
+    Raises the reference's KeyError when a cell holds a category that is not a state name.
+    defer_scan: leave the NaN scan (and so the groups) pending for ColumnarEvidence.start_scan /
+    finish_scan."""
     if data.columns.has_duplicates:
         return None
     cats = _frame_categoricals(data, columns)
@@ -378,12 +415,26 @@ def ingest_columnar(model, data, columns):
                 raise KeyError(f"evidence holds a category of {col} that is not a state name")
         raws.append(raw)
         luts.append(lut)
-    nc = len(columns)
-    has_nan = np.zeros(nc, dtype=np.uint8)
+    if defer_scan:
+        return ColumnarEvidence(raws, luts, None, n, addrs)
+    has_nan = np.zeros(len(columns), dtype=np.uint8)
+    _scan_negative(addrs, n, has_nan)
+    return ColumnarEvidence(raws, luts, _nan_groups(raws, has_nan, n), n)
+
+
+def _scan_negative(addrs, n, has_nan):
+    """has_nan[j] = 1 when column j (int8 category codes at addrs[j], n rows) holds a -1 (NaN):
+    the native scan on _host_threads() threads."""
+    nc = len(addrs)
     if nc and n:
         ptrs = (ctypes.c_void_p * nc)(*addrs)
         N.check(N.load_library().pgm_host_any_negative_i8(ptrs, nc, n, has_nan.ctypes.data_as(ctypes.c_void_p),
                                                           _host_threads()), "host_any_negative_i8")
+
+
+def _nan_groups(raws, has_nan, n):
+    """Rows grouped by their missing-column pattern, from the NaN-holding columns only."""
+    nc = len(raws)
     nan_cols = np.nonzero(has_nan)[0].tolist()
     if not nan_cols or n == 0:
         groups = [(np.ones(nc, dtype=bool), np.arange(n))]
@@ -403,7 +454,7 @@ def ingest_columnar(model, data, columns):
                     mask[j] = False
             groups.append((mask, rows))
         groups.sort(key=lambda gr: gr[1][0])
-    return ColumnarEvidence(raws, luts, groups, n)
+    return groups
 
 
 def _host_row_hash(codes):
@@ -487,15 +538,42 @@ def get_plan(model, variables, evidence_vars, col_of):
     return plan
 
 
-def _ingest(model, data):
+def _ingest(model, data, defer_scan=False):
     """(columns, col_of, evidence) of a frame: the zero-copy Categorical path when every column is
-    one, else the general encoder."""
+    one (its NaN scan left pending when defer_scan), else the general encoder."""
     columns = list(data.columns)
     col_of = {c: i for i, c in enumerate(columns)}
-    ev = ingest_columnar(model, data, columns)
+    ev = ingest_columnar(model, data, columns, defer_scan=defer_scan)
     if ev is None:
         ev = ingest_frame(model, data, columns)
     return columns, col_of, ev
+
+
+def _direct_speculative(model, data, ingested, variables, marginals):
+    """The direct path of a large categorical frame, overlapped with its NaN scan: while the scan runs on
+    a worker thread, the plan of the all-observed pattern maps, uploads, runs and downloads (the scan and
+    the device path take ~0.6 ms each on a 100 k-row munin frame).  Returns (plan, pinned result) when
+    the scan then finds no NaN (the frame is that one pattern), else None — the result is discarded and
+    the caller takes the grouped path with the groups the scan built.  An evidence code out of range raises
+    only when the frame had no NaN (a NaN cell reaches the kernel as an out-of-range code)."""
+    columns, col_of, ev = ingested
+    if not isinstance(ev, ColumnarEvidence) or ev.groups is not None or len(data) < FAST_MIN_ROWS:
+        return None
+    ev.start_scan()
+    plan, host, error = None, None, None
+    try:
+        plan = get_plan(model, list(variables), columns, col_of)
+        if plan.kind == "fused" and list(plan.variables) == list(variables):
+            host = _fused_to_host(plan, ev, columns, col_of, len(data), marginals)
+    except IndexError as e:
+        error = e
+    finally:
+        ev.finish_scan()
+    if len(ev.groups) != 1 or not ev.groups[0][0].all():
+        return None
+    if error is not None:
+        raise error
+    return (plan, host) if host is not None else None
 
 
 # frames of at least this many rows that are one evidence pattern of a fused plan take the direct path
@@ -603,7 +681,16 @@ def _run_groups(model, data, base_vars, want_marg, want_map, extra_nan_vars, ing
 def wide_columns(model, columns):
     """Evidence columns whose variable has more states than the uint8 codes of the batched plans hold
     (state numbers 0..253; 254 marks a non-state, 255 = NaN).  The reference has no such limit
-    (utils/state_name.py:71-84): frames with one of these take _rowwise_frame."""
+    (utils/state_name.py:71-84): frames with one of these take _rowwise_frame.  The model's largest
+    state count is cached per structure epoch (a 1,038-column munin frame: one check, not 1,038
+    get_cardinality calls, ~0.6 ms)."""
+    cpds = model.get_cpds()
+    key = (model.__dict__.get("_epoch", 0), len(cpds))
+    hit = model.__dict__.get("_pgmpy_amd_max_card")
+    if hit is None or hit[0] != key:
+        hit = model.__dict__["_pgmpy_amd_max_card"] = (key, max((int(c.cardinality[0]) for c in cpds), default=0))
+    if hit[1] < MISSING:
+        return []
     return [c for c in columns if int(model.get_cardinality(c)) >= MISSING]
 
 
@@ -670,12 +757,18 @@ def predict_probability_frame(model, data):
         return pd.DataFrame({}, index=data.index)
     if wide_columns(model, data.columns):
         return _rowwise_frame(model, data, "marg")
-    ingested = _ingest(model, data)
-    plan = _single_fused_plan(model, data, *ingested, order)
-    if plan is not None:
+    ingested = _ingest(model, data, defer_scan=n >= FAST_MIN_ROWS)
+    direct = _direct_speculative(model, data, ingested, order, True)
+    marg = direct[1] if direct is not None else None
+    if marg is None:
+        if isinstance(ingested[2], ColumnarEvidence):
+            ingested[2].finish_scan()
+        plan = _single_fused_plan(model, data, *ingested, order)
+        if plan is not None:
+            marg = _fused_to_host(plan, ingested[2], ingested[0], ingested[1], n, True)
+    if marg is not None:
         # one pattern: the marginals' rows ARE the result's columns (plan.variables == order, each
         # variable's states consecutive), so the frame is built on the pinned output block, no copy
-        marg = _fused_to_host(plan, ingested[2], ingested[0], ingested[1], n, True)
         names = [var + "_" + str(s) for var in order for s in model.get_cpds(var).state_names[var]]
         assert len(names) == marg.shape[0]
         return pd.DataFrame(marg.T, columns=names, index=data.index, copy=False)
@@ -740,10 +833,17 @@ def predict_frame(model, data):
         raise IndexError("list index out of range (predict on an empty DataFrame)")
     if wide_columns(model, data.columns):
         return _rowwise_frame(model, data, "map")
-    ingested = _ingest(model, data)
-    plan = _single_fused_plan(model, data, *ingested, order)
-    if plan is not None:  # one pattern, no NaN cell: the MAP columns straight from the pinned index
-        idx = _fused_to_host(plan, ingested[2], ingested[0], ingested[1], len(data), False).astype(np.int64)
+    ingested = _ingest(model, data, defer_scan=len(data) >= FAST_MIN_ROWS)
+    direct = _direct_speculative(model, data, ingested, order, False)
+    if direct is None:
+        if isinstance(ingested[2], ColumnarEvidence):
+            ingested[2].finish_scan()
+        plan = _single_fused_plan(model, data, *ingested, order)
+        if plan is not None:
+            direct = plan, _fused_to_host(plan, ingested[2], ingested[0], ingested[1], len(data), False)
+    if direct is not None:  # one pattern, no NaN cell: the MAP columns straight from the pinned index
+        plan = direct[0]
+        idx = direct[1].astype(np.int64)
         vals = {}
         for i in reversed(range(len(plan.variables))):
             var, c = plan.variables[i], plan.cards[i]
