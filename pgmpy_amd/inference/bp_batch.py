@@ -29,15 +29,24 @@ from ..program import Program
 
 
 class BatchedCalibration:
-    def __init__(self, bjt, beliefs, seps, n_rows, marginals=None):
+    def __init__(self, bjt, beliefs, seps, n_rows, marginals=None, done=None):
         self.bjt = bjt
         self.beliefs = beliefs  # clique -> (tensor [labels..., ROW], labels)
         self.seps = seps        # (parent, child) -> (tensor [sep..., ROW], sep labels)
         self.n_rows = n_rows
         self._marg = marginals or {}
+        self._done = done  # calibrated on another stream (an in-flight lane): its completion event
+
+    def wait(self):
+        """Order the current stream after the calibration (a no-op unless it ran on an in-flight lane's
+        stream); every accessor below calls it, a caller reading the tensors directly calls it first."""
+        if self._done is not None:
+            E._torch().cuda.current_stream().wait_event(self._done)
+        return self
 
     def clique_belief(self, clique, row):
         """Host copy of one row's belief, axes in the clique tuple's order (C-order flat)."""
+        self.wait()
         t, ls = self.beliefs[tuple(clique)]
         out = E.contract(t, ls + [E.ROW], None, None, [E.ROW] + list(clique), combine="copy")
         return E.to_host(out)[row].ravel()
@@ -45,6 +54,7 @@ class BatchedCalibration:
     def clique_beliefs_rows(self, rows):
         """{clique: [len(rows), Π card]} host copies of the given rows' beliefs, axes in each clique
         tuple's order (C-order flat) — one device pass and one download per clique."""
+        self.wait()
         torch = E._torch()
         idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=E.device())
         out = {}
@@ -56,6 +66,7 @@ class BatchedCalibration:
 
     def marginal(self, var):
         """[n_rows, card] normalized marginal of `var` per row."""
+        self.wait()
         if var in self._marg:
             return E.to_host(self._marg[var]).T.copy()
         c = self.bjt.var_clique[var]
@@ -65,6 +76,7 @@ class BatchedCalibration:
         return E.to_host(m)
 
     def marginals_device(self):
+        self.wait()
         return dict(self._marg)
 
 
@@ -340,7 +352,13 @@ class BPSchedule:
 
 
 class BatchedJunctionTree:
-    def __init__(self, jt):
+    """inflight (r05): calibrate_codes keeps this many calibration batches in flight — k compiled schedules
+    (own buffers) taken round robin, each on its own stream ordered after the caller's, so one batch's
+    first levels overlap the previous batch's last (C4, 2 in flight: 1.16 -> 1.31 M calibrations/s at
+    1,000 rows, 1.31 -> 1.41 M at 4,000; profiles/r05y/).  A returned calibration stays valid for the
+    next k - 1 calls; its accessors order the caller's stream after it."""
+
+    def __init__(self, jt, inflight=1):
         import networkx as nx
 
         self.jt = jt
@@ -366,6 +384,9 @@ class BatchedJunctionTree:
         self.variables = sorted(self.var_clique, key=str)
         self.sizes = {c: int(np.prod([self.card[v] for v in c])) for c in self.cliques}
         self._schedules = {}
+        self.inflight = max(1, int(inflight))
+        self._lane = 0
+        self._lane_streams = {}
 
     def _sum_sep(self):
         return sum(int(np.prod([self.card[v] for v in c if v in p])) for p, c in self.order)
@@ -380,8 +401,8 @@ class BatchedJunctionTree:
         in both sweeps: 8 (4 sum|C| + 4 sum|S|)."""
         return 8 * (4 * sum(self.sizes.values()) + 4 * self._sum_sep())
 
-    def schedule(self, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True):
-        key = (n_rows, tuple(ev_vars), operation, marginals, graph)
+    def schedule(self, n_rows, ev_vars, operation="marginalize", marginals=True, graph=True, lane=0):
+        key = (n_rows, tuple(ev_vars), operation, marginals, graph, lane)
         sch = self._schedules.get(key)
         if sch is None:
             sch = BPSchedule(self, n_rows, ev_vars, operation, marginals, graph)
@@ -390,10 +411,31 @@ class BatchedJunctionTree:
 
     def calibrate_codes(self, codes, ev_vars, n_rows, operation="marginalize", err=None, marginals=False):
         """codes: device uint8 [len(ev_vars), n_rows] (255 = unobserved)."""
-        sch = self.schedule(n_rows, ev_vars, operation, marginals)
-        cal = sch.run(codes)
+        if self.inflight == 1:
+            sch = self.schedule(n_rows, ev_vars, operation, marginals)
+            cal = sch.run(codes)
+            if err is not None:
+                err.copy_(sch.err)
+            return cal
+        torch = E._torch()
+        lane = self._lane
+        self._lane = (lane + 1) % self.inflight
+        sch = self.schedule(n_rows, ev_vars, operation, marginals, lane=lane)
+        caller = torch.cuda.current_stream()
+        st = self._lane_streams.get(lane)
+        if st is None:
+            st = self._lane_streams[lane] = torch.cuda.Stream()
+        # after what the caller queued: the codes' producer, and its reads of this lane's previous results
+        st.wait_stream(caller)
+        with torch.cuda.stream(st):
+            cal = sch.run(codes)
+            if err is not None:
+                err.copy_(sch.err)
+            done = torch.cuda.Event()
+            done.record(st)
+        cal._done = done
         if err is not None:
-            err.copy_(sch.err)
+            caller.wait_event(done)
         return cal
 
     def encode(self, df):
