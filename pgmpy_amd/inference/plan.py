@@ -699,14 +699,17 @@ class QueryRunner:
         L = N.lib()
         import torch
 
-        # any program the query replays is captured before this runner's lock is taken (engine.DeviceLock)
-        if self.plan.kind != "fused":
+        # any program the query replays is captured before this runner's lock is taken (engine.DeviceLock).
+        # A fused plan whose joint the fused kernel does not produce takes the steps program too (through
+        # the fused path it ran the batched steps program with a device error flag read back: ~0.3 ms)
+        steps = self.plan.kind != "fused" or (self.joint and not self.plan.joint_fused_ok)
+        if steps:
             self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
         else:
             self.plan.prepare_run(1, [self.key])
         ts = E.thread_stream()
         with self.lock:
-            if self.plan.kind != "fused":  # host copies inside the captured graph: one launch + one sync
+            if steps:  # codes and results in mapped host memory: one AQL chain (or graph launch) + one wait
                 return self.plan.query_one(codes, self.key, stream=ts)
             with torch.cuda.stream(ts):
                 return self._run_fused(L, codes)

@@ -23,7 +23,7 @@ for W in c1 c2; do
 done
 for R in 4000 1000; do
   timeout -k 10 300 python bench.py --workload c4 --rows $R --steps 20 --warmup 3 > $O/c4_$R.json 2> $O/c4.err || { tail -20 $O/c4.err; exit 1; }
-  python -c "import json; d=json.load(open('$O/c4_$R.json')); print('c4', $R, round(d['value']/1e6,4), 'M/s', d['parity']['ok'], round(d['executed_step_bytes_per_calibration']/1e6,3), 'MB/cal')"
+  python -c "import json; d=json.load(open('$O/c4_$R.json')); o=d.get('one_in_flight') or {}; print('c4', $R, round(d['value']/1e6,4), 'M/s (inflight', d.get('inflight'), '; one at a time', round((o.get('value') or 0)/1e6,4), ')', d['parity']['ok'], round(d['executed_step_bytes_per_calibration']/1e6,3), 'MB/cal')"
 done
 timeout -k 10 300 python bench.py --workload c5 --steps 20 --warmup 5 > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 1; }
 python -c "import json; d=json.load(open('$O/c5.json')); print('c5', round(d['value']/1e9,3), 'G rows/s; kernel frac', round(d['roofline']['frac'],3))"
