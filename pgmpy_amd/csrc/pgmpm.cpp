@@ -179,6 +179,10 @@ struct PMSpec {  // one fused step's specialisation
   bool has_m = true;  // false: the product alone (pgm_product_n_bind), no marginal
   unsigned gx = 1;
   uint64_t total = 0;  // blocks
+  // marginal-only passes: a kept dim no row operand carries (only row-less operands such as psi vary along
+  // it), walked inside the block — its T states share the loaded row-operand values (-1: none)
+  int tdim = -1;
+  unsigned T = 1;
 };
 
 // a bound launch: one step, or several independent steps merged into one kernel (pgm_pm_merge:
@@ -257,6 +261,10 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   const bool store = sp.store, xcd = sp.xcd, nt = sp.nt, has_m = sp.has_m;
   const unsigned gx = sp.gx;
   const uint64_t total = sp.total;
+  const int td = sp.tdim;
+  const unsigned T = td >= 0 ? sp.T : 1;
+  auto tsfx = [&](unsigned t) { return T > 1 ? "t" + std::to_string(t) : std::string(); };
+  auto tiled = [&](int i) { return td >= 0 && k.ks[i][td] != 0; };  // operand i varies along the tile dim
   std::string o;
   o += pm_signature(name, k.n_ops);
   if (xcd) o += pm_xcd_remap(total);
@@ -282,6 +290,7 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     return t;
   });
   for (int q : kord) {
+    if (q == td) continue;  // walked inside the block
     const unsigned dq = k.kdiv[q].d;
     pgmi_appendf(o, "  { const unsigned q = idx / %uu, g = idx - q * %uu; idx = q;", dq, dq);
     if (k.ksc[q]) pgmi_appendf(o, " oc += (long long)g * %lldLL;", (long long)k.ksc[q]);
@@ -306,12 +315,17 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     if (k.vec[i]) {
       for (int u = 0; u < XI; ++u)
         pgmi_appendf(o, "  const pgm_d2 h%d_%d = ((const pgm_d2 *)(o%d + f%d))[c%d];\n", i, u, i, i, u);
+    } else if (tiled(i)) {
+      for (unsigned t = 0; t < T; ++t)
+        pgmi_appendf(o, "  const double h%d%s = o%d[f%d + %lldLL];\n", i, tsfx(t).c_str(), i, i,
+                     (long long)t * (long long)k.ks[i][td]);
     } else {
       pgmi_appendf(o, "  const double h%d = o%d[f%d];\n", i, i, i);
     }
   }
   const char *init = red == PGM_RED_MAX ? "-__builtin_inf()" : "0.0";
-  for (int u = 0; u < XI && has_m; ++u) pgmi_appendf(o, "  pgm_d2 a%d = {%s, %s};\n", u, init, init);
+  for (unsigned t = 0; t < T && has_m; ++t)
+    for (int u = 0; u < XI; ++u) pgmi_appendf(o, "  pgm_d2 a%d%s = {%s, %s};\n", u, tsfx(t).c_str(), init, init);
   // reduced dims as nested loops (dim 0 outermost: the generic kernel's entry order); the innermost
   // dims whose trip product stays within `unroll` are unrolled
   int first_unrolled = k.nr;
@@ -346,30 +360,39 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
     if (k.vec[i]) {
       pgmi_appendf(o, "%sconst pgm_d2 *p%d = (const pgm_d2 *)(o%d + f%d + %s);\n", ind.c_str(), i, i, i, J.c_str());
       for (int u = 0; u < XI; ++u) pgmi_appendf(o, "%sconst pgm_d2 v%d_%d = p%d[c%d];\n", ind.c_str(), i, u, i, u);
+    } else if (tiled(i)) {
+      for (unsigned t = 0; t < T; ++t)
+        pgmi_appendf(o, "%sconst double s%d%s = o%d[f%d + %s + %lldLL];\n", ind.c_str(), i, tsfx(t).c_str(), i, i,
+                     J.c_str(), (long long)t * (long long)k.ks[i][td]);
     } else {
       pgmi_appendf(o, "%sconst double s%d = o%d[f%d + %s];\n", ind.c_str(), i, i, i, J.c_str());
     }
   }
-  for (int u = 0; u < XI; ++u) {
-    for (int h = 0; h < 2; ++h) {
-      const char cx = h ? 'y' : 'x';
-      auto term = [&](int i) {
-        char buf[64];
-        if (k.jvar[i] && k.vec[i]) snprintf(buf, sizeof buf, "v%d_%d.%c", i, u, cx);
-        else if (k.jvar[i]) snprintf(buf, sizeof buf, "s%d", i);
-        else if (k.vec[i]) snprintf(buf, sizeof buf, "h%d_%d.%c", i, u, cx);
-        else snprintf(buf, sizeof buf, "h%d", i);
-        return std::string(buf);
-      };
-      std::string e = "1.0";
-      for (int i = 0; i < k.n_ops; ++i) {
-        if (k.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
-        else if (k.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
-          e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+  for (unsigned t = 0; t < T; ++t) {
+    const std::string ts = tsfx(t);
+    for (int u = 0; u < XI; ++u) {
+      for (int h = 0; h < 2; ++h) {
+        const char cx = h ? 'y' : 'x';
+        auto term = [&](int i) {
+          char buf[64];
+          const char *sf = tiled(i) ? ts.c_str() : "";
+          if (k.jvar[i] && k.vec[i]) snprintf(buf, sizeof buf, "v%d_%d.%c", i, u, cx);
+          else if (k.jvar[i]) snprintf(buf, sizeof buf, "s%d%s", i, sf);
+          else if (k.vec[i]) snprintf(buf, sizeof buf, "h%d_%d.%c", i, u, cx);
+          else snprintf(buf, sizeof buf, "h%d%s", i, sf);
+          return std::string(buf);
+        };
+        std::string e = "1.0";
+        for (int i = 0; i < k.n_ops; ++i) {
+          if (k.kind[i] == PGM_PRODN_MUL) e = "(" + e + " * " + term(i) + ")";
+          else if (k.kind[i] == PGM_PRODN_RATIO && i + 1 < MOPS)
+            e = "(" + e + " * pgm_ratio(" + term(i) + ", " + term(i + 1) + "))";
+        }
+        pgmi_appendf(o, "%sconst double w%d%s%c = %s;\n", ind.c_str(), u, ts.c_str(), cx, e.c_str());
       }
-      pgmi_appendf(o, "%sconst double w%d%c = %s;\n", ind.c_str(), u, cx, e.c_str());
+      pgmi_appendf(o, "%sconst pgm_d2 w%d%s = {w%d%sx, w%d%sy};\n", ind.c_str(), u, ts.c_str(), u, ts.c_str(), u,
+                   ts.c_str());
     }
-    pgmi_appendf(o, "%sconst pgm_d2 w%d = {w%dx, w%dy};\n", ind.c_str(), u, u, u);
   }
   if (store) {
     pgmi_appendf(o, "%spgm_d2 *cj = (pgm_d2 *)(C + oc + %s);\n", ind.c_str(), lin(k.rsc).c_str());
@@ -381,12 +404,16 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
         pgmi_appendf(o, "%s%scj[x%d] = w%d;\n", ind.c_str(), guard.c_str(), u, u);
     }
   }
-  for (int u = 0; u < XI && has_m; ++u) {
-    if (red == PGM_RED_MAX)
-      pgmi_appendf(o, "%sa%d.x = pgm_maxn(a%d.x, w%d.x); a%d.y = pgm_maxn(a%d.y, w%d.y);\n", ind.c_str(), u, u, u, u,
-              u, u);
-    else
-      pgmi_appendf(o, "%sa%d += w%d;\n", ind.c_str(), u, u);
+  for (unsigned t = 0; t < T && has_m; ++t) {
+    const std::string tss = tsfx(t);
+    const char *ts = tss.c_str();
+    for (int u = 0; u < XI; ++u) {
+      if (red == PGM_RED_MAX)
+        pgmi_appendf(o, "%sa%d%s.x = pgm_maxn(a%d%s.x, w%d%s.x); a%d%s.y = pgm_maxn(a%d%s.y, w%d%s.y);\n", ind.c_str(),
+                     u, ts, u, ts, u, ts, u, ts, u, ts, u, ts);
+      else
+        pgmi_appendf(o, "%sa%d%s += w%d%s;\n", ind.c_str(), u, ts, u, ts);
+    }
   }
   for (int r = k.nr - 1; r >= 0; --r) {
     ind.resize(ind.size() - 2);
@@ -404,12 +431,17 @@ static std::string pm_body(const PMSpec &sp, const std::string &name) {
   }
   // marginal stores: nontemporal when the step stores no product (a marginal-only pass writes nothing
   // else), plain (write-back L2) otherwise
-  for (int u = 0; u < XI && has_m; ++u) {
-    const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
-    if (!store)
-      pgmi_appendf(o, "  %s__builtin_nontemporal_store(a%d, (pgm_d2 *)(M + om) + x%d);\n", guard.c_str(), u, u);
-    else
-      pgmi_appendf(o, "  %s((pgm_d2 *)(M + om))[x%d] = a%d;\n", guard.c_str(), u, u);
+  for (unsigned t = 0; t < T && has_m; ++t) {
+    const std::string ts = tsfx(t);
+    const std::string mo = T > 1 ? "M + om + " + std::to_string((long long)t * (long long)k.ksm[td]) + "LL" : "M + om";
+    for (int u = 0; u < XI; ++u) {
+      const std::string guard = tail ? "if (x" + std::to_string(u) + " < " + std::to_string(NP) + "u) " : "";
+      if (!store)
+        pgmi_appendf(o, "  %s__builtin_nontemporal_store(a%d%s, (pgm_d2 *)(%s) + x%d);\n", guard.c_str(), u, ts.c_str(),
+                     mo.c_str(), u);
+      else
+        pgmi_appendf(o, "  %s((pgm_d2 *)(%s))[x%d] = a%d%s;\n", guard.c_str(), mo.c_str(), u, u, ts.c_str());
+    }
   }
   o += "}\n";
   return o;
@@ -778,6 +810,25 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   sp.nt = nt;
   sp.gx = (unsigned)gx;
   sp.total = total;
+  // a marginal-only pass re-loads its row operands (child messages) for every state of a kept dim that
+  // only row-less operands (psi) carry — an L2-bound walk (C4 level 2: 64 states of the 32,256-state
+  // clique); walk the largest such dim (2..8 states) inside the block instead, its states sharing the
+  // loaded values, while >= 2,048 blocks remain and T x XI accumulators fit (C4, 4,000 rows: one batch in
+  // flight 1.32-1.33 -> 1.36 M calibrations/s, two 1.39-1.43 -> 1.42-1.45 M; 1,000 rows unchanged; r05ac)
+  if (!C && has_m && k.mdiv < 0) {
+    unsigned best = 1;
+    for (int q = 0; q + 1 < k.nk; ++q) {
+      const unsigned d = k.kdiv[q].d;
+      bool rowless = d >= 2 && d <= 8 && k.ksm[q] != 0;
+      for (int t = 0; rowless && t < k.n_ops; ++t)
+        if (k.vec[t] && k.ks[t][q]) rowless = false;
+      if (rowless && d > best && total / d >= 2048 && d * (unsigned)XI <= 16) best = d, sp.tdim = q;
+    }
+    if (sp.tdim >= 0) {
+      sp.T = best;
+      sp.total = total / best;
+    }
+  }
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;
   const std::string src = pm_source({sp}, starts, &blocks);

@@ -575,6 +575,56 @@ def test_product_n_marginal_bound_matches_generic(gpu, rows, red, store):
          ["a", "c", "e", "f", R], kinds=[NN.PRODN_MUL, NN.PRODN_RATIO, NN.PRODN_DEN, NN.PRODN_MUL])
 
 
+@pytest.mark.parametrize("red", ["sum", "max"])
+def test_marginal_only_psi_tile_matches_generic(gpu, red):
+    """r05: a marginal-only pass whose kept dims include some that only psi carries walks the largest of
+    them inside the block (its states share the loaded child messages; PMSpec.tdim) — the shape of C4's
+    32,256-state clique sending its message to the root: psi over (g, h, i, j, k, F), two child messages
+    over (h, k, F, rows), the message over (g, h, i, j, F, rows).  Equals the generic fused kernel (same
+    product and summation order) to 1e-14, and the source shows the tile (two accumulator sets)."""
+    import ctypes
+
+    import torch
+
+    from pgmpy_amd import _native as NN
+
+    E = _e()
+    L = NN.lib()
+    rng = np.random.default_rng(5)
+    cl = list("ghijkF")
+    card = dict(zip(cl, (4, 2, 4, 4, 4, 63)))
+    R, rows = E.ROW, 2000
+    psi = E.to_device(rng.random([card[v] for v in cl]))
+    m1 = E.to_device(rng.random([card["h"], card["k"], card["F"], rows]))
+    m2 = E.to_device(rng.random([card["h"], card["k"], card["F"], rows]))
+    ops = [(psi, cl), (m1, ["h", "k", "F", R]), (m2, ["h", "k", "F", R])]
+    marg = ["g", "h", "i", "j", "F", R]
+    outs = []
+    for bound_path in (False, True):
+        d, ptrs, C, ms, M, ok = E.prepare_product_n_marginal(ops, cl + [R], marg, None, None, False)
+        assert ok
+        args = (ctypes.byref(d), ptrs, None, ms, E._REDUCE[red], NN.ptr(M))
+        s = NN.stream_handle()
+        if bound_path:
+            buf = ctypes.create_string_buffer(1 << 20)
+            assert L.pgm_product_n_marginal_source(*args, buf, len(buf)) > 0
+            assert b"a0t1" in buf.value, "the psi-only dims are walked inside the block"
+            b = ctypes.c_void_p()
+            NN.check(L.pgm_product_n_marginal_bind(*args, ctypes.byref(b)), "bind")
+            assert b.value
+            NN.check(L.pgm_pm_bound_run(b, s), "run")
+            torch.cuda.synchronize()
+            L.pgm_pm_bound_destroy(b)
+        else:
+            NN.check(L.pgm_product_n_marginal(*args, s), "generic")
+        outs.append(E.to_host(M))
+    np.testing.assert_allclose(outs[1], outs[0], rtol=1e-14, atol=0)
+    h = {v: E.to_host(t) for v, t in (("psi", psi), ("m1", m1), ("m2", m2))}
+    full = h["psi"][..., None] * h["m1"][None, :, None, None, :, :, :] * h["m2"][None, :, None, None, :, :, :]
+    exp = full.sum(axis=4) if red == "sum" else full.max(axis=4)
+    np.testing.assert_allclose(outs[1], exp, rtol=1e-12)
+
+
 def test_bp_fused_marginals_many_rows(gpu):
     """Batched BP with >= 64 evidence rows takes the fused belief + separator-marginal kernels;
     calibrated beliefs must equal the unfused schedule's (single-row calibrations)."""
