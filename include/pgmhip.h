@@ -556,7 +556,8 @@ int pgm_dq_bound_destroy(void *dbound);
  * agent-scope fences between them; the first acquires, the last releases at system scope; independent
  * may be NULL), rings the doorbell once and returns when the last has completed — the outputs are then
  * visible to the host.  Contract: no HIP work that writes the chain's inputs may be pending (the chain
- * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.
+ * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.  Not under
+ * rocprofv3's queue interception (a chain crashed its interceptor; the Python side replays graphs there).
  * pgm_dq_profiling turns the queue's dispatch timestamps on or off (pgm_dq_timer_* need them). */
 int pgm_dq_bind_pm(void *dq, void *pm_bound, void **dbound);
 int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n);

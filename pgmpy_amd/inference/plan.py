@@ -926,11 +926,15 @@ class DirectQueue:
     @classmethod
     def for_queries(cls):
         """The current device's queue for compiled single queries (Program.bind_direct / run_direct; its
-        own queue, dispatch timestamps off), or None when PGM_QUERY_DIRECT=0 or the queue cannot be made
-        (the queries then replay their HIP graphs)."""
+        own queue, dispatch timestamps off), or None when PGM_QUERY_DIRECT=0, under rocprofv3, or when the
+        queue cannot be made (the queries then replay their HIP graphs)."""
         import torch
 
         if os.environ.get("PGM_QUERY_DIRECT", "1") == "0":
+            return None
+        if any(k.startswith("ROCPROF") for k in os.environ):
+            # under rocprofv3 the queue is intercepted and a chain (packets written together, one doorbell)
+            # crashed its interceptor: queries replay their graphs there (same kernels)
             return None
         d = torch.cuda.current_device()
         q = cls._queries.get(d, False)
