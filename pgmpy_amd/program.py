@@ -39,11 +39,12 @@ PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
 # levels down to the query marginal, then its normalisation).  C2 0.173-0.174 against 0.179 ms, C1 0.067
 # against 0.069-0.071 (profiles/r04o/; 8 or more blocks per level: C1 slower).  0 = one launch per level.
 # (r03's persistent grid-barrier form of several levels and its one-block-at-a-time generic chain were
-# measured slower and removed in r05.)  r05: with every level a specialised kernel the chain wins on C1
-# (0.062 -> 0.056 ms/query) and loses on C2 (0.123 -> 0.128 ms), so a program times both forms once before
-# its first run / capture and keeps the faster (_tune_chains; CHAIN_TUNE = False keeps the chain).
+# measured slower and removed in r05.)  r05: replayed as graphs the chain won on C1 (0.062 -> 0.056 ms/query)
+# and lost on C2 (0.123 -> 0.128 ms), so _tune_chains timed both forms per program; dispatched as one AQL
+# chain (the single-query default since) the chain wins on both — C2 0.111-0.112 vs 0.122-0.124 ms, C1 0.049
+# vs 0.060 (profiles/r05ae/) — so programs keep the chain; CHAIN_TUNE = True times both as graphs.
 WG_CHAIN_BLOCKS = 4
-CHAIN_TUNE = True
+CHAIN_TUNE = False
 # plain programs: every level batch of contractions (and the single-workgroup chain) runs as ONE
 # plan-specialised kernel (pgm_batch_specialise) instead of the descriptor-driven k_batch_c /
 # k_batch_wg_c (r05).  A/B knob PGM_BATCH_RTC=0
