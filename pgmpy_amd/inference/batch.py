@@ -383,7 +383,16 @@ def ingest_columnar(model, data, columns, defer_scan=False):
     if cats is None:
         return None
     n = len(data)
+    fast = _schema_fast(model, columns, cats, n)
+    if fast is not None:
+        raws, luts, addrs = fast
+        if defer_scan:
+            return ColumnarEvidence(raws, luts, None, n, addrs)
+        has_nan = np.zeros(len(columns), dtype=np.uint8)
+        _scan_negative(addrs, n, has_nan)
+        return ColumnarEvidence(raws, luts, _nan_groups(raws, has_nan, n), n)
     raws, luts, addrs = [], [], []
+    all_ok = True
     i8 = np.dtype(np.int8)
     cpd_of = getattr(model, "_cpd_index", None) or {}
     addressof, char_at = ctypes.addressof, ctypes.c_char.from_buffer
@@ -409,17 +418,64 @@ def ingest_columnar(model, data, columns, defer_scan=False):
             raise ValueError(f"variable {col} has {len(st)} states; uint8 codes hold at most 254")
         lut, ok = _category_lut(col, st, arr.dtype)
         if not ok:
+            all_ok = False
             bad = np.nonzero(lut[:len(arr.dtype.categories)] == 254)[0]
             if np.isin(raw, bad.astype(np.int8)).any():
                 encode_frame(model, data, [col])  # raises the reference's KeyError for the cell
                 raise KeyError(f"evidence holds a category of {col} that is not a state name")
         raws.append(raw)
         luts.append(lut)
+    if all_ok:
+        _schema_store(model, columns, cats, luts)
     if defer_scan:
         return ColumnarEvidence(raws, luts, None, n, addrs)
     has_nan = np.zeros(len(columns), dtype=np.uint8)
     _scan_negative(addrs, n, has_nan)
     return ColumnarEvidence(raws, luts, _nan_groups(raws, has_nan, n), n)
+
+
+# frame schemas already ingested: (model, epoch, columns, the columns' CategoricalDtype objects) -> their LUTs,
+# when every category of every column is a state name.  A frame of the same schema (the same dtype objects:
+# the same frame again, or frames built from one dtype per variable) then skips the per-column CPD and LUT
+# lookups (a 1,038-column munin frame: ~0.5 ms of the ~2.2 ms predict_probability).  The dtype objects are
+# kept referenced, so their ids stay theirs while cached.
+_SCHEMA_CACHE = {}
+_SCHEMA_CACHE_MAX = 32
+
+
+def _schema_key(model, columns, dtypes):
+    return (id(model), model.__dict__.get("_epoch", 0), tuple(columns), tuple(map(id, dtypes)))
+
+
+def _schema_store(model, columns, cats, luts):
+    dtypes = [a.dtype for a in cats]
+    with _LUT_LOCK:
+        if len(_SCHEMA_CACHE) >= _SCHEMA_CACHE_MAX:
+            _SCHEMA_CACHE.clear()
+        _SCHEMA_CACHE[_schema_key(model, columns, dtypes)] = (model, dtypes, list(luts))
+
+
+def _schema_fast(model, columns, cats, n):
+    """(raws, luts, addrs) of a frame whose schema was ingested before, or None (the general loop)."""
+    dtypes = [a.dtype for a in cats]
+    hit = _SCHEMA_CACHE.get(_schema_key(model, columns, dtypes))
+    if hit is None or hit[0] is not model:
+        return None
+    try:
+        raws = [a._codes for a in cats]
+    except AttributeError:  # pragma: no cover - pandas internals moved
+        return None
+    i8 = np.dtype(np.int8)
+    if not all(r.dtype is i8 and r.flags.c_contiguous for r in raws):
+        return None
+    if not n:
+        return raws, hit[2], [0] * len(raws)
+    addressof, char_at = ctypes.addressof, ctypes.c_char.from_buffer
+    try:
+        addrs = [addressof(char_at(r)) for r in raws]
+    except (TypeError, ValueError):  # a read-only buffer: the general loop
+        return None
+    return raws, hit[2], addrs
 
 
 def _scan_negative(addrs, n, has_nan):
