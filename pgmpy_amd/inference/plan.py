@@ -603,8 +603,7 @@ class PatternPlan:
                                       itemgetter(*idx) if idx else None)
             if sel is not None:
                 host["codes"].array[:, 0] = sel(codes)
-            dq = DirectQueue.for_queries()
-            if dq is not None and prog.bind_direct(dq):
+            if prog._direct or ((dq := DirectQueue.for_queries()) is not None and prog.bind_direct(dq)):
                 # the steps as one chain of AQL packets: written and rung in ~2 us, returns when the
                 # results are in host memory (a graph launch spends ~17 us on the host first)
                 prog.run_direct()
@@ -932,13 +931,14 @@ class DirectQueue:
 
         if os.environ.get("PGM_QUERY_DIRECT", "1") == "0":
             return None
-        if any(k.startswith("ROCPROF") for k in os.environ):
-            # under rocprofv3 the queue is intercepted and a chain (packets written together, one doorbell)
-            # crashed its interceptor: queries replay their graphs there (same kernels)
-            return None
         d = torch.cuda.current_device()
         q = cls._queries.get(d, False)
         if q is False:
+            if any(k.startswith("ROCPROF") for k in os.environ):
+                # under rocprofv3 the queue is intercepted and a chain (packets written together, one
+                # doorbell) crashed its interceptor: queries replay their graphs there (same kernels)
+                cls._queries[d] = None
+                return None
             try:
                 q = cls(d)
                 N.check(N.lib().pgm_dq_profiling(q._h, 0), "dq_profiling")
