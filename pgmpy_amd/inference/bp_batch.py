@@ -315,6 +315,19 @@ class BPSchedule:
                             if ok:
                                 _, sigma, _ = prog.product_n_marginal(fops, lp + [R], list(sc) + [R], out=tp,
                                                                       kinds=fk, reduce=red, store=False)
+                    if sigma is None and src != tuple(lp):
+                        # a second scope whose smallest computed container is the same source: both marginals
+                        # in one read of it (C4's root child scopes, 129 / 64 MB sources read once, not twice:
+                        # 3.45 -> 3.40 MB per calibration, +1 % at 4,000 rows; profiles/r05ai/)
+                        partner = next((s2 for s2 in ordered[si + 1:] if s2 not in have
+                                        and not set(s2) <= set(sc) and not set(sc) <= set(s2)
+                                        and min((h for h in have if set(s2) <= set(h)), key=scope_size) == src), None)
+                        if partner is not None:
+                            two = prog.product_n_marginals([(have[src], list(src) + [R])], list(src) + [R],
+                                                           list(sc) + [R], list(partner) + [R], out=have[src],
+                                                           reduce=red)
+                            if two is not None:
+                                sigma, have[partner] = two
                     if sigma is None:
                         sigma = prog.contract(have[src], list(src) + [R], None, None, list(sc) + [R], reduce=red,
                                               combine="copy")
