@@ -286,6 +286,28 @@ def test_columnar_ingestion_matches_host_encoder():
     with pytest.raises(KeyError):
         ingest_columnar(m, bad, cols)
     assert ingest_columnar(m, df.astype({cols[1]: object}), cols) is None
+    # r05: the NaN scan left pending (the direct path runs meanwhile), then run on a worker thread and
+    # joined, gives the same groups
+    dev = ingest_columnar(m, df, cols, defer_scan=True)
+    assert dev.groups is None
+    dev.start_scan()
+    dev.finish_scan()
+    assert {tuple(np.nonzero(~mk)[0]): set(r.tolist()) for mk, r in dev.groups} == exp
+    # r05: frame-schema cache — a frame whose every category is a state name is ingested through the stored
+    # LUTs the second time (same codes); a model structure edit (epoch) misses
+    from pgmpy_amd.inference import batch as B
+
+    clean = pd.DataFrame({c: pd.Categorical.from_codes(rng.integers(0, len(m.states[c]), n).astype(np.int8),
+                                                       categories=[str(s) for s in m.states[c]]) for c in cols})
+    e1 = ingest_columnar(m, clean, cols)
+    cats = B._frame_categoricals(clean, cols)
+    assert B._schema_fast(m, cols, cats, n) is not None
+    e2 = ingest_columnar(m, clean, cols)
+    assert all(a is b for a, b in zip(e1.luts, e2.luts))
+    assert np.array_equal(e2.host_codes_for(list(range(len(cols))), rows), encode_frame(m, clean, cols))
+    assert B._schema_fast(m, cols, B._frame_categoricals(df, cols), n) is None  # "unused" categories: not stored
+    m._bump()
+    assert B._schema_fast(m, cols, cats, n) is None
 
 
 def test_specialised_row_kernel_source_compiles_for_gfx950():
