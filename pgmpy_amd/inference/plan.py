@@ -607,7 +607,8 @@ class PatternPlan:
                 # the steps as one chain of AQL packets: written and rung in ~2 us, returns when the
                 # results are in host memory (a graph launch spends ~17 us on the host first)
                 prog.run_direct()
-            else:
+            else:  # the graph on the calling thread's own stream (engine.thread_stream) unless one is given
+                stream = stream if stream is not None else E.thread_stream()
                 s = N.stream_handle(stream)
                 prog.run(stream)
                 N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
@@ -706,11 +707,10 @@ class QueryRunner:
             self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
         else:
             self.plan.prepare_run(1, [self.key])
-        ts = E.thread_stream()
         with self.lock:
             if steps:  # codes and results in mapped host memory: one AQL chain (or graph launch) + one wait
-                return self.plan.query_one(codes, self.key, stream=ts)
-            with torch.cuda.stream(ts):
+                return self.plan.query_one(codes, self.key)
+            with torch.cuda.stream(E.thread_stream()):
                 return self._run_fused(L, codes)
 
     def _run_fused(self, L, codes):
