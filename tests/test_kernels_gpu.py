@@ -1028,3 +1028,49 @@ def test_chain_tuning_keeps_results(gpu, monkeypatch):
         o.zero_()
     prog.run()
     check()
+
+
+def test_program_direct_chain_and_eligibility(gpu):
+    """r05: Program.bind_direct / run_direct — a plain program whose steps are all plan-specialised launches
+    (here 6 dependent levels, the first a level of 130 jobs split into parts over the kernel-argument budget)
+    runs as one AQL chain on a user-mode queue with the graph replay's results bit for bit; a program with a
+    step that is not a specialised launch (a raw host-ordered step) does not qualify and says why."""
+    import torch
+
+    from pgmpy_amd.inference.plan import DirectQueue
+    from pgmpy_amd.program import Program
+
+    E = _e()
+    rng = np.random.default_rng(21)
+    dq = DirectQueue()
+    prog = Program()
+    xs = [E.to_device(rng.random((8, 4))) for _ in range(200)]
+    W = [E.to_device(rng.random((8, 8)) / 4) for _ in range(200)]
+    prog.begin_batch()  # 200 independent jobs x 3 pointers > 512: specialised in parts
+    cur = [prog.contract(W[i], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    prog.end_batch()
+    for lv in range(5):
+        prog.begin_batch()
+        cur = [prog.contract(W[(i + lv) % 200], ["b", "a"], cur[i], ["a", "r"], ["b", "r"], reduce="sum")
+               for i in range(0, len(cur), 2)]
+        prog.end_batch()
+    out = cur
+    assert prog.bind_direct(dq), prog.direct_note
+    assert any("parts" in n for n in prog.notes), list(prog.notes)
+    prog.run_direct()
+    got = [E.to_host(t).copy() for t in out]
+    for t in out:
+        t.zero_()
+    torch.cuda.synchronize()
+    prog.run()
+    torch.cuda.synchronize()
+    for a, t in zip(got, out):
+        np.testing.assert_array_equal(a, E.to_host(t))
+    bad = Program()
+    bad.begin_batch()
+    y = bad.contract(W[0], ["b", "a"], xs[0], ["a", "r"], ["b", "r"], reduce="sum")
+    bad.end_batch()
+    bad.raw_step(lambda s: None, "host-ordered no-op")
+    assert not bad.bind_direct(dq)
+    assert "not specialised" in bad.direct_note, bad.direct_note
+    del y
