@@ -553,7 +553,8 @@ int pgm_dq_bound_destroy(void *dbound);
  * plan-specialised launch (pgm_pm_bound_* handle: a fused product step, a merged level or a specialised
  * contraction batch) to the queue; pgm_dq_run_chain writes the n launches as one dependent chain (each
  * packet's barrier bit set unless independent[i] is 1 — launch i reads nothing launch i-1 writes — and
- * agent-scope fences between them; the first acquires, the last releases at system scope; independent
+ * agent-scope fences on every packet, the last releasing at system scope — inputs the host writes between
+ * chains must be in coherent host memory (pgm_host_alloc), which the kernels read uncached; independent
  * may be NULL), rings the doorbell once and returns when the last has completed — the outputs are then
  * visible to the host.  Contract: no HIP work that writes the chain's inputs may be pending (the chain
  * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.  Not under
