@@ -671,60 +671,27 @@ class PatternPlan:
 
 class QueryRunner:
     """One evidence row through a compiled plan, results back on the host (VariableElimination.query
-    on a Bayesian network, ExactInference.py:246-457).  Owns its device codes/output buffers and a
-    pinned host staging buffer; a lock makes concurrent queries from several threads on one
+    on a Bayesian network, ExactInference.py:246-457): the plan's steps program with its codes and
+    results in mapped host memory (PatternPlan.query_one — one AQL chain on the query queue, or one graph
+    replay), whatever the plan's kind.  r05: fused plans took the fused row kernel here (codes up, the
+    pass, results down on the thread's stream: 0.44 ms per query on alarm, against 25 us for the steps
+    program; profiles/r05ao/).  A lock makes concurrent queries from several threads on one
     VariableElimination safe (the reference calls map_query from joblib threads on one object,
     DiscreteBayesianNetwork.py:871)."""
 
     def __init__(self, plan, joint):
-        import torch
-
         self.plan = plan
         self.joint = bool(joint)
         self.lock = threading.Lock()
-        n_ev = max(1, len(plan.evidence_vars))
-        dev = E.device()
-        self.d_codes = torch.zeros((n_ev, 1), dtype=torch.uint8, device=dev)
-        self.h_codes = torch.zeros((n_ev, 1), dtype=torch.uint8, pin_memory=True)
-        self.out = plan.alloc_outputs(1, marginals=not joint, joint=joint)
         self.key = "joint" if joint else "marg"
-        self.h_out = torch.empty(tuple(self.out[self.key].shape), dtype=torch.float64, pin_memory=True)
-        # runs go to the calling thread's own stream (engine.thread_stream): what the default stream
-        # queued for these buffers (zero fills) completes first
-        torch.cuda.current_stream().synchronize()
 
     def run(self, codes):
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
         the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
-        L = N.lib()
-        import torch
-
-        # any program the query replays is captured before this runner's lock is taken (engine.DeviceLock).
-        # A fused plan whose joint the fused kernel does not produce takes the steps program too (through
-        # the fused path it ran the batched steps program with a device error flag read back: ~0.3 ms)
-        steps = self.plan.kind != "fused" or (self.joint and not self.plan.joint_fused_ok)
-        if steps:
-            self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
-        else:
-            self.plan.prepare_run(1, [self.key])
+        # the program is built and captured before this runner's lock is taken (engine.DeviceLock)
+        self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
         with self.lock:
-            if steps:  # codes and results in mapped host memory: one AQL chain (or graph launch) + one wait
-                return self.plan.query_one(codes, self.key)
-            with torch.cuda.stream(E.thread_stream()):
-                return self._run_fused(L, codes)
-
-    def _run_fused(self, L, codes):
-        """The fused path on the current (this thread's) stream: codes up, one pass, result down."""
-        s = N.stream_handle()
-        hc = self.h_codes.numpy()
-        hc[:len(codes), 0] = codes
-        N.check(L.pgm_memcpy_h2d(N.ptr(self.d_codes), ctypes.c_void_p(self.h_codes.data_ptr()),
-                                 hc.nbytes, s), "memcpy_h2d")
-        self.plan.run(self.d_codes, 1, 0, 1, self.out)
-        dst = self.out[self.key]
-        N.check(L.pgm_memcpy_d2h(ctypes.c_void_p(self.h_out.data_ptr()), N.ptr(dst),
-                                 dst.numel() * 8, s), "memcpy_d2h")
-        return self.h_out.numpy().reshape(-1).copy()
+            return self.plan.query_one(codes, self.key)
 
 
 class BoundRows:
