@@ -595,7 +595,12 @@ class PatternPlan:
         Returns a new fp64 ndarray (`key` "marg" or "joint")."""
         L = N.lib()
         with self._lock:
-            prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
+            q1 = self.__dict__.get("_q1")  # key -> (program, host buffers) of the one-row host-io program
+            hit = q1.get(key) if q1 is not None else None
+            if hit is None:
+                prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
+                self.__dict__.setdefault("_q1", {})[key] = hit = (prog, host)
+            prog, host = hit
             sel = self.__dict__.get("_ev_sel")
             if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
                 idx = [self.col_of[v] for v in self.ev_used]
@@ -689,7 +694,9 @@ class QueryRunner:
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
         the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
         # the program is built and captured before this runner's lock is taken (engine.DeviceLock)
-        self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
+        if not self.__dict__.get("_prepared"):
+            self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
+            self._prepared = True
         with self.lock:
             return self.plan.query_one(codes, self.key)
 
