@@ -42,8 +42,9 @@ PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
 # measured slower and removed in r05.)  r05: replayed as graphs the chain won on C1 (0.062 -> 0.056 ms/query)
 # and lost on C2 (0.123 -> 0.128 ms), so _tune_chains timed both forms per program; dispatched as one AQL
 # chain (the single-query default since) the chain wins on both — C2 0.111-0.112 vs 0.122-0.124 ms, C1 0.049
-# vs 0.060 (profiles/r05ae/) — so programs keep the chain; CHAIN_TUNE = True times both as graphs.
-WG_CHAIN_BLOCKS = 4
+# vs 0.060 (profiles/r05ae/) — so programs keep the chain; CHAIN_TUNE = True times both as graphs.  Levels of up
+# to 8 blocks chained (r05aq, after every single query took the chain): C1 0.0255 -> 0.0245 ms, C2 unchanged.
+WG_CHAIN_BLOCKS = 8
 CHAIN_TUNE = False
 # plain programs: every level batch of contractions (and the single-workgroup chain) runs as ONE
 # plan-specialised kernel (pgm_batch_specialise) instead of the descriptor-driven k_batch_c /
