@@ -1292,8 +1292,11 @@ def bench_c5(args, dist, rank, world, inp=None):
 def bench_c2(args):
     """C2: one munin query, 100 leaf findings -> 1 root, greedy device contraction.  The evidence rows
     are the reference's own (tests/golden/munin_c2_rows.json: forward_sample(size=20, seed=0) of
-    pgmpy, the same 100 findings per row, so one compiled plan): step k queries row k % 20, and
-    after the timed region every row's root posterior is checked against the reference's value."""
+    pgmpy, the same 100 findings per row, so one compiled plan): step k queries row k % 20.  After the
+    timed region every row is checked against the reference on two outputs of the SAME compiled
+    program: the root posterior (one-hot on all 20 rows, so it pins the support) and the unnormalised
+    joint before normalize, P(root, findings) over the pruned model (1e-46 .. 1e-28: it pins the scale;
+    ExactInference.py:404-420, make_golden.py gen_munin_c2_mass) at rtol 1e-9."""
     import torch
 
     from pgmpy_amd.inference import VariableElimination
@@ -1322,47 +1325,76 @@ def bench_c2(args):
     runner, = ve._compiled.values()
     plan = runner.plan
     ps = plan.path_stats(1)
-    worst, ok = 0.0, True
+    prog = plan.__dict__.get("_q1", {}).get("joint", (None,))[0]
+    worst, worst_mass, ok = 0.0, 0.0, True
+    masses = []
     for row, ev in zip(g["rows"], rows):
         got = ve.query(q, ev, show_progress=False)
         want = np.asarray(row["root"]["values"], dtype=np.float64)
         x = np.asarray(got.values).ravel()
         ok &= bool(np.allclose(x, want, rtol=1e-6, atol=1e-12))
         worst = max(worst, float(np.max(np.abs(x - want))))
-    return {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
-            "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
-            "plan": {"kind": plan.kind, **ps},
-            "chain_tuning": [getattr(h[0], "chain_tuning", None) for h in plan.__dict__.get("_progs", {}).values()],
-            "achieved": {"GB/s": ps["bytes"] / dt / 1e9, "TFLOP/s": ps["flops"] / dt / 1e12,
-                         "note": "algorithmic bytes / flops of the executed plan (contraction.choose_path; SURVEY §8(d) C2) per query"},
-            "reference": {"value": 52.7, "unit": "s/query", "note": "pgmpy numpy path, survey container (not this host)"},
-            "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
-                    "same query/evidence variables); first_query_s includes pruning, planning and graph capture",
-            "data": "the reference's 20 forward-sampled munin rows (tests/golden/munin_c2_rows.json), step k = row k % 20",
-            "parity": {"ok": ok, "rows_checked": len(rows), "max_abs_err": worst, "rtol": 1e-6, "atol": 1e-12,
-                       "against": "reference root posteriors (tests/golden/munin_c2_rows.json)"},
-            "result": list(np.asarray(r.values))}
+        un = np.asarray(ve.query_unnormalized(q, ev).values, dtype=np.float64).ravel()
+        want_un = np.asarray(row["root_unnormalized"], dtype=np.float64)
+        ok &= bool(np.allclose(un, want_un, rtol=1e-9, atol=0))
+        worst_mass = max(worst_mass, float(np.max(np.abs(un - want_un)) / np.max(np.abs(want_un))))
+        masses.append(float(want_un.sum()))
+    ok &= len(ve._compiled) == 1  # the checked outputs came from the timed program
+    out = {"metric": "munin single-row query latency (C2)", "value": dt, "unit": "s/query",
+           "higher_is_better": False, "steps": args.steps, "warmup": args.warmup, "first_query_s": t_cold,
+           "plan": {"kind": plan.kind, **ps},
+           "launches_per_query": len(prog._direct) if prog is not None and prog._direct else None,
+           "dispatch": getattr(prog, "direct_note", None),
+           "roofline": {"bound": "latency (dependent launches; the executed plan's bytes take ~8 us at HBM peak)",
+                        "achieved": ps["bytes"] / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ps["bytes"] / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "tflops": ps["flops"] / dt / 1e12,
+                        "note": "algorithmic bytes / flops of the executed plan (contraction.choose_path; "
+                                "SURVEY §8(d) C2) per query over the wall time per query"},
+           "reference": {"value": float(np.mean([r["seconds"][-1] for r in g["rows"]])), "unit": "s/query",
+                         "note": "pgmpy's own VariableElimination.query on these 20 rows (opt_einsum shim, greedy; "
+                                 "make_golden.py gen_munin_c2_mass, 5 processes on the build container's 8-core "
+                                 "Xeon) - not this host"},
+           "note": "steady state: the evidence pattern's compiled plan is cached (new evidence values, "
+                   "same query/evidence variables); first_query_s includes pruning, planning and compiling",
+           "data": "the reference's 20 forward-sampled munin rows (tests/golden/munin_c2_rows.json), step k = row k % 20",
+           "parity": {"ok": ok, "rows_checked": len(rows), "max_abs_err": worst, "rtol": 1e-6, "atol": 1e-12,
+                      "mass_max_rel_err": worst_mass, "mass_rtol": 1e-9,
+                      "mass_range": [min(masses), max(masses)],
+                      "against": "reference root posteriors AND unnormalised root joints (tests/golden/munin_c2_rows.json), "
+                                 "both read from the timed program's outputs"},
+           "result": list(np.asarray(r.values))}
+    if not args.no_cpu_baseline:
+        # the oracle's prune + classic elimination (oracle.ve.eliminate: the build's elimination rule in
+        # numpy; its greedy_contract restates opt_einsum's greedy, which takes ~46 s per query here like
+        # the reference) on all 20 rows, one core
+        from oracle import ve as OVE
+        from oracle.network import load_network
+
+        net = load_network("munin")
+        t0 = time.perf_counter()
+        for ev in rows:
+            OVE.query(net, q, ev, contract=OVE.eliminate)
+        out["cpu_baseline"] = {"value": (time.perf_counter() - t0) / len(rows), "unit": "s/query", "cores": 1,
+                               "kind": "port", "sample": "the same 20 rows, numpy oracle: pruning + classic "
+                                                         "variable elimination in min-clique order (oracle.ve.eliminate)"}
+    return out
 
 
 def bench_c1(args):
-    """C1: alarm VariableElimination.query, single evidence rows (50 seeded patterns: 3 query vars,
-    5 evidence vars), device path (compiled per pattern) vs the numpy oracle on the host."""
+    """C1: alarm VariableElimination.query, single evidence rows: the reference's own 50 seeded patterns
+    (tests/golden/alarm_queries.json, SURVEY §8(d) C1: 3 query variables, 5 findings from
+    forward_sample(seed=1)), device path (compiled per pattern), every pattern's joint checked against
+    the reference after the timed region; the numpy oracle on the host beside it."""
     import torch
 
     from pgmpy_amd.inference import VariableElimination
     from pgmpy_amd.utils import get_example_model
-    from pgmpy_amd.utils.sampling import forward_sample_codes
 
+    with open(os.path.join(ROOT, "tests", "golden", "alarm_queries.json")) as f:
+        g = json.load(f)
+    pats = [(p["variables"], p["evidence"]) for p in g["patterns"]]
     m = get_example_model("alarm")
-    nodes_sorted = sorted(m.nodes())
-    rng = random.Random(1)
-    codes, nodes = forward_sample_codes(m, 50, seed=1)
-    pos = {v: i for i, v in enumerate(nodes)}
-    pats = []
-    for r in range(50):
-        pick = rng.sample(nodes_sorted, 8)
-        q, e = pick[:3], pick[3:]
-        pats.append((q, {v: m.states[v][codes[pos[v], r]] for v in e}))
     ve = VariableElimination(m)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -1377,27 +1409,43 @@ def bench_c1(args):
     reps = max(1, args.steps // 10)
     for _ in range(reps):
         for q, e in pats:
-            r = ve.query(q, e, show_progress=False)
+            ve.query(q, e, show_progress=False)
     torch.cuda.synchronize()
     warm = (time.perf_counter() - t0) / (reps * len(pats))
-    tuned = [getattr(h[0], "chain_tuning", None) for rn in ve._compiled.values()
-             for h in rn.plan.__dict__.get("_progs", {}).values()]
-    tuned = [t for t in tuned if t]
+    worst, ok = 0.0, True
+    for p in g["patterns"]:
+        r = ve.query(p["variables"], p["evidence"], show_progress=False)
+        got = np.asarray(r.values, dtype=np.float64).ravel()
+        want = np.asarray(p["joint"]["values"], dtype=np.float64)
+        ok &= list(r.variables) == list(p["joint"]["variables"]) and bool(np.allclose(got, want, rtol=1e-6, atol=1e-12))
+        worst = max(worst, float(np.max(np.abs(got - want))))
+    h = g["history_cvp_low"]
+    r = ve.query(["HISTORY"], {"CVP": "LOW"}, show_progress=False)
+    ok &= bool(np.allclose(np.asarray(r.values).ravel(), h["values"], rtol=1e-6, atol=1e-12))
+    direct = sum(bool(getattr(h_[0], "_direct", None)) for rn in ve._compiled.values()
+                 for h_ in rn.plan.__dict__.get("_q1", {}).values())
     out = {"metric": "alarm single-row query latency (C1)", "value": warm, "unit": "s/query",
-           "higher_is_better": False, "patterns": len(pats), "first_query_s": cold,
-           "chain_tuning": {"programs": len(tuned),
-                            "kept_chain": sum(t["chained_us"] <= t["per_level_us"] for t in tuned)},
-           "note": "value: compiled pattern plans cached (same query/evidence variables, new values)"}
+           "higher_is_better": False, "patterns": len(pats), "queries_timed": reps * len(pats),
+           "first_query_s": cold, "programs_on_aql_chain": direct,
+           "roofline": {"bound": "latency (a few dependent launches per query; bytes are a few KB)",
+                        "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None},
+           "note": "value: compiled pattern plans cached (same query/evidence variables, new values)",
+           "parity": {"ok": ok, "patterns_checked": len(pats) + 1, "max_abs_err": worst, "rtol": 1e-6,
+                      "atol": 1e-12, "against": "reference joints (tests/golden/alarm_queries.json) + "
+                                                "HISTORY|CVP=LOW"}}
     if not args.no_cpu_baseline:
         from oracle import ve as OVE
         from oracle.network import load_network
 
         net = load_network("alarm")
-        t0 = time.perf_counter()
-        for q, e in pats:
+        t0, n = time.perf_counter(), 0
+        while n < len(pats) or time.perf_counter() - t0 < 2.0:
+            q, e = pats[n % len(pats)]
             OVE.query(net, q, e)
-        out["cpu_baseline"] = {"value": (time.perf_counter() - t0) / len(pats), "unit": "s/query", "cores": 1,
-                               "kind": "port", "sample": "the same 50 patterns, numpy oracle"}
+            n += 1
+        out["cpu_baseline"] = {"value": (time.perf_counter() - t0) / n, "unit": "s/query", "cores": 1,
+                               "kind": "port", "sample": f"{n} queries over the same 50 patterns, numpy oracle "
+                                                         "(pruning + greedy contraction per call)"}
     # the oracle is a readable restatement (it re-prunes per call and contracts with plain einsum), not a
     # stand-in for pgmpy's speed here: the reference's own latency on C1 is quoted beside it
     out["reference"] = {"value": 0.43e-3, "unit": "s/query",
@@ -1406,8 +1454,27 @@ def bench_c1(args):
     return out
 
 
+def _c4_pmc_summary():
+    """The committed PMC summary of the C4 sweep (tools/c4_step_pmc.py: separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes over one 4,000-row replay, FETCH x2 per the MI355X guide): the newest round's."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "c4pmc_summary.json")),
+                   key=lambda p: (os.path.basename(os.path.dirname(p))[:3], os.path.getmtime(p)))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    return {"source": os.path.relpath(paths[-1], ROOT), "rows": d.get("rows"),
+            "fetch_bytes_x2": d.get("fetch_bytes_x2"), "write_bytes": d.get("write_bytes"),
+            "hbm_side_bytes": d.get("hbm_side_bytes"), "floor_bytes": d.get("floor_bytes"),
+            "ratio_to_floor": d.get("ratio_to_floor"), "ratio_to_step_bytes": d.get("ratio_to_step_bytes")}
+
+
 def bench_c4(args):
-    """C4: pathfinder batched BP calibration (min-fill JT), 4 leaf findings per row."""
+    """C4: pathfinder batched BP calibration (min-fill JT), 4 leaf findings per row.  value: one
+    calibration batch at a time (BatchedJunctionTree inflight=1, what BeliefPropagation.calibrate_batch
+    runs by default); `two_in_flight` the same batches with two in flight (calibrate_batch(inflight=2))."""
     import torch
 
     from pgmpy_amd.inference.bp_batch import BatchedJunctionTree
@@ -1418,52 +1485,79 @@ def bench_c4(args):
 
     m = get_example_model("pathfinder")
     jt = junction_tree_from_model(m)
-    # --c4-inflight k (default 2): k calibration batches in flight (BatchedJunctionTree inflight: own
-    # schedules and streams, round robin; batch j+1's first levels overlap batch j's last ones)
-    bjt = BatchedJunctionTree(jt, inflight=args.c4_inflight)
+    bjt = BatchedJunctionTree(jt, inflight=1)
     n = args.rows
     ev, ev_vars, _, _ = leaf_findings_codes(m, n, per_row=4, seed=7)
     d = upload_codes(ev)
-    for _ in range(max(1, args.warmup) * bjt.inflight):
-        bjt.calibrate_codes(d, ev_vars, n)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cal = bjt.calibrate_codes(d, ev_vars, n)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    one = None
-    if bjt.inflight > 1:  # the same steps with one batch in flight (shares lane 0's compiled schedule)
-        bjt.inflight, bjt._lane = 1, 0
-        for _ in range(max(1, args.warmup)):
+
+    def rate(inflight):
+        bjt.inflight, bjt._lane = inflight, 0
+        for _ in range(max(1, args.warmup) * inflight):
             bjt.calibrate_codes(d, ev_vars, n)
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
+        t0 = time.perf_counter()
         for _ in range(args.steps):
-            bjt.calibrate_codes(d, ev_vars, n)
+            c = bjt.calibrate_codes(d, ev_vars, n)
         torch.cuda.synchronize()
-        one = n * args.steps / (time.perf_counter() - t1)
-        bjt.inflight = args.c4_inflight
+        return (time.perf_counter() - t0) / args.steps, c
+
+    dt, cal = rate(1)
+    two = None
+    if args.c4_inflight > 1:  # lane 0's compiled schedule is shared with the one-at-a-time run
+        dt2, _ = rate(args.c4_inflight)
+        two = {"value": n / dt2, "unit": "calibrations/s", "inflight": args.c4_inflight, "ms_per_step": dt2 * 1e3,
+               "note": "the same calibration batches with this many in flight (own schedules and streams, "
+                       "round robin; BeliefPropagation.calibrate_batch(inflight=k))"}
+        bjt.inflight, bjt._lane = 1, 0
     bpc = bjt.bytes_per_calibration()
     sch = bjt.schedule(n, ev_vars, "marginalize", False)
     parity = _c4_parity(m, cal, ev, ev_vars, n)
     step_bytes = sum(sch.prog.step_bytes) / n if sch.prog.step_bytes else None
-    return {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
-            "rows_per_step": n, "ms_per_step": dt * 1e3, "bytes_per_calibration": bpc,
-            "achieved_GBps": bpc * n / dt / 1e9, "frac_of_8TBps": bpc * n / dt / 1e9 / HBM_PEAK_GBS,
-            "executed_step_bytes_per_calibration": step_bytes,
-            "executed_step_GBps": step_bytes * n / dt / 1e9 if step_bytes else None,
-            "reference_schedule_bytes_per_calibration": bjt.reference_bytes_per_calibration(),
-            "note": "bytes_per_calibration: every belief written once + separator messages / sigma' written and "
-                    "read once (this schedule's floor); executed_step_bytes: the sum over the launched steps of "
-                    "every tensor each reads or writes (operands re-read by the collect and distribute passes, "
-                    "aggregates); the reference schedule's figure reads and writes every belief in both passes "
-                    "(SURVEY §8(d) C4)",
-            "cliques": len(bjt.cliques), "inflight": bjt.inflight,
-            "one_in_flight": {"value": one, "unit": "calibrations/s",
-                              "note": "the same calibration batches one at a time (BatchedJunctionTree inflight=1)"}
-            if one is not None else None,
-            "parity": parity}
+    out = {"metric": "pathfinder BP calibrations/s (C4)", "value": n / dt, "unit": "calibrations/s",
+           "higher_is_better": True, "rows_per_step": n, "steps": args.steps, "ms_per_step": dt * 1e3,
+           "inflight": 1,
+           "roofline": {"bound": "hbm", "achieved": bpc * n / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": bpc * n / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "bytes_per_calibration": bpc,
+                        "executed_step_bytes_per_calibration": step_bytes,
+                        "executed_step_GBps": step_bytes * n / dt / 1e9 if step_bytes else None,
+                        "executed_step_frac": step_bytes * n / dt / 1e9 / HBM_PEAK_GBS if step_bytes else None,
+                        "pmc": _c4_pmc_summary(),
+                        "note": "achieved: this schedule's floor (every belief written once, every separator "
+                                "message / sigma' written and read once: 8 (sum|C| + 4 sum|S|)) over the wall time "
+                                "per calibration; executed_step_bytes: every tensor each launched step reads or "
+                                "writes; pmc: memory-side bytes of one 4,000-row replay (committed rocprofv3 "
+                                "passes) against that floor"},
+           "reference_schedule_bytes_per_calibration": bjt.reference_bytes_per_calibration(),
+           "reference_schedule_note": "SURVEY §8(d) C4's 8 (4 sum|C| + 4 sum|S|) counts every belief read and "
+                                      "written in both passes; this schedule does not move those bytes, so that "
+                                      "figure over this rate is not an achieved bandwidth",
+           "cliques": len(bjt.cliques),
+           "two_in_flight": two,
+           "parity": parity}
+    if not args.no_cpu_baseline:
+        # the oracle's calibration (oracle/bp.py: findings as 0/1 indicators, one collect + one
+        # distribute sweep of _update_beliefs) row by row for ~10 s, one core
+        from oracle import bp as OBP
+        from oracle.network import load_network
+        from pgmpy_amd.inference.EliminationOrder import min_fill_decomposition
+
+        net = load_network("pathfinder")
+        bags, edges = min_fill_decomposition(m)
+        pots = OBP.initial_potentials(net, bags)
+        t0, done = time.perf_counter(), 0
+        while done < n and (done < 2 or time.perf_counter() - t0 < args.cpu_seconds_c4):
+            r = done
+            e = {v: net.states[v][int(ev[j, r])] for j, v in enumerate(ev_vars) if ev[j, r] != 255}
+            OBP.calibrate(bags, edges, OBP.apply_evidence(net, pots, bags, e))
+            done += 1
+        out["cpu_baseline"] = {"value": done / (time.perf_counter() - t0), "unit": "calibrations/s", "cores": 1,
+                               "kind": "port", "sample": f"the first {done} rows of the same batch, numpy oracle "
+                                                         "(oracle/bp.py calibrate), one row at a time"}
+    out["reference"] = {"value": 1 / 1.8, "unit": "calibrations/s",
+                        "note": "pgmpy BeliefPropagation(jt).calibrate() on this junction tree, 1.66-1.96 s, survey "
+                                "container (SURVEY §6) - not this host"}
+    return out
 
 
 def _c4_parity(m, cal, ev, ev_vars, n):
@@ -1485,6 +1579,33 @@ def _c4_parity(m, cal, ev, ev_vars, n):
         return {"ok": False, "rows_checked": len(rows), "error": str(e)[:400]}
 
 
+def subconfigs(args):
+    """BASELINE.json configs[0], [1] and [3] as sub-objects of the default (C3) line at N = 1, each run
+    after the C3 window with its own timing, roofline, parity and same-host one-core CPU baseline
+    (the driver's own run measures them).  Step counts are fixed here so the line's
+    total stays a few minutes whatever --steps the driver passes."""
+    import copy
+
+    import torch
+
+    out = {}
+    for name, fn, over in (("c1", bench_c1, dict(steps=100, warmup=5)),
+                           ("c2", bench_c2, dict(steps=400, warmup=40)),
+                           ("c4", bench_c4, dict(steps=20, warmup=3, rows=4000))):
+        a = copy.copy(args)
+        vars(a).update(over)
+        t0 = time.perf_counter()
+        try:
+            out[name] = fn(a)
+        except Exception as e:  # reported, never silently dropped; the headline stands on its own
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+        out[name]["bench_s"] = round(time.perf_counter() - t0, 2)
+        gc.collect()
+        torch.cuda.empty_cache()
+        log(f"[sub] {name} {out[name].get('value')} ({out[name]['bench_s']} s)")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1501,7 +1622,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c4-inflight", type=int, default=2,
-                    help="c4: calibration batches in flight (own schedules, own streams, round robin)")
+                    help="c4: also time this many calibration batches in flight (own schedules, own streams, "
+                         "round robin; the headline is one at a time)")
+    ap.add_argument("--cpu-seconds-c4", type=float, default=10.0, help="c4: seconds of oracle calibrations")
+    ap.add_argument("--no-subconfigs", action="store_true",
+                    help="c3 at N=1: skip the c1 / c2 / c4 sub-objects (configs[0], [1], [3])")
     ap.add_argument("--no-api-e2e", action="store_true", help="c3: skip the public-API DataFrame rate")
     ap.add_argument("--no-c5", action="store_true",
                     help="c3: skip the C5 sub-object (1M rows split over the ranks: host delivery, MAP, RCCL gather)")
@@ -1544,6 +1669,8 @@ def main():
     dist, rank, world = dist_setup(args.gpus, args.dist_backend)
     if args.workload == "c3":
         res = bench_c3(args, dist, rank, world)
+        if world == 1 and not args.no_subconfigs:
+            res.update(subconfigs(args))
     elif args.workload == "c5":
         res = (bench_c5_host if args.c5_delivery == "host" else bench_c5)(args, dist, rank, world)
     elif args.workload == "c2":

@@ -552,14 +552,20 @@ int pgm_dq_bound_destroy(void *dbound);
  * plain Program, pgmpy/inference/ExactInference.py:349-440, C1 / C2).  pgm_dq_bind_pm re-binds one
  * plan-specialised launch (pgm_pm_bound_* handle: a fused product step, a merged level or a specialised
  * contraction batch) to the queue; pgm_dq_run_chain writes the n launches as one dependent chain (each
- * packet's barrier bit set unless independent[i] is 1 — launch i reads nothing launch i-1 writes — and
+ * packet's barrier bit set unless independent[i] is 1 — launch i reads nothing launch i-1 writes; the last
+ * packet always waits for every earlier one — and
  * agent-scope fences on every packet, the last releasing at system scope — inputs the host writes between
  * chains must be in coherent host memory (pgm_host_alloc), which the kernels read uncached; independent
  * may be NULL), rings the doorbell once and returns when the last has completed — the outputs are then
  * visible to the host.  Contract: no HIP work that writes the chain's inputs may be pending (the chain
- * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.  Not under
- * rocprofv3's queue interception (a chain crashed its interceptor; the Python side replays graphs there).
- * pgm_dq_profiling turns the queue's dispatch timestamps on or off (pgm_dq_timer_* need them). */
+ * does not drain the device; the host writes inputs through mapped memory).  At most 128 launches.  All n
+ * slots are reserved at once after every check that can fail (no half-written chain is left on the
+ * queue).  Refused (PGM_EINVAL) while a pgm_dq_timer span is open on the queue: only the last packet
+ * carries a completion signal, so there are no per-dispatch timestamps to report.
+ * pgm_dq_profiling turns the queue's dispatch timestamps on or off (pgm_dq_timer_* need them).  Leave it
+ * on for a queue a profiler may intercept (r06): a kernel-tracing tool reads every dispatch's timestamps
+ * from its own completion signals, which needs the queue's profiling enabled — r05 turned it off on the
+ * query queue and rocprofv3 crashed on the chain. */
 int pgm_dq_bind_pm(void *dq, void *pm_bound, void **dbound);
 int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n);
 int pgm_dq_profiling(void *dq, int32_t on);

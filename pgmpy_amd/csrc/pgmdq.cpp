@@ -49,6 +49,7 @@ struct DirectQueue {
   hsa_profile_t profile = HSA_PROFILE_BASE;
   hsa_queue_t *q = nullptr;
   std::vector<hsa_signal_t> ring;
+  std::vector<uint8_t> armed;  // per ring slot: the dispatch that last used it carried its signal
   uint64_t issued = 0;  // dispatches written so far
   uint64_t freq = 1;    // HSA system timestamp frequency (Hz)
   // fences: the first dispatch after bind/sync acquires at system scope (inputs written by HIP are
@@ -234,6 +235,7 @@ int pgm_dq_create(int hip_device, void **out) {
   (void)hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &dq->freq);
   if (!dq->freq) dq->freq = 1;
   dq->ring.reserve(kRing);
+  dq->armed.assign(kRing, 0);
   // completion signals without an interrupt event (HSA_AMD_SIGNAL_AMD_GPU_ONLY): the CP only writes
   // the value (and the profiling timestamps); the host polls it (an interrupt signal: +0.5 us per
   // dispatch, profiles/r02e_store_release_ab.json)
@@ -247,10 +249,9 @@ int pgm_dq_create(int hip_device, void **out) {
   return PGM_OK;
 }
 
-// the next ring signal (armed to 1) and queue slot; recycles the signal of dispatch n - kRing.  arm =
-// false: a packet without a completion signal (the inner packets of a chain): its ring signal is left
-// as it is (0: the slot's previous use completed, or never used)
-static int next_slot(DirectQueue *dq, hsa_signal_t *sig, void **slot, uint64_t *qidx, bool arm = true) {
+// the next ring signal (armed to 1) and queue slot; recycles the signal of dispatch n - kRing (chains
+// reserve their slots in pgm_dq_run_chain)
+static int next_slot(DirectQueue *dq, hsa_signal_t *sig, void **slot, uint64_t *qidx) {
   if (dq->queue_error.load()) return fail(PGM_EDEVICE, "direct queue: queue error %d", dq->queue_error.load());
   const uint64_t n = dq->issued;
   hsa_signal_t s = dq->ring[n % kRing];
@@ -264,7 +265,8 @@ static int next_slot(DirectQueue *dq, hsa_signal_t *sig, void **slot, uint64_t *
       dq->have_start = true;
     }
   }
-  if (arm) hsa_signal_store_relaxed(s, 1);
+  hsa_signal_store_relaxed(s, 1);
+  dq->armed[n % kRing] = 1;
   hsa_queue_t *q = dq->q;
   const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
   const auto t0 = std::chrono::steady_clock::now();
@@ -296,6 +298,7 @@ static void publish(DirectQueue *dq, void *slot, uint32_t header, uint64_t idx) 
 static int wait_tail(DirectQueue *dq) {
   const uint64_t from = std::max(dq->group_first, dq->issued >= kRing ? dq->issued - kRing : 0);
   for (uint64_t i = from; i < dq->issued; ++i) {
+    if (!dq->armed[i % kRing]) continue;  // an inner chain packet: no signal (its chain's last one covers it)
     const int rc = wait_zero(dq, dq->ring[i % kRing]);
     if (rc != PGM_OK) return rc;
   }
@@ -518,12 +521,17 @@ int pgm_dq_launch_group(void *const *dbounds, int32_t n) {
 }
 
 // a dependent chain (a compiled program's steps): every packet waits for the ones before it (barrier bit;
-// not on a packet flagged independent of its predecessor — the parts of one split level) and fences at
-// agent scope, so each reads what the earlier ones wrote; the last releases at system scope (outputs the
-// host reads in mapped memory; inputs it writes there are coherent host memory, read uncached).  The
-// packets are written together and the doorbell rung once; no HIP drain (the caller's contract: HIP
-// work that produced the inputs completed before).  Waits for the chain's last packet outside the
-// queue lock, so other threads' chains queue behind it meanwhile.
+// not on a packet flagged independent of its predecessor — the parts of one split level — except the
+// last, which always waits, so its completion signal and system-scope release cover the whole chain) and
+// fences at agent scope, so each reads what the earlier ones wrote; the last releases at system scope
+// (outputs the host reads in mapped memory; inputs it writes there are coherent host memory, read
+// uncached).  The packets are written together and the doorbell rung once; no HIP drain (the caller's
+// contract: HIP work that produced the inputs completed before).  Waits for the chain's last packet
+// outside the queue lock, so other threads' chains queue behind it meanwhile.
+//
+// Everything that can fail is checked before the first slot is reserved (queue error, the timer, the
+// ring signal of the last packet, room for all n packets), so a failure never leaves reserved slots
+// without a valid header in front of the packet processor.
 int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n) {
   if (!dbounds || n <= 0) return fail(PGM_EINVAL, "dq_run_chain: empty chain");
   if (n > (int32_t)(kRing / 2)) return fail(PGM_EINVAL, "dq_run_chain: %d launches > %d per chain", n, (int)(kRing / 2));
@@ -537,19 +545,35 @@ int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n
   hsa_signal_t last{};
   {
     std::lock_guard<std::mutex> lk(dq->mu);
-    uint64_t last_idx = 0;
+    if (dq->queue_error.load()) return fail(PGM_EDEVICE, "direct queue: queue error %d", dq->queue_error.load());
+    // only the last packet carries a completion signal, so a timer span (dispatch timestamps per ring
+    // signal) cannot cover a chain: refuse rather than report stale timestamps
+    if (dq->timing) return fail(PGM_EINVAL, "dq_run_chain: a pgm_dq_timer span is open on this queue");
+    const uint64_t first = dq->issued, last_n = first + (uint64_t)n - 1;
+    // the last packet's ring signal: its previous use (dispatch last_n - kRing) must have completed
+    last = dq->ring[last_n % kRing];
+    if (last_n >= kRing) {
+      const int rc = wait_zero(dq, last);
+      if (rc != PGM_OK) return rc;
+    }
+    // room for all n packets before any is reserved
+    hsa_queue_t *q = dq->q;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hsa_queue_load_write_index_relaxed(q) + (uint64_t)n - hsa_queue_load_read_index_scacquire(q) > q->size) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kWaitLimitS)
+        return fail(PGM_EDEVICE, "direct queue: no room for a %d-packet chain for %.0f s", n, kWaitLimitS);
+    }
+    hsa_signal_store_relaxed(last, 1);
+    // one reservation of n slots (single-producer queue: the caller holds dq->mu)
+    const uint64_t idx0 = hsa_queue_add_write_index_relaxed(q, (uint64_t)n);
     for (int32_t i = 0; i < n; ++i) {
       const DirectBound *db = (const DirectBound *)dbounds[i];
-      hsa_signal_t sig;
-      void *slot;
-      uint64_t idx;
+      const uint64_t idx = idx0 + (uint64_t)i;
+      void *slot = (char *)q->base_address + (idx & (q->size - 1)) * 64;
       // only the last packet signals its completion: a signal on every packet lengthened each dependent
       // launch by ~1 us (C2, 20 launches: 0.123 vs 0.104 ms/query, profiles/r05t/); the queue's read
       // index guards the slots of the others
-      const bool signal = i == n - 1;
-      const int rc = next_slot(dq, &sig, &slot, &idx, signal);
-      if (rc != PGM_OK) return rc;
-      if (!signal) sig.handle = 0;
+      const bool is_last = i == n - 1;
       hsa_kernel_dispatch_packet_t *pkt = (hsa_kernel_dispatch_packet_t *)slot;
       pkt->workgroup_size_x = (uint16_t)db->wg;
       pkt->workgroup_size_y = 1;
@@ -563,25 +587,33 @@ int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n
       pkt->kernel_object = db->kernel_object;
       pkt->kernarg_address = db->kernarg;
       pkt->reserved2 = 0;
-      pkt->completion_signal = sig;
+      pkt->completion_signal.handle = is_last ? last.handle : 0;
       // every packet acquires at agent scope, the first one too: the inputs the host writes between chains live
       // in coherent (fine-grained) host memory the kernels read uncached, so no system-scope acquire (which
       // also dropped the CPT tables from L2 each query) is needed — C2 0.106 -> 0.103 ms, C1 0.043 -> 0.040
       // (profiles/r05an/); the last packet still releases at system scope for the host's reads
       const uint16_t acq = (uint16_t)HSA_FENCE_SCOPE_AGENT;
-      const uint16_t rel = i == n - 1 ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : (uint16_t)HSA_FENCE_SCOPE_AGENT;
+      const uint16_t rel = is_last ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : (uint16_t)HSA_FENCE_SCOPE_AGENT;
+      const bool barrier = i == 0 || is_last || !independent || !independent[i];
       __atomic_store_n((uint32_t *)slot,
                        header_word(HSA_PACKET_TYPE_KERNEL_DISPATCH, acq, rel,
-                                   (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS),
-                                   i == 0 || !independent || !independent[i]),
+                                   (uint16_t)(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS), barrier),
                        __ATOMIC_RELEASE);
-      if (i == 0) dq->group_first = dq->issued;
-      dq->last_kernel = dq->issued;
-      dq->issued += 1;
-      last = sig;
-      last_idx = idx;
+      dq->armed[(first + (uint64_t)i) % kRing] = is_last ? 1 : 0;
+      // the doorbell never covers the end of the ring: ring it on the last slot before the wrap as
+      // well.  A profiler's intercept queue (rocprofv3 --kernel-trace) hands the packets one doorbell
+      // covers to its interceptor as ONE contiguous array starting at the first new slot; a run that
+      // wraps is read past the end of the ring.  r06a's trace of C2 (20 packets per chain on a
+      // 4,096-slot queue) died with SIGSEGV at the page after the proxy ring, in the HSA runtime called
+      // from this doorbell store, on the 205th chain — the first whose slots wrap (slots 4,080..4,099);
+      // producers that ring once per packet (HIP, pgm_dq_launch) never hand it a wrapping run.
+      if (!is_last && ((idx + 1) & (q->size - 1)) == 0)
+        hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
     }
-    hsa_signal_store_screlease(dq->q->doorbell_signal, (hsa_signal_value_t)last_idx);
+    dq->group_first = first;
+    dq->last_kernel = last_n;
+    dq->issued = last_n + 1;
+    hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx0 + (uint64_t)n - 1));
     dq->need_release = false;  // the last packet released at system scope
     dq->fresh = true;
   }
@@ -631,6 +663,7 @@ int pgm_dq_timer_stop_ticks(void *handle, uint64_t *start, uint64_t *end, uint64
   hsa_amd_profiling_dispatch_time_t te{};
   const uint64_t from = std::max(std::max(dq->group_first, dq->t_first), dq->issued >= kRing ? dq->issued - kRing + 1 : 0);
   for (uint64_t i = from; i <= dq->last_kernel; ++i) {
+    if (!dq->armed[i % kRing]) continue;
     hsa_amd_profiling_dispatch_time_t t;
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
     te.end = std::max(te.end, t.end);
@@ -640,6 +673,7 @@ int pgm_dq_timer_stop_ticks(void *handle, uint64_t *start, uint64_t *end, uint64
   dq->disp_ticks = dq->disp_n = 0;
   const uint64_t lo = std::max(dq->t_first, dq->issued >= kRing ? dq->issued - kRing : 0);
   for (uint64_t i = lo; i <= dq->last_kernel && i < dq->issued; ++i) {
+    if (!dq->armed[i % kRing]) continue;
     hsa_amd_profiling_dispatch_time_t t;
     HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
     if (t.end > t.start) {

@@ -220,7 +220,7 @@ class VariableElimination(Inference):
                                                 elimination_order=elimination_order, joint=joint,
                                                 show_progress=show_progress)
 
-    def _query_compiled(self, variables, evidence, joint, ek=None):
+    def _query_compiled(self, variables, evidence, joint, ek=None, unnorm=False):
         """query() for a Bayesian network with the greedy order, through a compiled evidence-pattern
         plan (pgmpy_amd.inference.plan.PatternPlan) cached per (query variables, evidence
         variables): pruning (inference/base.py:154-212), the evidence slice, the greedy contraction
@@ -270,13 +270,18 @@ class VariableElimination(Inference):
             codes = None
         if codes is None:
             codes = [model.get_cpds(v).get_state_no(v, evidence[v]) for v in ev_vars]
-        vals = runner.run(codes)
+        if unnorm:
+            vals, un = runner.run(codes, unnorm=True)
+        else:
+            vals = runner.run(codes)
         # state tables of the query variables, taken once per runner like the code tables above
         qtabs = runner.__dict__.get("_query_tables")
         if qtabs is None:
             from ..utils.state_name import StateTable
 
             qtabs = runner._query_tables = {v: StateTable(model.get_cpds(v).state_names[v]) for v in variables}
+        if unnorm:
+            return DiscreteFactor._trusted(variables, plan.cards, un, qtabs)
         if joint:
             return DiscreteFactor._trusted(variables, plan.cards, vals, qtabs)
         res = {}
@@ -284,6 +289,28 @@ class VariableElimination(Inference):
             a = plan.acc_off[i]
             res[v] = DiscreteFactor._trusted([v], [plan.cards[i]], vals[a:a + plan.cards[i]], qtabs)
         return res
+
+    @E.serialized
+    def query_unnormalized(self, variables, evidence=None):
+        """The joint over `variables` that query() divides by its mass, as a DiscreteFactor: the
+        reference's contract result (ExactInference.py:404-406) before normalize (L420), i.e. the
+        sum-product of the pruned model's evidence-sliced CPDs (inference/base.py:154-212).  It is
+        an output of the same compiled single-query program query() replays (one more copy job in its
+        last launch), so a query's scale is checkable, not only its support.  Bayesian networks,
+        greedy order, evidence variables of < 255 states (the compiled path)."""
+        evidence = dict(evidence) if evidence is not None else dict()
+        if not isinstance(self.model, DiscreteBayesianNetwork):
+            raise ValueError("query_unnormalized: Bayesian networks only (other models' query() is unnormalised)")
+        common = set(evidence).intersection(variables)
+        if common:
+            raise ValueError(f"Can't have the same variables in both `variables` and `evidence`. "
+                             f"Found in both: {common}")
+        for v in itertools.chain(variables, evidence):
+            if v not in self.model:
+                raise ValueError(f"{v} not in the model")
+        if any(self.model.get_cardinality(v) >= N.PGM_EV_MISSING for v in evidence):
+            raise ValueError("query_unnormalized: evidence variables of 255+ states are not on the compiled path")
+        return self._query_compiled(list(variables), evidence, True, unnorm=True)
 
     @E.serialized
     def max_marginal(self, variables=None, evidence=None, elimination_order="MinFill", show_progress=True):
@@ -620,15 +647,25 @@ class BeliefPropagation(Inference):
         return final
 
     @E.serialized_instance
-    def calibrate_batch(self, evidence, operation="marginalize"):
+    def calibrate_batch(self, evidence, operation="marginalize", inflight=1):
         """Batched calibration: one calibration per evidence row.
 
         evidence: DataFrame (state names, NaN = unobserved).  Returns a
         pgmpy_amd.inference.bp_batch.BatchedCalibration with per-row clique
-        beliefs and marginals on the device."""
+        beliefs and marginals on the device.  The compiled schedules live as long as this object's
+        junction tree (one BatchedJunctionTree per tree and `inflight`).  inflight=k: up to k
+        calibrations stay in flight across calls (own schedules and streams, round robin), so the
+        next call's first levels overlap this one's last; a returned calibration stays valid for the
+        next k - 1 calls."""
         from .bp_batch import BatchedJunctionTree
 
-        return BatchedJunctionTree(self.junction_tree).calibrate_frame(evidence, operation=operation)
+        cache = self.__dict__.setdefault("_batched", {})
+        key = (id(self.junction_tree), int(inflight))
+        hit = cache.get(key)
+        if hit is None or hit.jt is not self.junction_tree:
+            cache.clear()
+            hit = cache[key] = BatchedJunctionTree(self.junction_tree, inflight=inflight)
+        return hit.calibrate_frame(evidence, operation=operation)
 
 
 class BeliefPropagationWithMessagePassing(Inference):

@@ -440,6 +440,8 @@ class BatchedJunctionTree:
             st = self._lane_streams[lane] = torch.cuda.Stream()
         # after what the caller queued: the codes' producer, and its reads of this lane's previous results
         st.wait_stream(caller)
+        if hasattr(codes, "record_stream"):  # the caller may drop its codes tensor before the lane reads it
+            codes.record_stream(st)
         with torch.cuda.stream(st):
             cal = sch.run(codes)
             if err is not None:
@@ -468,10 +470,16 @@ class BatchedJunctionTree:
         return codes, ev_vars
 
     def calibrate_frame(self, df, operation="marginalize"):
+        """One calibration per row of df (state names; NaN = unobserved).  encode() has already
+        rejected unknown states, so the codes are in range; one at a time (inflight 1) the device's
+        range flag is read back as well, k in flight skips that synchronisation (it would serialise
+        the lanes)."""
         from .batch import download, upload_codes
 
         codes, ev_vars = self.encode(df)
         d = upload_codes(codes)
+        if self.inflight > 1:
+            return self.calibrate_codes(d, ev_vars, len(df), operation, marginals=True)
         sch = self.schedule(len(df), ev_vars, operation)
         cal = sch.run(d)
         if int(download(sch.err)[0]) != 0:

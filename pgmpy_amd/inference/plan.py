@@ -553,6 +553,13 @@ class PatternPlan:
             bufs["joint"] = out_buf("joint", [self.P, n])
             prog.contract(R.reshape(self.P, n), ["q", E.ROW], Z, [E.ROW], ["q", E.ROW], combine="div_raw",
                           out=bufs["joint"])
+        if host_io:
+            # the single-query program also hands out the joint BEFORE normalisation (the reference's
+            # contract result, ExactInference.py:404-406, ahead of normalize at L420): one more job of
+            # this last batch, no extra launch; query_one(..., unnorm=True) returns it
+            bufs["unnorm"] = out_buf("unnorm", [self.P, n])
+            prog.contract(R.reshape(self.P, n), ["q", E.ROW], None, None, ["q", E.ROW], combine="copy",
+                          out=bufs["unnorm"])
         prog.end_batch()
         if "map" in outs:
             bufs["map"] = torch.empty(n, dtype=torch.int32, device=dev)
@@ -588,11 +595,12 @@ class PatternPlan:
         for n in {min(chunk, n_rows - c0) for c0 in range(0, n_rows, chunk)}:
             self.prepare_steps(n, outs)
 
-    def query_one(self, codes, key, stream=None):
+    def query_one(self, codes, key, stream=None, unnorm=False):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v, already checked
         against the state names on the host) through the steps program whose codes and result live in
         host memory the kernels access directly: fill the codes, one graph launch, one synchronize.
-        Returns a new fp64 ndarray (`key` "marg" or "joint")."""
+        Returns a new fp64 ndarray (`key` "marg" or "joint"); with unnorm=True the pair (that, the
+        unnormalised joint [P] the same program computed before dividing by its mass)."""
         L = N.lib()
         with self._lock:
             q1 = self.__dict__.get("_q1")  # key -> (program, host buffers) of the one-row host-io program
@@ -617,6 +625,8 @@ class PatternPlan:
                 s = N.stream_handle(stream)
                 prog.run(stream)
                 N.check(L.pgm_stream_sync_spin(s), "stream_sync_spin")  # latency-bound: poll, don't block
+            if unnorm:
+                return host[key].array.reshape(-1).copy(), host["unnorm"].array.reshape(-1).copy()
             return host[key].array.reshape(-1).copy()
 
     def _run_steps(self, codes, ld, row0, n_rows, out, err):
@@ -690,15 +700,16 @@ class QueryRunner:
         self.lock = threading.Lock()
         self.key = "joint" if joint else "marg"
 
-    def run(self, codes):
+    def run(self, codes, unnorm=False):
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:
-        the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]."""
+        the normalised joint [P] (C-order over plan.variables) or the marginals [n_acc]; with
+        unnorm=True also the unnormalised joint [P] of the same run (PatternPlan.query_one)."""
         # the program is built and captured before this runner's lock is taken (engine.DeviceLock)
         if not self.__dict__.get("_prepared"):
             self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
             self._prepared = True
         with self.lock:
-            return self.plan.query_one(codes, self.key)
+            return self.plan.query_one(codes, self.key, unnorm=unnorm)
 
 
 class BoundRows:
@@ -899,8 +910,16 @@ class DirectQueue:
     @classmethod
     def for_queries(cls):
         """The current device's queue for compiled single queries (Program.bind_direct / run_direct; its
-        own queue, dispatch timestamps off), or None when PGM_QUERY_DIRECT=0, under rocprofv3, or when the
-        queue cannot be made (the queries then replay their HIP graphs)."""
+        own queue), or None when PGM_QUERY_DIRECT=0 or the queue cannot be made (the queries then replay
+        their HIP graphs).
+
+        r06: the queue keeps its dispatch timestamps ON.  r05 switched them off here
+        (pgm_dq_profiling(q, 0)) and the chain then crashed rocprofv3, so queries bypassed the queue
+        under the profiler.  A kernel-tracing tool intercepts every queue, puts its own completion
+        signal on each dispatch and reads that dispatch's start/end with
+        hsa_amd_profiling_get_dispatch_time, which needs profiling enabled on the queue the packets run
+        on; turning it off on an intercepted queue takes away the timestamps the tool relies on.  Only a
+        chain's last packet carries a signal of ours, so the timestamps cost the chain nothing."""
         import torch
 
         if os.environ.get("PGM_QUERY_DIRECT", "1") == "0":
@@ -908,14 +927,8 @@ class DirectQueue:
         d = torch.cuda.current_device()
         q = cls._queries.get(d, False)
         if q is False:
-            if any(k.startswith("ROCPROF") for k in os.environ):
-                # under rocprofv3 the queue is intercepted and a chain (packets written together, one
-                # doorbell) crashed its interceptor: queries replay their graphs there (same kernels)
-                cls._queries[d] = None
-                return None
             try:
                 q = cls(d)
-                N.check(N.lib().pgm_dq_profiling(q._h, 0), "dq_profiling")
             except RuntimeError:
                 q = None
             cls._queries[d] = q

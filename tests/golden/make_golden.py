@@ -26,6 +26,7 @@ Fixture inventory (SURVEY.md §8(c) "Golden vectors"):
   munin_predict.npz            C3 template rows, MAP codes and marginals
   munin_c2_query.json          C2: 100 leaf findings -> 1 root posterior (row 0)
   munin_c2_rows.json           C2 on all 20 sampled rows: root + two joint=False sets
+                               (+ munin_c2_mass: the root query's unnormalised joint per row)
   pathfinder_bp.npz / .json    C4: min-fill JT + beliefs (checksums) + marginals
 """
 import argparse
@@ -635,6 +636,53 @@ def gen_munin_c2_rows(jobs=6, rows=20):
     _dump("munin_c2_rows.json", {"variables": q, "separate_variables": qms, "evidence_variables": E, "rows": res})
 
 
+def _c2_mass_worker(i):
+    """Row i's root query through the reference, recording what its contract call returns: the
+    pruned, evidence-sliced sum-product (ExactInference.py:404-406) BEFORE normalize (L420)."""
+    _setup()
+    import pgmpy.inference.ExactInference as XI
+    from pgmpy.inference import VariableElimination
+
+    m, samples, E, q, _ = _c2_pattern()
+    evidence = {v: str(samples.iloc[i][v]) for v in E}
+    seen = []
+    contract = XI.contract
+
+    def recording_contract(*a, **k):
+        r = contract(*a, **k)
+        seen.append(np.array(r, dtype=np.float64, copy=True))
+        return r
+
+    XI.contract = recording_contract
+    try:
+        t0 = time.time()
+        post = VariableElimination(m).query(q, evidence, show_progress=False)
+        dt = time.time() - t0
+    finally:
+        XI.contract = contract
+    assert len(seen) == 1, len(seen)
+    return {"row": i, "root_unnormalized": [float(x) for x in seen[0].ravel()],
+            "root": [float(x) for x in np.asarray(post.values).ravel()], "seconds": dt}
+
+
+def gen_munin_c2_mass(jobs=6):
+    """the C2 root posterior is one-hot on all 20 rows, so its normalised value pins
+    only the support.  Add to every row of munin_c2_rows.json the root query's unnormalised joint
+    (the reference's contract output before normalize: P(root, findings) over the pruned model,
+    inference/base.py:154-212 + ExactInference.py:349-406) as `root_unnormalized`."""
+    path = os.path.join(HERE, "munin_c2_rows.json")
+    with open(path) as f:
+        g = json.load(f)
+    with Pool(jobs) as pool:
+        res = pool.map(_c2_mass_worker, list(range(len(g["rows"]))), chunksize=1)
+    for r in res:
+        row = g["rows"][r["row"]]
+        assert np.allclose(r["root"], row["root"]["values"], rtol=1e-12, atol=0), r["row"]
+        row["root_unnormalized"] = r["root_unnormalized"]
+        row["seconds"].append(r["seconds"])
+    _dump("munin_c2_rows.json", g)
+
+
 # ----------------------------------------------------------------------------- Markov networks
 def _sorted_fac(phi):
     """A factor as {variables sorted, values aligned to them} (hash-order independent)."""
@@ -814,6 +862,7 @@ GENS = {
     "munin_predict": gen_munin_predict,
     "munin_c2": gen_munin_c2,
     "munin_c2_rows": gen_munin_c2_rows,
+    "munin_c2_mass": gen_munin_c2_mass,
 }
 
 if __name__ == "__main__":
@@ -829,6 +878,8 @@ if __name__ == "__main__":
             gen_munin_predict(a.munin_rows, a.jobs)
         elif name == "munin_c2_rows":
             gen_munin_c2_rows(min(a.jobs, 6))
+        elif name == "munin_c2_mass":
+            gen_munin_c2_mass(min(a.jobs, 6))
         else:
             GENS[name]()
         print(f"[{name}] {time.time() - t0:.1f}s")
