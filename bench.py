@@ -285,6 +285,11 @@ class Launcher:
             return ms if ms is not None else self.timer.stop_ms()
         spans = [q.timer_stop_ticks() for q in self.qs]  # one HSA system clock for every queue
         stats = [q.dispatch_stats() for q in self.qs]
+        # the raw per-dispatch timestamps behind the span (tools/c3_span_check.py recomputes the line's
+        # kernel_ms and frac from them): [queue, start tick, end tick] in issue order per queue
+        self.dispatch_times = {"freq": spans[0][2],
+                               "dispatches": [[qi, int(a), int(b)] for qi, q in enumerate(self.qs)
+                                              for a, b in q.dispatch_times()]}
         n = sum(c for _, c in stats)
         # each timed dispatch's own duration, averaged: the per-launch figure rocprofv3's kernel trace
         # reports (with several queues it includes the time the dispatch shares the GPU with others)
@@ -683,6 +688,9 @@ def bench_c3(args, dist, rank, world):
             # the timed dispatches' own durations averaged (queue timestamps): the per-launch number to
             # compare with the committed rocprofv3 kernel-trace average (profiles/*_kernel_stats.csv)
             "dispatch_avg_ms": getattr(launcher, "dispatch_avg_ms", None),
+            # every timed dispatch's own HSA timestamps ([queue, start, end] ticks at `freq` Hz): the span
+            # above is max(end) - min(start) over them (tools/c3_span_check.py recomputes frac from these)
+            "dispatch_times": getattr(launcher, "dispatch_times", None),
             # the batches' outputs + inputs (algorithmic bytes): the default 24 batches (343 MB) exceed
             # the MI355X's 256 MiB Infinity Cache (MALL), so a step's output lines are evicted to HBM
             # before its buffer comes round again and the achieved rate is an HBM rate; with a set

@@ -547,6 +547,10 @@ int pgm_dq_timer_stop_ticks(void *dq, uint64_t *start, uint64_t *end, uint64_t *
  * pgm_dq_timer_stop_ticks) and how many were summed (those still in the 256-signal ring) — the
  * per-launch duration a kernel trace reports, which exceeds span / launches when queues overlap */
 int pgm_dq_timer_dispatch_stats(void *dq, uint64_t *sum_ticks, uint64_t *count);
+/* r06: after a timer stop, each timed dispatch's own start / end (HSA system ticks, the frequency of
+ * pgm_dq_timer_stop_ticks) in issue order, at most cap of them (those still in the signal ring);
+ * *count = how many were written.  The raw timestamps behind the C3 line's span-based frac. */
+int pgm_dq_timer_dispatch_times(void *dq, uint64_t *start, uint64_t *end, int32_t cap, int32_t *count);
 int pgm_dq_bound_destroy(void *dbound);
 /* r05 (ABI 22): a compiled query's steps on the queue (VariableElimination.query through a captured
  * plain Program, pgmpy/inference/ExactInference.py:349-440, C1 / C2).  pgm_dq_bind_pm re-binds one

@@ -249,6 +249,8 @@ _SIGS = {
     "pgm_dq_run_chain": ([ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32],
                          ctypes.c_int),
     "pgm_dq_profiling": ([_P, ctypes.c_int32], ctypes.c_int),
+    "pgm_dq_timer_dispatch_times": ([_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -700,6 +700,30 @@ int pgm_dq_timer_dispatch_stats(void *handle, uint64_t *sum_ticks, uint64_t *cou
   return PGM_OK;
 }
 
+// after a timer stop: each timed dispatch's own (start, end) in HSA system ticks, in issue order — the
+// dispatches of the span still in the signal ring (the C3 line commits them so its span-based frac can
+// be recomputed from the raw timestamps, tools/c3_span_check.py)
+int pgm_dq_timer_dispatch_times(void *handle, uint64_t *start, uint64_t *end, int32_t cap, int32_t *count) {
+  DirectQueue *dq = (DirectQueue *)handle;
+  if (!dq || !count || (cap > 0 && (!start || !end))) return fail(PGM_EINVAL, "dq_timer_dispatch_times: null argument");
+  *count = 0;
+  std::lock_guard<std::mutex> lk(dq->mu);
+  if (dq->timing) return fail(PGM_EINVAL, "dq_timer_dispatch_times: timer still running");
+  if (!dq->profiling || dq->issued == dq->t_first) return PGM_OK;
+  const uint64_t lo = std::max(dq->t_first, dq->issued >= kRing ? dq->issued - kRing : 0);
+  int32_t k = 0;
+  for (uint64_t i = lo; i <= dq->last_kernel && i < dq->issued && k < cap; ++i) {
+    if (!dq->armed[i % kRing]) continue;
+    hsa_amd_profiling_dispatch_time_t t;
+    HSA_TRY(hsa_amd_profiling_get_dispatch_time(dq->agent, dq->ring[i % kRing], &t));
+    start[k] = t.start;
+    end[k] = t.end;
+    ++k;
+  }
+  *count = k;
+  return PGM_OK;
+}
+
 int pgm_dq_bound_destroy(void *dbound) {
   DirectBound *db = (DirectBound *)dbound;
   if (!db) return PGM_OK;

@@ -2511,7 +2511,19 @@ void pgmi_appendf(std::string &o, const char *fmt, ...) {
 // 100 k-row launch keep more CUs streaming than 98 x 1,024 once the outputs go to HBM instead of the
 // Infinity Cache; three interleaved repeats, 20 steps: 26.6 / 26.7 / 27.9 G rows/s against 27.3 / 25.1 /
 // 25.3 G at 512 (192: 27.0 / 26.7 / 26.0; 128: 25.7 / 25.6 / 26.6; 1,024: 25.5 / 24.7 / 25.5)
-static constexpr int jit_wg() { return 320; }
+// r06 (one 157-block launch never covers the 256 CUs): 192 — 261 blocks of 384 rows per
+// 100 k-row launch, every CU a block from each launch; three interleaved repeats at the driver's 20 steps
+// (profiles/r06b/): 26.29 / 26.82 / 26.04 G rows/s, frac 0.607 / 0.613 / 0.612, against 25.20 / 26.20 /
+// 25.74 G, frac 0.572 / 0.606 / 0.588 at 320; the 400-batch ring is unchanged (0.70-0.71).  A/B knob
+// PGM_ROWS_JIT_WG (a multiple of 64 in [64, 1024]), read once.
+static int jit_wg() {
+  static const int wg = [] {
+    const char *e = getenv("PGM_ROWS_JIT_WG");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 64 && v <= 1024 && v % 64 == 0) ? v : 192;
+  }();
+  return wg;
+}
 
 // output store form of the specialised kernels: write-through — 8-B relaxed agent-scope atomic stores /
 // 16-B buffer stores with the sc1 bit — so every output line goes past the XCD's L2 in the dispatch that

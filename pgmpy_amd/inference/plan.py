@@ -969,6 +969,17 @@ class DirectQueue:
                 "dq_timer_stop")
         return a.value, b.value, f.value
 
+    def dispatch_times(self, cap=4096):
+        """[(start, end)] ticks of each dispatch of the last timed span, in issue order
+        (pgm_dq_timer_dispatch_times; the frequency is timer_stop_ticks()'s third value)."""
+        import ctypes
+
+        a = (ctypes.c_uint64 * cap)()
+        b = (ctypes.c_uint64 * cap)()
+        n = ctypes.c_int32()
+        N.check(N.lib().pgm_dq_timer_dispatch_times(self._h, a, b, cap, ctypes.byref(n)), "dq_timer_dispatch_times")
+        return [(a[i], b[i]) for i in range(n.value)]
+
     def dispatch_stats(self):
         """(sum of the last timed span's per-dispatch durations in ticks, dispatches summed)."""
         import ctypes
