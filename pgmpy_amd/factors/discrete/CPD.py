@@ -4,12 +4,15 @@ A CPT P(X | U1..Uk) stored as a DiscreteFactor over [X, U1..Uk] (flat C-order,
 CPD.py:180-182).  normalize / marginalize / reduce renormalise columns; the
 column sums and the division run on the device (pgm_contract).
 """
+import logging
 import numbers
 
 import numpy as np
 
 from ... import engine as E
 from .DiscreteFactor import DiscreteFactor
+
+logger = logging.getLogger("pgmpy")
 
 
 class TabularCPD(DiscreteFactor):
@@ -117,6 +120,39 @@ class TabularCPD(DiscreteFactor):
         f.name_to_no = self.name_to_no.copy()
         f.no_to_name = self.no_to_name.copy()
         return f
+
+    def reorder_parents(self, new_order, inplace=True):
+        """The CPT with its parents (evidence) in `new_order` (CPD.py:598-727): the values transposed
+        on the device (one strided copy, pgm_contract).  inplace=True re-initialises the CPD over
+        [variable] + new_order and returns get_values() — as the reference does through
+        DiscreteFactor.__init__ without state names, so the state names become 0..card-1;
+        inplace=False returns the reordered 2-D values and leaves the CPD as it was."""
+        if (len(self.variables) <= 1 or (set(new_order) - set(self.variables))
+                or (set(self.variables[1:]) - set(new_order))):
+            raise ValueError("New order either has missing or extra arguments")
+        if list(new_order) == list(self.variables[1:]):
+            logger.warning("Same ordering provided as current")
+            return self.get_values()
+        card = dict(zip(self.variables, (int(c) for c in self.cardinality)))
+        A = self._d()
+        labels = list(self.variables)
+        out_labels = [self.variables[0]] + list(new_order)
+        moved = E.contract(A, labels, None, None, out_labels, combine="copy")
+        if inplace:
+            cardinality = [self.variable_card] + [card[v] for v in new_order]
+            DiscreteFactor.__init__(self, out_labels, cardinality, moved)
+            return self.get_values()
+        return E.to_host(moved).reshape(self.cardinality[0], int(np.prod([card[v] for v in new_order])))
+
+    def to_dataframe(self):
+        """The CPT as a DataFrame (CPD.py:336-410): one row per combination of the parents' states
+        (a MultiIndex named after them, parents in the CPD's order), one column per state of the
+        variable (columns named after it), each row a conditional distribution."""
+        import pandas as pd
+
+        idx = pd.MultiIndex.from_product([self.state_names[v] for v in self.variables], names=self.variables)
+        flat = pd.DataFrame({"probability": np.asarray(self._values_readonly()).ravel()}, index=idx)
+        return flat["probability"].unstack(self.variable)
 
     def is_valid_cpd(self):
         v = self._shape2d(self._values_readonly())  # internal read: does not expose the values

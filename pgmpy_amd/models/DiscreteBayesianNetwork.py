@@ -167,6 +167,48 @@ class DiscreteBayesianNetwork(nx.DiGraph):
             m.add_cpds(*[cpd.copy() for cpd in self.cpds])
         return m
 
+    @E.serialized
+    def get_state_probability(self, states):
+        """P(states) for a full or partial assignment {variable: state name}
+        (DiscreteBayesianNetwork.py:991-1041; same checks, same ValueError messages).
+
+        The reference sums the product of every CPD over every combination of the unassigned variables
+        (itertools.product: exponential in their number — alarm with 6 of 37 unassigned is ~500
+        combinations, munin is out of reach).  Here only the assigned variables' ancestors take part
+        (every other CPD sums to 1 over its own variable: barren), each CPD is sliced at the assigned
+        states as a strided view of its device values, and what is left is ONE planned contraction to
+        a scalar on the device (inference.contraction.contract_factors, the greedy-path machinery of
+        VariableElimination.query); CPDs fully inside the assignment contribute one host value each."""
+        self.check_model()
+        for var, state in states.items():
+            if var not in self.nodes():
+                raise ValueError(f"{var} not in the model.")
+            if state not in self.states[var]:
+                raise ValueError(f"State: {state} not define for {var}")
+        if not states:
+            return 1.0
+        from ..inference.contraction import contract_factors
+
+        anc = self._get_ancestors_of(list(states))
+        host = 1.0
+        ops = []
+        for node in self.nodes():
+            if node not in anc:
+                continue
+            cpd = self.get_cpds(node)
+            idx = {v: cpd.name_to_no[v][states[v]] for v in cpd.variables if v in states}
+            rest = [v for v in cpd.variables if v not in idx]
+            if not rest:
+                host *= float(cpd._values_readonly()[tuple(idx[v] for v in cpd.variables)])
+                continue
+            t = cpd._d()
+            if idx:
+                t = t[tuple(idx[v] if v in idx else slice(None) for v in cpd.variables)]
+            ops.append((t, rest))
+        if not ops:
+            return host
+        return host * float(E.to_host(contract_factors(ops, [])).reshape(-1)[0])
+
     # ------------------------------------------------------------------ d-separation (DAG.py)
     def _get_ancestors_of(self, nodes):
         if not isinstance(nodes, (list, tuple)):

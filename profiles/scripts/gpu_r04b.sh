@@ -1,5 +1,5 @@
 # round 4: new GPU tests (hazards, direct API path, pinned shard runs), the e2e stage profile, then
-# the C3 working-set experiment (tools/gpu_r04a.sh)
+# the C3 working-set experiment (profiles/scripts/gpu_r04a.sh)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 TAG=${1:-r04b}
@@ -19,4 +19,4 @@ for OUT in marginals map; do
   timeout -k 10 300 python bench.py --workload c5 --c5-output $OUT --steps 20 --warmup 5 > gpurun_out/${TAG}_c5_host_$OUT.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/${TAG}_c5_host_$OUT.json')); print('c5 host $OUT', round(d['value']/1e9,3), 'G rows/s', 'ms/step', round(d['ms_per_step'],3), 'kernel', round(d['kernel_ms'],4), 'copy', round(d['copy_ms'],3), 'GB/s', round(d['copy_GBps'],1), d['parity'])"
 done
-bash tools/gpu_r04a.sh r04a
+bash profiles/scripts/gpu_r04a.sh r04a

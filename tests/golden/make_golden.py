@@ -683,6 +683,74 @@ def gen_munin_c2_mass(jobs=6):
     _dump("munin_c2_rows.json", g)
 
 
+# ----------------------------------------------------------------------------- small API completion
+def gen_api_extras():
+    """DiscreteBayesianNetwork.get_state_probability (DiscreteBayesianNetwork.py:991-1041;
+    the reference enumerates every combination of the unassigned variables, so alarm cases leave at most
+    6 of its 37 unassigned), TabularCPD.reorder_parents (CPD.py:598-727) and to_dataframe (CPD.py:336-410)."""
+    from pgmpy.factors.discrete import TabularCPD
+
+    out = {"state_probability": [], "reorder_parents": [], "to_dataframe": []}
+    asia = _model("asia")
+    cases = [("asia", {"either": "no", "tub": "no", "xray": "yes", "bronc": "no"}),
+             ("asia", {"smoke": "yes"}), ("asia", {"lung": "yes", "dysp": "no"}),
+             ("asia", {v: str(asia.states[v][i % len(asia.states[v])]) for i, v in enumerate(sorted(asia.nodes()))})]
+    alarm = _model("alarm")
+    rng = random.Random(5)
+    from pgmpy.sampling import BayesianModelSampling
+
+    samples = BayesianModelSampling(alarm).forward_sample(size=4, seed=3, show_progress=False)
+    nodes = sorted(alarm.nodes())
+    for k in range(4):
+        keep = rng.sample(nodes, len(nodes) - (6 if k < 3 else 0))
+        row = samples.iloc[k]
+        cases.append(("alarm", {v: str(row[v]) for v in keep}))
+    for net, st in cases:
+        m = asia if net == "asia" else alarm
+        t0 = time.time()
+        p = m.get_state_probability(st)
+        out["state_probability"].append({"network": net, "states": st, "probability": float(p),
+                                         "seconds": time.time() - t0})
+        print(net, len(st), p)
+    errs = []
+    for st in ({"nope": "yes"}, {"smoke": "maybe"}):
+        try:
+            asia.get_state_probability(st)
+        except ValueError as e:
+            errs.append({"states": st, "error": "ValueError", "message": str(e)})
+    out["state_probability_errors"] = errs
+    # reorder_parents: the reference's docstring CPD and an alarm CPD with 4 parents, inplace and not
+    grade = dict(variable="grade", variable_card=3,
+                 values=[[0.1, 0.1, 0.0, 0.4, 0.2, 0.1], [0.3, 0.2, 0.1, 0.4, 0.3, 0.2], [0.6, 0.7, 0.9, 0.2, 0.5, 0.7]],
+                 evidence=["diff", "intel"], evidence_card=[2, 3])
+    big = alarm.get_cpds("CATECHOL")
+    for spec, order in ((grade, ["intel", "diff"]), (None, list(reversed(big.variables[1:])))):
+        for inplace in (False, True):
+            cpd = TabularCPD(**spec) if spec else big.copy()
+            before = {"variable": cpd.variable, "variable_card": int(cpd.variable_card),
+                      "values": np.asarray(cpd.get_values()).tolist(), "evidence": list(cpd.variables[1:]),
+                      "evidence_card": [int(c) for c in cpd.cardinality[1:]],
+                      "state_names": {k: [str(x) for x in v] for k, v in cpd.state_names.items()}}
+            r = cpd.reorder_parents(order, inplace=inplace)
+            out["reorder_parents"].append({
+                "cpd": before, "new_order": order, "inplace": inplace, "returned": np.asarray(r).tolist(),
+                "variables_after": list(cpd.variables), "cardinality_after": [int(c) for c in cpd.cardinality],
+                "values_after": np.asarray(cpd.values).ravel().tolist(),
+                "state_names_after": {k: [str(x) for x in v] for k, v in cpd.state_names.items()}})
+    try:
+        TabularCPD(**grade).reorder_parents(["intel"])
+    except ValueError as e:
+        out["reorder_parents_error"] = str(e)
+    for node in ("HISTORY", "CATECHOL", "HR"):
+        df = alarm.get_cpds(node).to_dataframe()
+        out["to_dataframe"].append({"node": node, "columns": [str(c) for c in df.columns],
+                                    "columns_name": str(df.columns.name),
+                                    "index_names": [str(n) for n in df.index.names],
+                                    "index": [[str(x) for x in (t if isinstance(t, tuple) else (t,))] for t in df.index],
+                                    "values": df.to_numpy().tolist()})
+    _dump("api_extras.json", out)
+
+
 # ----------------------------------------------------------------------------- Markov networks
 def _sorted_fac(phi):
     """A factor as {variables sorted, values aligned to them} (hash-order independent)."""
@@ -863,6 +931,7 @@ GENS = {
     "munin_c2": gen_munin_c2,
     "munin_c2_rows": gen_munin_c2_rows,
     "munin_c2_mass": gen_munin_c2_mass,
+    "api_extras": gen_api_extras,
 }
 
 if __name__ == "__main__":

@@ -132,3 +132,46 @@ def test_large_factor_ops(gpu):
     np.testing.assert_allclose(M.values, a.sum(axis=(1, 3, 5)), rtol=1e-11)
     N = A.normalize(inplace=False)
     np.testing.assert_allclose(N.values, a / a.sum(), rtol=1e-11)
+
+
+def test_api_extras_against_reference(gpu):
+    """VERDICT r05 #8 against the reference's own outputs (make_golden.py gen_api_extras):
+    DiscreteBayesianNetwork.get_state_probability (DiscreteBayesianNetwork.py:991-1041; asia incl. the
+    docstring's 0.02605122, alarm with 31 and 37 of 37 variables assigned) through the device contraction,
+    its ValueErrors; TabularCPD.reorder_parents (CPD.py:598-727) inplace and not, on the docstring CPD and
+    alarm's CATECHOL, including the reference's reset of the state names when inplace; to_dataframe
+    (CPD.py:336-410) on three alarm CPDs."""
+    import pandas as pd
+
+    from pgmpy_amd.factors.discrete import TabularCPD
+    from pgmpy_amd.utils import get_example_model
+
+    g = load_json("api_extras.json")
+    nets = {n: get_example_model(n) for n in ("asia", "alarm")}
+    for c in g["state_probability"]:
+        got = nets[c["network"]].get_state_probability(c["states"])
+        np.testing.assert_allclose(got, c["probability"], rtol=1e-12, atol=1e-300, err_msg=str(c["states"]))
+    for e in g["state_probability_errors"]:
+        with pytest.raises(ValueError, match=e["message"].split(":")[0]):
+            nets["asia"].get_state_probability(e["states"])
+    alarm = nets["alarm"]
+    for c in g["reorder_parents"]:
+        b = c["cpd"]
+        sn = {k: list(v) for k, v in b["state_names"].items()}
+        cpd = TabularCPD(b["variable"], b["variable_card"], b["values"], b["evidence"], b["evidence_card"],
+                         state_names=sn if b["variable"] != "grade" else {})
+        r = cpd.reorder_parents(c["new_order"], inplace=c["inplace"])
+        np.testing.assert_array_equal(np.asarray(r), np.asarray(c["returned"]))
+        assert list(cpd.variables) == c["variables_after"]
+        assert [int(x) for x in cpd.cardinality] == c["cardinality_after"]
+        np.testing.assert_array_equal(np.asarray(cpd.values).ravel(), np.asarray(c["values_after"]))
+        assert {k: [str(x) for x in v] for k, v in cpd.state_names.items()} == c["state_names_after"]
+    with pytest.raises(ValueError, match="New order either has missing or extra arguments"):
+        TabularCPD("grade", 3, [[0.1] * 6, [0.3] * 6, [0.6] * 6], ["diff", "intel"], [2, 3]).reorder_parents(["intel"])
+    for c in g["to_dataframe"]:
+        df = alarm.get_cpds(c["node"]).to_dataframe()
+        assert isinstance(df, pd.DataFrame)
+        assert [str(x) for x in df.columns] == c["columns"] and str(df.columns.name) == c["columns_name"]
+        assert [str(n) for n in df.index.names] == c["index_names"]
+        assert [[str(x) for x in (t if isinstance(t, tuple) else (t,))] for t in df.index] == c["index"]
+        np.testing.assert_array_equal(df.to_numpy(), np.asarray(c["values"]))
