@@ -468,6 +468,18 @@ int pgm_rows_shard_run(void *const *handles, int32_t n_shards, int32_t mode, con
  * missing-column pattern from those columns only (predict's per-row NaN handling,
  * pgmpy/models/DiscreteBayesianNetwork.py:862-878). */
 int pgm_host_any_negative_i8(const int8_t *const *cols, int32_t n_cols, int64_t n, uint8_t *out, int32_t threads);
+/* r06 (pgmhost.cpp, one persistent pool of at most 16 host threads): the same scan as a job fed column by
+ * column — begin (n rows, room for `capacity` columns), push column pointers as they become known (each
+ * push is scanned on the pool while the caller goes on), end (waits, out[j] = 1 when pushed column j holds a
+ * negative code; *n_cols = columns pushed; frees the job).  The caller keeps the columns alive until end.
+ * pgm_host_lut_map_u8: dst[j * ld + i] = luts[j][(uint8_t)src[j][i]] (luts[j] NULL: the byte itself), on
+ * the pool — the plan's evidence columns from category codes to state codes (state_name.py:71-84 per
+ * cell in the reference). */
+int pgm_host_scan_begin(int64_t n, int32_t capacity, int32_t threads, void **job);
+int pgm_host_scan_push(void *job, const int8_t *const *cols, int32_t count);
+int pgm_host_scan_end(void *job, uint8_t *out, int32_t *n_cols);
+int pgm_host_lut_map_u8(const int8_t *const *src, const uint8_t *const *luts, int32_t n_cols, int64_t n, uint8_t *dst,
+                        int64_t ld, int32_t threads);
 
 /* Resident ring of row batches (streaming predict_probability / predict): one launch of the
  * plan-specialised two-rows-per-lane kernel ("pgm_rows_ring") stays resident while the host publishes

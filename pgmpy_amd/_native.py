@@ -213,6 +213,11 @@ _SIGS = {
     "pgm_rows_shard_run": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.c_int64, _P, ctypes.c_int64, _P, _P], ctypes.c_int),
     "pgm_host_any_negative_i8": ([ctypes.POINTER(_P), ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int32], ctypes.c_int),
+    "pgm_host_scan_begin": ([ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_P)], ctypes.c_int),
+    "pgm_host_scan_push": ([_P, ctypes.POINTER(_P), ctypes.c_int32], ctypes.c_int),
+    "pgm_host_scan_end": ([_P, _P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "pgm_host_lut_map_u8": ([ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.c_int32, ctypes.c_int64, _P, ctypes.c_int64,
+                             ctypes.c_int32], ctypes.c_int),
     "pgm_rows_ring_create": ([_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64),
                               ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.POINTER(_P), ctypes.c_int64,
                               ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P, ctypes.POINTER(ctypes.c_void_p)],

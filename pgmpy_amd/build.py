@@ -14,6 +14,7 @@ ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "pgmhip.hip")
 SRC_DQ = os.path.join(HERE, "csrc", "pgmdq.cpp")  # direct AQL dispatch (host code, HSA runtime)
 SRC_PM = os.path.join(HERE, "csrc", "pgmpm.cpp")  # plan-specialised batched-BP steps (host code, hipRTC)
+SRC_HOST = os.path.join(HERE, "csrc", "pgmhost.cpp")  # DataFrame ingestion helpers (host threads only)
 INC = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "lib", "libpgmhip.so")
 ARCH = "gfx950"
@@ -28,13 +29,13 @@ def hipcc():
 
 def build(force=False, verbose=True, out=OUT, defines=()):
     """defines: extra -D macros (tools only, e.g. PGM_ROWS_TIMELINE into lib/libpgmhip_timeline.so)."""
-    deps = [SRC, SRC_DQ, SRC_PM, os.path.join(HERE, "csrc", "pgm_internal.h"), os.path.join(INC, "pgmhip.h")]
+    deps = [SRC, SRC_DQ, SRC_PM, SRC_HOST, os.path.join(HERE, "csrc", "pgm_internal.h"), os.path.join(INC, "pgmhip.h")]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", tmp, SRC, SRC_DQ, SRC_PM, "-lhiprtc", "-lhsa-runtime64"]
+           "-Wno-unused-result", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", tmp, SRC, SRC_DQ, SRC_PM, SRC_HOST, "-lhiprtc", "-lhsa-runtime64"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -3861,41 +3861,7 @@ int pgm_codes_remap(const int8_t *raw, int64_t ld_raw, int32_t n_cols, int64_t n
 // host-side scan (no device): for each of n_cols int8 code columns (n cells each), whether any cell is
 // negative (pandas Categorical NaN = -1).  Columns are split over up to `threads` host threads; each
 // column is OR-reduced 8 cells per 64-bit word and tested on the sign bits.
-int pgm_host_any_negative_i8(const int8_t *const *cols, int32_t n_cols, int64_t n, uint8_t *out, int32_t threads) {
-  if (n_cols < 0 || n < 0 || (n_cols > 0 && (!cols || !out))) return fail(PGM_EINVAL, "host_any_negative_i8: bad argument");
-  for (int32_t j = 0; j < n_cols; ++j)
-    if (!cols[j] && n > 0) return fail(PGM_EINVAL, "host_any_negative_i8: column %d is null", j);
-  auto scan = [&](int32_t lo, int32_t hi) {
-    for (int32_t j = lo; j < hi; ++j) {
-      const int8_t *c = cols[j];
-      const int64_t words = n / 8;
-      uint64_t acc = 0;
-      for (int64_t w = 0; w < words; ++w) {
-        uint64_t x;
-        memcpy(&x, c + 8 * w, 8);
-        acc |= x;
-      }
-      bool neg = (acc & 0x8080808080808080ull) != 0;
-      for (int64_t i = words * 8; i < n && !neg; ++i) neg = c[i] < 0;
-      out[j] = neg ? 1 : 0;
-    }
-  };
-  const int64_t work = (int64_t)n_cols * n;
-  int nt = std::max(1, std::min<int>(threads, (int)std::min<int64_t>(64, work / (1 << 20) + 1)));
-  nt = std::min(nt, std::max(1, n_cols));
-  if (nt == 1) {
-    scan(0, n_cols);
-    return PGM_OK;
-  }
-  std::vector<std::thread> pool;
-  const int32_t per = (n_cols + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t) {
-    const int32_t lo = t * per, hi = std::min(n_cols, lo + per);
-    if (lo < hi) pool.emplace_back(scan, lo, hi);
-  }
-  for (auto &th : pool) th.join();
-  return PGM_OK;
-}
+// pgm_host_any_negative_i8: pgmhost.cpp (r06: one persistent host thread pool)
 
 int pgm_sample_joint(const double *joint, int64_t ld, int64_t P, const int32_t *group, const double *u, int64_t n,
                      int32_t *out_idx, void *stream) {

@@ -38,7 +38,8 @@ class DeviceLock:
     `peak_readers` records the most threads ever inside at once (a test's evidence of overlap)."""
 
     def __init__(self):
-        self._cv = threading.Condition(threading.Lock())
+        self._mu = threading.Lock()
+        self._cv = threading.Condition(self._mu)
         self._readers = 0
         self._writer = None
         self._wdepth = 0
@@ -53,25 +54,38 @@ class DeviceLock:
         return t
 
     def acquire_shared(self):
-        me, t = threading.get_ident(), self._t()
-        with self._cv:
-            if t.n > 0 or self._writer == me:
-                t.n += 1
+        # r06: the uncontended path takes the plain mutex only (a nested hold not even that: its count is
+        # thread-local), and a release notifies only when a writer waits for the last reader — a compiled
+        # single query (C1 / C2) takes this pair once per call
+        t = self._tls
+        n = getattr(t, "n", 0)
+        if n > 0:
+            t.n = n + 1
+            return
+        me = threading.get_ident()
+        with self._mu:
+            if self._writer == me:
+                t.n = 1
+                if not hasattr(t, "counted"):
+                    t.counted = False
                 return
             while self._writer is not None or self._waiting_writers:
                 self._cv.wait()
             self._readers += 1
-            self.peak_readers = max(self.peak_readers, self._readers)
+            if self._readers > self.peak_readers:
+                self.peak_readers = self._readers
             t.n, t.counted = 1, True
 
     def release_shared(self):
-        t = self._t()
-        with self._cv:
-            t.n -= 1
-            if t.n == 0 and t.counted:
+        t = self._tls
+        n = t.n - 1
+        t.n = n
+        if n == 0 and t.counted:
+            with self._mu:
                 t.counted = False
                 self._readers -= 1
-                self._cv.notify_all()
+                if self._readers == 0 and self._waiting_writers:
+                    self._cv.notify_all()
 
     def acquire_exclusive(self):
         me, t = threading.get_ident(), self._t()

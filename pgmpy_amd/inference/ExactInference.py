@@ -48,6 +48,53 @@ def _tuple_getter(keys):
     return itemgetter(*keys)
 
 
+def _query_result(plan, variables, joint, vals, qtabs):
+    """query()'s answer from a compiled run's values: the normalised joint, or {var: marginal}."""
+    if joint:
+        return DiscreteFactor._trusted(variables, plan.cards, vals, qtabs)
+    res = {}
+    for i, v in enumerate(variables):
+        a = plan.acc_off[i]
+        res[v] = DiscreteFactor._trusted([v], [plan.cards[i]], vals[a:a + plan.cards[i]], qtabs)
+    return res
+
+
+class _FastQuery:
+    """A compiled single-query pattern's per-call work, bound once (r06): the evidence values of the
+    plan's columns through their variables' state-name tables straight into a bytes object (C-level
+    map), handed to the runner as the codes (QueryRunner.run_bytes), the result built from the run.
+    The values of the evidence variables the plan pruned away are looked up too, so an unknown state
+    name anywhere still takes the full path and its reference error.  Returns None (the caller takes
+    the full path) when the model or a CPD changed, or a value is not a state name of its table."""
+
+    __slots__ = ("model", "epoch", "runner", "plan", "get_used", "tab_used", "get_rest", "tab_rest",
+                 "variables", "joint", "qtabs", "run_bytes")
+
+    def __init__(self, model, runner, ev_vars, tables, variables, joint, qtabs):
+        plan = runner.plan
+        self.model, self.epoch, self.runner, self.plan = model, getattr(model, "_epoch", None), runner, plan
+        tab = dict(zip(ev_vars, tables))
+        used = list(plan.ev_used)
+        rest = [v for v in ev_vars if v not in set(used)]
+        self.get_used, self.tab_used = _tuple_getter(used), [tab[v] for v in used]
+        self.get_rest, self.tab_rest = (_tuple_getter(rest), [tab[v] for v in rest]) if rest else (None, None)
+        self.variables, self.joint, self.qtabs = variables, joint, qtabs
+        self.run_bytes = getattr(runner, "run_bytes", None)
+
+    def __call__(self, evidence):
+        if (self.run_bytes is None or getattr(self.model, "_epoch", None) != self.epoch
+                or not self.plan.is_current()):
+            return None
+        try:
+            codes = bytes(map(dict.__getitem__, self.tab_used, self.get_used(evidence)))
+            if self.get_rest is not None:
+                bytes(map(dict.__getitem__, self.tab_rest, self.get_rest(evidence)))
+        except (KeyError, TypeError, ValueError):
+            return None
+        vals = self.run_bytes(codes)
+        return _query_result(self.plan, list(self.variables), self.joint, vals, self.qtabs)
+
+
 def _product_all(factors):
     if not factors:
         return None
@@ -151,6 +198,13 @@ class VariableElimination(Inference):
         """P(variables | evidence) (ExactInference.py:246-457)."""
         evidence = evidence if evidence is not None else dict()
         if virtual_evidence is None and elimination_order == "greedy" and type(evidence) is dict:
+            fast = self.__dict__.get("_fast")
+            if fast is not None:  # a repeated (query variables, evidence variables) pattern: _FastQuery
+                ent = fast.get((tuple(variables), tuple(evidence), bool(joint)))
+                if ent is not None:
+                    r = ent(evidence)
+                    if r is not None:
+                        return r
             # the (query, evidence) variable names were checked for this model structure before: the
             # checks below would pass again (C2: 100 evidence names, ~10 us of membership tests per query)
             vk = (tuple(variables), tuple(evidence), id(self.model), getattr(self.model, "_epoch", None))
@@ -282,13 +336,15 @@ class VariableElimination(Inference):
             qtabs = runner._query_tables = {v: StateTable(model.get_cpds(v).state_names[v]) for v in variables}
         if unnorm:
             return DiscreteFactor._trusted(variables, plan.cards, un, qtabs)
-        if joint:
-            return DiscreteFactor._trusted(variables, plan.cards, vals, qtabs)
-        res = {}
-        for i, v in enumerate(variables):
-            a = plan.acc_off[i]
-            res[v] = DiscreteFactor._trusted([v], [plan.cards[i]], vals[a:a + plan.cards[i]], qtabs)
-        return res
+        if tabs is not None:  # the next call of this pattern skips the lookups above (_FastQuery)
+            fast = self.__dict__.get("_fast")
+            if fast is None:
+                fast = self.__dict__.setdefault("_fast", {})
+            if len(fast) >= 256:
+                fast.clear()
+            fast[(tuple(variables), ek, bool(joint))] = _FastQuery(model, runner, ev_vars, tabs[1], list(variables),
+                                                                  bool(joint), qtabs)
+        return _query_result(plan, variables, bool(joint), vals, qtabs)
 
     @E.serialized
     def query_unnormalized(self, variables, evidence=None):

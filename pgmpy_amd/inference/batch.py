@@ -574,13 +574,15 @@ _PLAN_CACHE_MAX = 64
 _plan_cache_lock = threading.Lock()
 
 
-def get_plan(model, variables, evidence_vars, col_of):
+def get_plan(model, variables, evidence_vars, col_of, key=None):
     """The compiled plan of an evidence pattern, cached on the model (at most 64, least recently
     used dropped first).  A cached plan is reused only while PatternPlan.is_current(): the model's
     structure and the values of the CPDs it read are unchanged (a CPD edited, replaced, added or
     removed recompiles, as the reference recomputes from the current CPDs on every call)."""
-    # evidence variable -> codes column, in evidence_vars order (one pass: munin patterns hold ~1,000)
-    key = (tuple(variables), tuple(evidence_vars), tuple(col_of.get(k, -1) for k in evidence_vars))
+    # evidence variable -> codes column, in evidence_vars order (one pass: munin patterns hold ~1,000);
+    # `key`: the same tuple, precomputed by a caller that caches it per frame schema
+    if key is None:
+        key = (tuple(variables), tuple(evidence_vars), tuple(col_of.get(k, -1) for k in evidence_vars))
     with _plan_cache_lock:
         cache = model.__dict__.get(_PLAN_CACHE_ATTR)
         if cache is None:
@@ -635,6 +637,205 @@ def _direct_speculative(model, data, ingested, variables, marginals):
 # frames of at least this many rows that are one evidence pattern of a fused plan take the direct path
 # (_fused_to_host: pinned staging both ways, outputs handed to the result frame without a copy)
 FAST_MIN_ROWS = int(os.environ.get("PGM_API_FAST_MIN_ROWS", 50_000))
+
+# column structures of frames seen before: id(columns Index) -> (the Index, model, epoch, columns list,
+# col_of, the plan-cache key part of col_of).  A pandas Index is immutable, so the same object means the
+# same columns; the entry keeps it referenced, so its id stays its own while cached.
+_FRAME_COLS = {}
+_FRAME_COLS_MAX = 32
+_SCAN_CHUNK = 128  # columns per native scan push while the frame is walked
+
+
+_COLUMN_CHECKS = {}
+
+
+def column_checks(model, data):
+    """The reference's column checks of predict / predict_probability (DiscreteBayesianNetwork.py:
+    850-856, 960-966: no variable missing, or a column that is not a node: ValueError) and the missing
+    variables in its set order, cached per (columns Index object, model structure epoch): a 1,038-column
+    frame builds four sets of ~1,000 names per call otherwise (~0.15 ms of a 1 ms predict_probability)."""
+    cols = data.columns
+    epoch = model.__dict__.get("_epoch", 0)
+    hit = _COLUMN_CHECKS.get(id(cols))
+    if hit is None or hit[0] is not cols or hit[1] is not model or hit[2] != epoch:
+        nodes, have = set(model.nodes()), set(cols)
+        status = "none" if have == nodes else ("extra" if have - nodes else "ok")
+        hit = (cols, model, epoch, status, list(nodes - have))
+        with _LUT_LOCK:
+            if len(_COLUMN_CHECKS) >= _FRAME_COLS_MAX:
+                _COLUMN_CHECKS.clear()
+            _COLUMN_CHECKS[id(cols)] = hit
+    if hit[3] == "none":
+        raise ValueError("No variable missing in data. Nothing to predict")
+    if hit[3] == "extra":
+        raise ValueError("Data has variables which are not in the model")
+    return list(hit[4])
+
+
+_RESULT_COLS = {}
+
+
+def _result_columns(model, order):
+    """predict_probability's result columns f"{var}_{state}" (DiscreteBayesianNetwork.py:985-988) as a
+    pandas Index, cached per (model structure epoch, missing variables)."""
+    import pandas as pd
+
+    key = (id(model), model.__dict__.get("_epoch", 0), tuple(order))
+    hit = _RESULT_COLS.get(key)
+    if hit is None or hit[0] is not model:
+        names = pd.Index([var + "_" + str(s) for var in order for s in model.get_cpds(var).state_names[var]])
+        if len(_RESULT_COLS) >= _FRAME_COLS_MAX:
+            _RESULT_COLS.clear()
+        hit = _RESULT_COLS[key] = (model, names)
+    return hit[1]
+
+
+def _frame_columns(model, data):
+    cols = data.columns
+    epoch = model.__dict__.get("_epoch", 0)
+    hit = _FRAME_COLS.get(id(cols))
+    if hit is not None and hit[0] is cols and hit[1] is model and hit[2] == epoch:
+        return hit[3:]
+    if cols.has_duplicates:
+        return None
+    columns = list(cols)
+    node_map = getattr(model, "_node", None)
+    if node_map is None or not all(c in node_map for c in columns):
+        return None  # a column that is not a node: the general path raises the reference's error
+    col_of = {c: i for i, c in enumerate(columns)}
+    ent = (cols, model, epoch, columns, col_of, tuple(columns), tuple(range(len(columns))))
+    with _LUT_LOCK:
+        if len(_FRAME_COLS) >= _FRAME_COLS_MAX:
+            _FRAME_COLS.clear()
+        _FRAME_COLS[id(cols)] = ent
+    return ent[3:]
+
+
+def _direct_categorical(model, data, order, marginals):
+    """The public API's direct path for a large pandas Categorical frame (r06), or None
+    (the general path then runs, with the reference's errors).
+
+    The device work of the all-observed pattern goes out FIRST: the plan's few evidence columns (7 of
+    munin's 1,038) LUT-mapped on the host pool into pinned staging (pgm_host_lut_map_u8; a column whose
+    categories are the state names in order is copied as is), uploaded, the fused pass launched, the
+    result DMA'd into pinned memory, all asynchronous on the stream.  Then, while the GPU and the copy run,
+    the frame is walked once in Python (each column's codes address and dtype) and the addresses are
+    pushed, 128 columns at a time, to the native NaN scan (pgm_host_scan_begin / _push / _end) that runs
+    on the host pool behind the walk.  A NaN anywhere (another evidence pattern) discards the result;
+    otherwise the frame's schema is validated (every category a state name: the schema cache of
+    _schema_fast, else _category_lut per column) and the result block is returned.  r05 did the walk,
+    the scan and the mapping one after the other on the critical path (1.6 ms per 100 k rows)."""
+    import torch
+
+    n = len(data)
+    if n < FAST_MIN_ROWS:
+        return None
+    fc = _frame_columns(model, data)
+    if fc is None:
+        return None
+    columns, col_of, tcols, colidx = fc
+    try:
+        mgr = data._mgr
+        arrays = mgr.arrays
+        if len(arrays) != len(columns) or not np.array_equal(mgr.blknos, np.arange(len(columns))):
+            return None
+    except Exception:  # pandas internals moved: the general path
+        return None
+    cat_t = pd_categorical()
+    L = N.lib()
+    key = (tuple(order), tcols, colidx)
+    plan = get_plan(model, list(order), columns, col_of, key=key)
+    if plan.kind != "fused" or list(plan.variables) != list(order):
+        return None
+    used = [col_of[v] for v in plan.ev_used]
+    srcs, luts = [], []
+    for j in used:
+        a = arrays[j]
+        if type(a) is not cat_t:
+            return None
+        raw = a._codes
+        if raw.dtype != np.int8 or not raw.flags.c_contiguous:
+            return None
+        st = model.get_cpds(columns[j]).state_names[columns[j]]
+        lut, ok = _category_lut(columns[j], st, a.dtype)
+        if not ok:
+            return None  # a category that is not a state name: the general path raises for its cells
+        srcs.append(raw)
+        luts.append(None if _lut_is_identity(lut, len(a.dtype.categories)) else lut)
+    s = N.stream_handle()
+    k = max(1, len(used))
+    stage = _pinned((k, n), torch.uint8)
+    if used:
+        sp = (ctypes.c_void_p * len(used))(*[r.ctypes.data for r in srcs])
+        lp = (ctypes.c_void_p * len(used))(*[None if t is None else t.ctypes.data for t in luts])
+        N.check(L.pgm_host_lut_map_u8(sp, lp, len(used), n, stage.ctypes.data_as(ctypes.c_void_p), n,
+                                      _host_threads()), "host_lut_map_u8")
+    dcodes = torch.empty(stage.shape, dtype=torch.uint8, device=E.device())
+    N.check(L.pgm_memcpy_h2d(N.ptr(dcodes), stage.ctypes.data_as(ctypes.c_void_p), stage.nbytes, s), "memcpy_h2d")
+    run_plan = plan.compact()
+    out = run_plan.alloc_outputs(n, marginals=marginals, map_=not marginals)
+    err = torch.zeros(1, dtype=torch.int32, device=dcodes.device)
+    run_plan.run(dcodes, n, 0, n, out, err=err)
+    dev = out["marg" if marginals else "map"]
+    host = _pinned(tuple(dev.shape), dev.dtype)
+    herr = _pinned((1,), torch.int32)
+    N.check(L.pgm_memcpy_d2h_async(herr.ctypes.data_as(ctypes.c_void_p), N.ptr(err), 4, s), "memcpy_d2h")
+    N.check(L.pgm_memcpy_d2h_async(host.ctypes.data_as(ctypes.c_void_p), N.ptr(dev), host.nbytes, s), "memcpy_d2h")
+    # the walk + scan, overlapped with the GPU work and the copies queued above
+    nc = len(columns)
+    job = ctypes.c_void_p()
+    N.check(L.pgm_host_scan_begin(n, nc, _host_threads(), ctypes.byref(job)), "host_scan_begin")
+    ok = True
+    dtypes = []
+    addressof, char_at = ctypes.addressof, ctypes.c_char.from_buffer
+    i8 = np.dtype(np.int8)
+    try:
+        for c0 in range(0, nc, _SCAN_CHUNK):
+            part = arrays[c0:c0 + _SCAN_CHUNK]
+            if not all(type(a) is cat_t for a in part):
+                ok = False
+                break
+            raws = [a._codes for a in part]
+            if not all(r.dtype is i8 and r.flags.c_contiguous for r in raws):
+                ok = False
+                break
+            dtypes.extend([a.dtype for a in part])
+            ptrs = (ctypes.c_void_p * len(raws))(*[addressof(char_at(r)) for r in raws])
+            N.check(L.pgm_host_scan_push(job, ptrs, len(raws)), "host_scan_push")
+    except (TypeError, ValueError):  # a read-only codes buffer: the general path
+        ok = False
+    finally:
+        has_nan = np.zeros(nc, dtype=np.uint8)
+        got = ctypes.c_int32()
+        N.check(L.pgm_host_scan_end(job, has_nan.ctypes.data_as(ctypes.c_void_p), ctypes.byref(got)), "host_scan_end")
+    N.check(L.pgm_stream_sync(s), "stream_sync")  # the staging / result buffers are released only after this
+    if not ok or got.value != nc or has_nan.any():
+        return None
+    skey = _schema_key(model, columns, dtypes)
+    hit = _SCHEMA_CACHE.get(skey)
+    if hit is None or hit[0] is not model:
+        all_luts = []
+        for j, d in enumerate(dtypes):  # first frame of this schema: every category a state name?
+            lut, lut_ok = _category_lut(columns[j], model.get_cpds(columns[j]).state_names[columns[j]], d)
+            if not lut_ok:
+                return None
+            all_luts.append(lut)
+        _schema_store(model, columns, arrays, all_luts)
+    if herr[0] != 0:
+        raise IndexError("evidence state code out of range")
+    return plan, host
+
+
+def pd_categorical():
+    import pandas as pd
+
+    return pd.Categorical
+
+
+def _lut_is_identity(lut, n_cat):
+    """The LUT maps category i to state i for every category (and NaN to MISSING): the codes can be
+    used as they are."""
+    return bool(lut[255] == MISSING and n_cat <= 127 and np.array_equal(lut[:n_cat], np.arange(n_cat)))
 
 
 def _single_fused_plan(model, data, columns, col_of, ev, variables):
@@ -806,16 +1007,18 @@ def predict_probability_frame(model, data):
     """DiscreteBayesianNetwork.predict_probability (DiscreteBayesianNetwork.py:912-989)."""
     import pandas as pd
 
-    missing_variables = set(model.nodes()) - set(data.columns)
-    order = list(missing_variables)  # the reference's set iteration order (column order of its output)
+    order = column_checks(model, data)  # the reference's set iteration order (column order of its output)
     n = len(data)
     if n == 0:  # the reference builds its frame from empty per-column lists: no columns at all
         return pd.DataFrame({}, index=data.index)
     if wide_columns(model, data.columns):
         return _rowwise_frame(model, data, "marg")
-    ingested = _ingest(model, data, defer_scan=n >= FAST_MIN_ROWS)
-    direct = _direct_speculative(model, data, ingested, order, True)
+    direct = _direct_categorical(model, data, order, True)
     marg = direct[1] if direct is not None else None
+    if marg is None:
+        ingested = _ingest(model, data, defer_scan=n >= FAST_MIN_ROWS)
+        direct = _direct_speculative(model, data, ingested, order, True)
+        marg = direct[1] if direct is not None else None
     if marg is None:
         if isinstance(ingested[2], ColumnarEvidence):
             ingested[2].finish_scan()
@@ -825,7 +1028,7 @@ def predict_probability_frame(model, data):
     if marg is not None:
         # one pattern: the marginals' rows ARE the result's columns (plan.variables == order, each
         # variable's states consecutive), so the frame is built on the pinned output block, no copy
-        names = [var + "_" + str(s) for var in order for s in model.get_cpds(var).state_names[var]]
+        names = _result_columns(model, order)
         assert len(names) == marg.shape[0]
         return pd.DataFrame(marg.T, columns=names, index=data.index, copy=False)
     cols = {}
@@ -883,14 +1086,16 @@ def predict_frame(model, data):
     """DiscreteBayesianNetwork.predict, MAP (DiscreteBayesianNetwork.py:731-910)."""
     import pandas as pd
 
-    missing_variables = set(model.nodes()) - set(data.columns)
-    order = list(missing_variables)
+    order = column_checks(model, data)
     if len(data) == 0:  # the reference indexes the first group of an empty groupby
         raise IndexError("list index out of range (predict on an empty DataFrame)")
     if wide_columns(model, data.columns):
         return _rowwise_frame(model, data, "map")
-    ingested = _ingest(model, data, defer_scan=len(data) >= FAST_MIN_ROWS)
-    direct = _direct_speculative(model, data, ingested, order, False)
+    direct = _direct_categorical(model, data, order, False)
+    ingested = None
+    if direct is None:
+        ingested = _ingest(model, data, defer_scan=len(data) >= FAST_MIN_ROWS)
+        direct = _direct_speculative(model, data, ingested, order, False)
     if direct is None:
         if isinstance(ingested[2], ColumnarEvidence):
             ingested[2].finish_scan()

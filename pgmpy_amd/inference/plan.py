@@ -595,7 +595,7 @@ class PatternPlan:
         for n in {min(chunk, n_rows - c0) for c0 in range(0, n_rows, chunk)}:
             self.prepare_steps(n, outs)
 
-    def query_one(self, codes, key, stream=None, unnorm=False):
+    def query_one(self, codes, key, stream=None, unnorm=False, codes_bytes=None):
         """One evidence row (codes[col_of[v]]: the state number of evidence variable v, already checked
         against the state names on the host) through the steps program whose codes and result live in
         host memory the kernels access directly: fill the codes, one graph launch, one synchronize.
@@ -609,13 +609,19 @@ class PatternPlan:
                 prog, _, _, _, _, host = self._steps_program(1, frozenset([key]), host_io=True)
                 self.__dict__.setdefault("_q1", {})[key] = hit = (prog, host)
             prog, host = hit
-            sel = self.__dict__.get("_ev_sel")
-            if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
-                idx = [self.col_of[v] for v in self.ev_used]
-                sel = self._ev_sel = ((lambda c, i=idx[0]: (c[i],)) if len(idx) == 1 else
-                                      itemgetter(*idx) if idx else None)
-            if sel is not None:
-                host["codes"].array[:, 0] = sel(codes)
+            if codes_bytes is not None:  # the ev_used codes, in order (one byte per column of the [cols, 1] buffer)
+                if len(codes_bytes) != len(self.ev_used):
+                    raise ValueError("query_one: one code per evidence column the plan reads")
+                if codes_bytes:
+                    ctypes.memmove(host["codes"].array.ctypes.data, codes_bytes, len(codes_bytes))
+            else:
+                sel = self.__dict__.get("_ev_sel")
+                if sel is None:  # the caller's column of each evidence variable the plan reads (col_of)
+                    idx = [self.col_of[v] for v in self.ev_used]
+                    sel = self._ev_sel = ((lambda c, i=idx[0]: (c[i],)) if len(idx) == 1 else
+                                          itemgetter(*idx) if idx else None)
+                if sel is not None:
+                    host["codes"].array[:, 0] = sel(codes)
             if prog._direct or ((dq := DirectQueue.for_queries()) is not None and prog.bind_direct(dq)):
                 # the steps as one chain of AQL packets: written and rung in ~2 us, returns when the
                 # results are in host memory (a graph launch spends ~17 us on the host first)
@@ -699,6 +705,14 @@ class QueryRunner:
         self.joint = bool(joint)
         self.lock = threading.Lock()
         self.key = "joint" if joint else "marg"
+
+    def run_bytes(self, codes):
+        """run() with the codes of plan.ev_used already as bytes, in that order (_FastQuery)."""
+        if not self.__dict__.get("_prepared"):
+            self.plan.prepare_steps(1, frozenset([self.key]), host_io=True)
+            self._prepared = True
+        with self.lock:
+            return self.plan.query_one(None, self.key, codes_bytes=codes)
 
     def run(self, codes, unnorm=False):
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:

@@ -273,12 +273,9 @@ class DiscreteBayesianNetwork(nx.DiGraph):
         Rows are grouped by evidence pattern; each pattern is one compiled device plan
         (fused one-lane-per-row kernel).  The output frame matches the reference:
         columns data.columns + missing variables, rows in index order, state names."""
-        from ..inference.batch import predict_frame
+        from ..inference.batch import column_checks, predict_frame
 
-        if set(data.columns) == set(self.nodes()):
-            raise ValueError("No variable missing in data. Nothing to predict")
-        elif set(data.columns) - set(self.nodes()):
-            raise ValueError("Data has variables which are not in the model")
+        column_checks(self, data)  # the reference's ValueErrors (cached per columns object)
         if algo is not None:
             from ..inference import Inference
 
@@ -293,10 +290,7 @@ class DiscreteBayesianNetwork(nx.DiGraph):
     @E.serialized
     def predict_probability(self, data):
         """Per-row marginals of every missing variable (DiscreteBayesianNetwork.py:912-989)."""
-        from ..inference.batch import predict_probability_frame
+        from ..inference.batch import column_checks, predict_probability_frame
 
-        if set(data.columns) == set(self.nodes()):
-            raise ValueError("No variable missing in data. Nothing to predict")
-        elif set(data.columns) - set(self.nodes()):
-            raise ValueError("Data has variables which are not in the model")
+        column_checks(self, data)  # the reference's ValueErrors (cached per columns object)
         return predict_probability_frame(self, data)
