@@ -142,6 +142,25 @@ typedef struct {
 
 int pgm_product_n(const pgm_productn_desc *d, const double *const *ops, double *C, void *stream);
 
+/* r06: an n-ary contraction, C[keep] = REDUCE over red of prod_t X_t[keep . keep_s[t] + red . red_s[t]]
+ * (up to PGM_PRODN_MAX_OPS operands, reduce PGM_RED_SUM or PGM_RED_MAX), as a JOB of a batch only
+ * (pgm_batch_add_contract_n): several consecutive pairwise steps of a contraction path
+ * (ExactInference.py:404-406, opt_einsum's pairwise tensordots) in one job of one launch, so the
+ * compiled path has fewer dependency levels.  A batch holding one runs only as its specialised kernel
+ * (pgm_batch_specialise); pgm_batch_run refuses it (PGM_EINVAL).  Products are rounded before they are
+ * summed, operands multiplied in order (a left fold, as factor_product). */
+typedef struct {
+  int32_t n_ops;
+  int32_t reduce;
+  int32_t n_keep;
+  int32_t n_red;
+  int64_t keep_card[PGM_MAX_DIMS];
+  int64_t keep_sc[PGM_MAX_DIMS];
+  int64_t keep_s[PGM_PRODN_MAX_OPS][PGM_MAX_DIMS];
+  int64_t red_card[PGM_MAX_DIMS];
+  int64_t red_s[PGM_PRODN_MAX_OPS][PGM_MAX_DIMS];
+} pgm_contractn_desc;
+
 /* The same product and, in the same pass, M = reduce(C) over the keep dims with marg_s == 0
  * (marg_s[i]: stride of keep dim i in M; the last keep dim, the evidence rows, must have stride 1
  * in C and M).  Batched-BP collect (a clique belief and its message to the parent,
@@ -315,6 +334,8 @@ int pgm_batch_add_gather(void *handle, const pgm_gather_desc *d, const double *A
 /* an n-ary product job (pgm_product_n's descriptor and checks; flat mode): batched BP runs every
  * small clique / separator product of one dependency level of the calibration as one launch */
 int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const double *const *ops, double *C);
+/* r06: an n-ary contraction job (pgm_contractn_desc; ops: a HOST array of n_ops device pointers). */
+int pgm_batch_add_contract_n(void *batch, const pgm_contractn_desc *d, const double *const *ops, double *C);
 /* a findings-indicator job (pgm_indicator's arguments): all of a BP sweep's findings in one launch */
 int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
                             int64_t s_state, int64_t s_row, int32_t *err_flag);

@@ -80,6 +80,21 @@ class ProductNDesc(ctypes.Structure):
     ]
 
 
+class ContractNDesc(ctypes.Structure):
+    """pgm_contractn_desc (r06): C[keep] = reduce over red of prod_t X_t."""
+    _fields_ = [
+        ("n_ops", ctypes.c_int32),
+        ("reduce", ctypes.c_int32),
+        ("n_keep", ctypes.c_int32),
+        ("n_red", ctypes.c_int32),
+        ("keep_card", _I64),
+        ("keep_sc", _I64),
+        ("keep_s", _I64 * PRODN_MAX_OPS),
+        ("red_card", _I64),
+        ("red_s", _I64 * PRODN_MAX_OPS),
+    ]
+
+
 class GemmDesc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int64), ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("k", ctypes.c_int64),
                 ("offsets", ctypes.c_void_p), ("stride", ctypes.c_int64 * 9), ("lane_order", ctypes.c_int32),
@@ -179,6 +194,7 @@ _SIGS = {
     "pgm_batch_add_contract": ([_P, ctypes.POINTER(ContractDesc), _P, _P, _P], ctypes.c_int),
     "pgm_batch_add_gather": ([_P, ctypes.POINTER(GatherDesc), _P, _P, _P, _P], ctypes.c_int),
     "pgm_batch_add_product_n": ([_P, ctypes.POINTER(ProductNDesc), ctypes.POINTER(_P), _P], ctypes.c_int),
+    "pgm_batch_add_contract_n": ([_P, ctypes.POINTER(ContractNDesc), ctypes.POINTER(_P), _P], ctypes.c_int),
     "pgm_batch_add_indicator": ([_P, _P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, ctypes.c_int64, _P],
                                 ctypes.c_int),
     "pgm_batch_set_mode": ([_P, ctypes.c_int32], ctypes.c_int),

@@ -66,8 +66,19 @@ struct GatherK {
   int32_t ev_card[PGM_MAX_DIMS];
 };
 
+// a planned n-ary contraction (pgm_batch_add_contract_n: C[keep] = reduce over red of prod_t X_t; r06):
+// several pairwise steps of a contraction path done as ONE job, so the path has fewer dependency levels
+struct ContractNK {
+  int32_t n_ops, nk, nr, red, g_log2, _pad;
+  uint32_t n_out, n_red;
+  uint32_t kcard[KMAX], rcard[KMAX];
+  int64_t ksc[KMAX];
+  int64_t ks[MOPS][KMAX], rs[MOPS][KMAX];
+};
+
 // one job of a batch (pgm_batch_*) as the specialiser sees it: blocks [block0, block0 + nblocks) of
-// the batch's 256-thread blocks; kind 0: C[keep] = reduce(combine(A, B)) (k), 1: an evidence gather (g)
+// the batch's 256-thread blocks; kind 0: C[keep] = reduce(combine(A, B)) (k), 1: an evidence gather (g),
+// 2: an n-ary contraction (n, operands ops[0 .. n.n_ops))
 struct pgmi_cs_job {
   int32_t kind, cmb, red;
   uint32_t block0, nblocks;
@@ -77,6 +88,8 @@ struct pgmi_cs_job {
   int32_t *err;
   ContractK k;
   GatherK g;
+  ContractNK n;
+  const double *ops[MOPS];
 };
 
 // a plan-specialised kernel for a batch of contraction jobs (pgmpm.cpp): one_wg = 0: one launch of

@@ -3394,6 +3394,9 @@ struct BatchHandle {
   int32_t spec = -1;  // every job a contraction with one (combine, reduce): combine * 3 + reduce; products: 100
   ChainJob *d_chain = nullptr;  // ONE_WORKGROUP batch (contractions only): descriptors staged in LDS
   size_t chain_lds = 0;         // dynamic LDS bytes of k_batch_wg_c
+  // r06: n-ary contraction jobs (kind 4; BatchJob::_pad indexes these): specialised kernel only
+  std::vector<ContractNK> njobs;
+  std::vector<std::vector<const double *>> nops;
 };
 
 static const int32_t kBatchSpecProducts = 100;  // BatchHandle::spec of a products-only batch
@@ -3560,6 +3563,110 @@ int pgm_batch_add_product_n(void *handle, const pgm_productn_desc *d, const doub
   return batch_append(h, J, pairs ? k.n_out / 2 : k.n_out);
 }
 
+// an n-ary contraction's plan: unit dims dropped, adjacent dims merged where every operand (and C, for
+// kept dims) steps through them as one, G lanes per output for long reductions of few outputs
+static int plan_contract_n(const pgm_contractn_desc *d, const double *const *ops, ContractNK &k) {
+  if (!d || !ops) return fail(PGM_EINVAL, "contract_n: null argument");
+  const int n = d->n_ops;
+  if (n < 1 || n > MOPS) return fail(PGM_EINVAL, "contract_n: %d operands (1..%d)", n, MOPS);
+  if (d->reduce != PGM_RED_SUM && d->reduce != PGM_RED_MAX) return fail(PGM_EINVAL, "contract_n: reduce must be sum or max");
+  if (d->n_keep < 0 || d->n_keep > PGM_MAX_DIMS || d->n_red < 0 || d->n_red > PGM_MAX_DIMS)
+    return fail(PGM_EINVAL, "contract_n: %d kept / %d reduced dims", d->n_keep, d->n_red);
+  for (int t = 0; t < n; ++t)
+    if (!ops[t]) return fail(PGM_EINVAL, "contract_n: operand %d is null", t);
+  memset(&k, 0, sizeof k);
+  k.n_ops = n;
+  k.red = d->reduce;
+  // kept dims (C-order: the last fastest), then reduced dims; each side merged from the inside out
+  struct Dim {
+    int64_t card, sc, s[MOPS];
+  };
+  auto collect = [&](int nd, const int64_t *card, const int64_t *sc, const int64_t (*st)[PGM_MAX_DIMS], std::vector<Dim> &out) {
+    for (int i = 0; i < nd; ++i) {
+      if (card[i] < 0) return false;
+      if (card[i] == 1) continue;
+      Dim x;
+      x.card = card[i];
+      x.sc = sc ? sc[i] : 0;
+      for (int t = 0; t < n; ++t) x.s[t] = st[t][i];
+      if (!out.empty()) {  // merge into the previous (outer) dim when it is this one's continuation
+        Dim &o = out.back();
+        bool ok = !sc || o.sc == x.sc * x.card;
+        for (int t = 0; ok && t < n; ++t) ok = o.s[t] == x.s[t] * x.card;
+        if (ok) {
+          o.card *= x.card;
+          o.sc = x.sc;
+          for (int t = 0; t < n; ++t) o.s[t] = x.s[t];
+          continue;
+        }
+      }
+      out.push_back(x);
+    }
+    return true;
+  };
+  std::vector<Dim> kd, rd;
+  for (int i = 0; i < d->n_keep; ++i)
+    if (d->keep_card[i] == 0) {
+      k.n_out = 0;
+      return PGM_OK;  // empty output: nothing to do
+    }
+  if (!collect(d->n_keep, d->keep_card, d->keep_sc, d->keep_s, kd) || !collect(d->n_red, d->red_card, nullptr, d->red_s, rd))
+    return fail(PGM_EINVAL, "contract_n: negative cardinality");
+  if ((int)kd.size() > KMAX || (int)rd.size() > KMAX)
+    return fail(PGM_EINVAL, "contract_n: %zu kept / %zu reduced dims after merging (at most %d each)", kd.size(), rd.size(), KMAX);
+  uint64_t n_out = 1, n_red = 1;
+  k.nk = (int)kd.size();
+  k.nr = (int)rd.size();
+  for (int i = 0; i < k.nk; ++i) {
+    n_out *= (uint64_t)kd[i].card;
+    if (n_out > 0x7fffffffull) return fail(PGM_EINVAL, "contract_n: output over 2^31 entries");
+    k.kcard[i] = (uint32_t)kd[i].card;
+    k.ksc[i] = kd[i].sc;
+    for (int t = 0; t < n; ++t) k.ks[t][i] = kd[i].s[t];
+  }
+  for (int i = 0; i < k.nr; ++i) {
+    if (rd[i].card == 0) {
+      n_red = 0;
+      break;
+    }
+    n_red *= (uint64_t)rd[i].card;
+    if (n_red > 0x7fffffffull) return fail(PGM_EINVAL, "contract_n: reduction over 2^31 entries");
+    k.rcard[i] = (uint32_t)rd[i].card;
+    for (int t = 0; t < n; ++t) k.rs[t][i] = rd[i].s[t];
+  }
+  if (n_red == 0) return fail(PGM_EINVAL, "contract_n: an empty reduction");
+  k.n_out = (uint32_t)n_out;
+  k.n_red = (uint32_t)n_red;
+  // lanes per output: up to 64 while the job's lanes stay under 4x a batch contraction's cap (a fused
+  // step's reduction is a walk of dependent load rounds; more lanes, fewer rounds each)
+  int g = 0;
+  if (k.nr > 0)
+    while (g < 6 && ((uint64_t)k.n_out << g) < 4 * kBatchLanesCap && (1ull << (g + 1)) <= n_red) ++g;
+  k.g_log2 = g;
+  return PGM_OK;
+}
+
+int pgm_batch_add_contract_n(void *handle, const pgm_contractn_desc *d, const double *const *ops, double *C) {
+  STALE_PROBE();
+  BatchHandle *h = (BatchHandle *)handle;
+  if (!h || !C) return fail(PGM_EINVAL, "batch_add_contract_n: null argument");
+  ContractNK k;
+  int rc = plan_contract_n(d, ops, k);
+  if (rc != PGM_OK) return rc;
+  if (k.n_out == 0) return PGM_OK;
+  BatchJob J;
+  memset(&J, 0, sizeof J);
+  J.kind = 4;
+  J.red = k.red;
+  J.C = C;
+  J._pad = (int32_t)h->njobs.size();
+  rc = batch_append(h, J, (uint64_t)k.n_out << k.g_log2, k.nr == 0 ? kBatchMaxBlocksProduct : 0);
+  if (rc != PGM_OK) return rc;
+  h->njobs.push_back(k);
+  h->nops.emplace_back(ops, ops + k.n_ops);
+  return PGM_OK;
+}
+
 int pgm_batch_add_indicator(void *handle, const uint8_t *codes, int64_t n_rows, int64_t card, double *out,
                             int64_t s_state, int64_t s_row, int32_t *err_flag) {
   STALE_PROBE();
@@ -3629,7 +3736,7 @@ int pgm_batch_finalize(void *handle) {
   for (const BatchJob &J : h->jobs) {
     uni = uni && J.kind == 0 && J.cmb == h->jobs[0].cmb && J.red == h->jobs[0].red;
     prod = prod && J.kind == 2;
-    contract_only = contract_only && J.kind == 0;
+    contract_only = contract_only && (J.kind == 0 || J.kind == 4);  // (kind 4: specialised kernel only)
   }
   if (uni) h->spec = h->jobs[0].cmb * 3 + h->jobs[0].red;
   if (prod) h->spec = kBatchSpecProducts;
@@ -3681,6 +3788,8 @@ int pgm_batch_run(void *handle, void *stream) {
   if (!h) return fail(PGM_EINVAL, "batch_run: null handle");
   if (h->jobs.empty()) return PGM_OK;
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_run: not finalized");
+  if (!h->njobs.empty())
+    return fail(PGM_EINVAL, "batch_run: n-ary contraction jobs run only in the batch's specialised kernel (pgm_batch_specialise)");
   if (h->mode == PGM_BATCH_ONE_WORKGROUP) {
     const uint32_t n_levels = (uint32_t)h->level_off.size() - 1;
     hipLaunchKernelGGL(k_batch_wg_c, dim3(1), dim3(256 * kChainVB), h->chain_lds, S(stream), (const ChainJob *)h->d_chain,
@@ -3704,9 +3813,20 @@ int pgm_batch_specialise(void *handle, void **bound) {
   if (!h->d_jobs) return fail(PGM_EINVAL, "batch_specialise: not finalized");
   std::vector<pgmi_cs_job> jobs;
   for (const BatchJob &J : h->jobs) {
-    if (J.kind > 1 || (J.kind == 0 && J.c.n_split != 1)) return PGM_OK;  // contractions and gathers only
+    if ((J.kind > 1 && J.kind != 4) || (J.kind == 0 && J.c.n_split != 1)) return PGM_OK;  // contractions and gathers only
     pgmi_cs_job c;
     memset(&c, 0, sizeof c);
+    if (J.kind == 4) {  // n-ary contraction
+      c.kind = 2;
+      c.red = J.red;
+      c.block0 = J.block0;
+      c.nblocks = J.nblocks;
+      c.C = J.C;
+      c.n = h->njobs[J._pad];
+      for (int t = 0; t < c.n.n_ops; ++t) c.ops[t] = h->nops[J._pad][t];
+      jobs.push_back(c);
+      continue;
+    }
     c.kind = J.kind;
     c.cmb = J.cmb;
     c.red = J.red;

@@ -1238,7 +1238,96 @@ static std::string cs_gather_body(const pgmi_cs_job &J, const std::string &name)
   return o;
 }
 
-static int cs_nptrs(const pgmi_cs_job &J) { return J.kind == 1 ? 4 : 3; }
+// an n-ary contraction job (r06; pgm_batch_add_contract_n): C[out] = reduce over the reduction space of
+// X_0 * X_1 * ... (a left fold), every decode and stride a literal; G lanes per output stride through the
+// flattened reduction index (its digits decoded with literal divisors), else literal nested loops
+static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
+  const ContractNK &k = J.n;
+  const int n = k.n_ops;
+  const bool mx = k.red == PGM_RED_MAX;
+  const char *init = mx ? "-__builtin_inf()" : "0.0";
+  std::string o;
+  pgmi_appendf(o, "__device__ __forceinline__ void %s(unsigned tid, unsigned nth", name.c_str());
+  for (int t = 0; t < n; ++t) pgmi_appendf(o, ", const double *__restrict__ X%d", t);
+  o += ", double *__restrict__ C) {\n";
+  const unsigned G = 1u << k.g_log2;
+  if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
+  pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  o += "    unsigned idx = out; long long oc = 0;";
+  for (int t = 0; t < n; ++t) pgmi_appendf(o, " long long o%d = 0;", t);
+  o += "\n";
+  for (int i = k.nk - 1; i >= 0; --i) {
+    const unsigned d = k.kcard[i];
+    if (i == 0) o += "    { const unsigned g_ = idx;";
+    else pgmi_appendf(o, "    { const unsigned q_ = idx / %uu, g_ = idx - q_ * %uu; idx = q_;", d, d);
+    if (k.ksc[i]) pgmi_appendf(o, " oc += (long long)g_ * %lldLL;", (long long)k.ksc[i]);
+    for (int t = 0; t < n; ++t)
+      if (k.ks[t][i]) pgmi_appendf(o, " o%d += (long long)g_ * %lldLL;", t, (long long)k.ks[t][i]);
+    o += " }\n";
+  }
+  auto prod = [&](const std::vector<std::string> &off) {
+    std::string e = "X0[" + off[0] + "]";
+    for (int t = 1; t < n; ++t) e = "(" + e + " * X" + std::to_string(t) + "[" + off[t] + "])";
+    return e;
+  };
+  auto upd = [&](const std::string &v) {
+    return mx ? "acc = pgm_maxn(acc, " + v + ");" : "acc = acc + " + v + ";";
+  };
+  pgmi_appendf(o, "    double acc = %s;\n", init);
+  if (k.nr == 0) {
+    std::vector<std::string> off;
+    for (int t = 0; t < n; ++t) off.push_back("o" + std::to_string(t));
+    o += "    acc = " + prod(off) + ";\n";
+  } else if (G > 1) {
+    pgmi_appendf(o, "    #pragma unroll 4\n    for (unsigned r = lane_g; r < %uu; r += %uu) {\n      unsigned ri = r;", k.n_red, G);
+    for (int t = 0; t < n; ++t) pgmi_appendf(o, " long long p%d = o%d;", t, t);
+    o += "\n";
+    for (int i = k.nr - 1; i >= 0; --i) {
+      const unsigned d = k.rcard[i];
+      if (i == 0) o += "      { const unsigned g_ = ri;";
+      else pgmi_appendf(o, "      { const unsigned q_ = ri / %uu, g_ = ri - q_ * %uu; ri = q_;", d, d);
+      for (int t = 0; t < n; ++t)
+        if (k.rs[t][i]) pgmi_appendf(o, " p%d += (long long)g_ * %lldLL;", t, (long long)k.rs[t][i]);
+      o += " }\n";
+    }
+    std::vector<std::string> off;
+    for (int t = 0; t < n; ++t) off.push_back("p" + std::to_string(t));
+    o += "      " + upd(prod(off)) + "\n    }\n";
+  } else {
+    std::string ind = "    ";
+    uint64_t inner = 1;
+    int first_unrolled = k.nr;
+    for (int r = k.nr - 1; r >= 0; --r) {
+      inner *= k.rcard[r];
+      if (inner > 64) break;
+      first_unrolled = r;
+    }
+    for (int r = 0; r < k.nr; ++r) {
+      pgmi_appendf(o, "%s#pragma unroll%s\n", ind.c_str(), r >= first_unrolled ? "" : " 2");
+      pgmi_appendf(o, "%sfor (unsigned r%d = 0; r%d < %uu; ++r%d) {\n", ind.c_str(), r, r, k.rcard[r], r);
+      ind += "  ";
+    }
+    std::vector<std::string> off;
+    for (int t = 0; t < n; ++t) {
+      std::string e = "o" + std::to_string(t);
+      for (int r = 0; r < k.nr; ++r)
+        if (k.rs[t][r]) e += " + (long long)r" + std::to_string(r) + " * " + std::to_string((long long)k.rs[t][r]) + "LL";
+      off.push_back(e);
+    }
+    o += ind + upd(prod(off)) + "\n";
+    for (int r = 0; r < k.nr; ++r) {
+      ind.resize(ind.size() - 2);
+      o += ind + "}\n";
+    }
+  }
+  if (G > 1)
+    for (unsigned off = G >> 1; off > 0; off >>= 1)
+      pgmi_appendf(o, "    %s\n", upd("__shfl_xor(acc, " + std::to_string(off) + ", 64)").c_str());
+  pgmi_appendf(o, "    %sC[oc] = acc;\n  }\n}\n", G > 1 ? "if (lane_g == 0) " : "");
+  return o;
+}
+
+static int cs_nptrs(const pgmi_cs_job &J) { return J.kind == 2 ? J.n.n_ops + 1 : J.kind == 1 ? 4 : 3; }
 
 int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int n_levels, int one_wg, void **bound) {
   *bound = nullptr;
@@ -1256,6 +1345,11 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
       if (g.nk < 0 || g.nk > KMAX || g.n_ev < 0 || g.n_ev > PGM_MAX_DIMS) return PGM_OK;  // nk 0: one output
       continue;
     }
+    if (jobs[j].kind == 2) {
+      const ContractNK &c = jobs[j].n;
+      if (c.n_ops < 1 || c.n_ops > MOPS || c.nk < 0 || c.nk > KMAX || c.nr < 0 || c.nr > KMAX) return PGM_OK;
+      continue;
+    }
     const ContractK &k = jobs[j].k;
     if (k.n_split != 1 || (k.row_mode != 0 && k.row_mode != 2) || k.nk < 0 || k.nk > KMAX || k.nr > KMAX ||
         (k.row_mode == 2 && k.nk < 1))
@@ -1268,7 +1362,9 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
       "return r != r ? 0.0 : r; }\n"
       "__device__ __forceinline__ double pgm_maxn(double a, double b) { return (a > b || a != a) ? a : b; }\n";
   for (int j = 0; j < n; ++j)
-    o += jobs[j].kind == 1 ? cs_gather_body(jobs[j], "cj" + std::to_string(j)) : cs_job_body(jobs[j], "cj" + std::to_string(j));
+    o += jobs[j].kind == 1   ? cs_gather_body(jobs[j], "cj" + std::to_string(j))
+         : jobs[j].kind == 2 ? cs_nary_body(jobs[j], "cj" + std::to_string(j))
+                             : cs_job_body(jobs[j], "cj" + std::to_string(j));
   pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", base[n]);
   // jobs [j0, j1) by block b: a balanced tree of literal comparisons (the jobs' block ranges ascend)
   std::function<void(std::string &, int, int, std::string)> dispatch = [&](std::string &s, int j0, int j1,
@@ -1279,7 +1375,11 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
       if (J.kind == 1)
         pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], (const unsigned char *)a.p[%d], (double *)a.p[%d], "
                         "(int *)a.p[%d]);\n", ind.c_str(), j0, J.block0, J.nblocks * 256u, p0, p0 + 1, p0 + 2, p0 + 3);
-      else
+      else if (J.kind == 2) {
+        pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu", ind.c_str(), j0, J.block0, J.nblocks * 256u);
+        for (int t = 0; t < J.n.n_ops; ++t) pgmi_appendf(s, ", a.p[%d]", p0 + t);
+        pgmi_appendf(s, ", (double *)a.p[%d]);\n", p0 + J.n.n_ops);
+      } else
         pgmi_appendf(s, "%scj%d((b - %uu) * 256u + lt, %uu, a.p[%d], a.p[%d], (double *)a.p[%d]);\n", ind.c_str(), j0,
                      J.block0, J.nblocks * 256u, p0, p0 + 1, p0 + 2);
       return;
@@ -1327,6 +1427,11 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
   b->blocks = blocks;
   b->threads = threads;
   for (int q = 0; q < n; ++q) {
+    if (jobs[q].kind == 2) {
+      for (int t = 0; t < jobs[q].n.n_ops; ++t) b->ptrs.push_back(jobs[q].ops[t]);
+      b->ptrs.push_back(jobs[q].C);
+      continue;
+    }
     b->ptrs.push_back(jobs[q].A);
     if (jobs[q].kind == 1) {
       b->ptrs.push_back((const double *)jobs[q].codes);

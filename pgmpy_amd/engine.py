@@ -504,6 +504,52 @@ def prepare_product_n(operands, out_labels, out=None, kinds=None):
     return d, ptrs, out
 
 
+def prepare_contract_n(operands, out_labels, reduce="sum", out=None):
+    """(descriptor, operand pointers, out) for C[out_labels] = REDUCE over the other labels of
+    prod_i X_i (pgm_contractn_desc, r06): several pairwise steps of a contraction path as one batch job.
+    operands: (device fp64 tensor, labels) pairs, up to PRODN_MAX_OPS."""
+    N.lib()
+    out_labels = list(out_labels)
+    if not 1 <= len(operands) <= N.PRODN_MAX_OPS:
+        raise ValueError(f"contract_n takes 1..{N.PRODN_MAX_OPS} operands")
+    card = {}
+    for t, ls in operands:
+        if len(ls) != t.dim():
+            raise ValueError("label count does not match tensor rank")
+        for dd, l in enumerate(ls):
+            c = int(t.shape[dd])
+            if card.setdefault(l, c) != c:
+                raise ValueError(f"cardinality mismatch for {l!r}")
+    for l in out_labels:
+        if l not in card:
+            raise ValueError(f"output label {l!r} not in any operand")
+    red = [l for l in card if l not in out_labels]
+    if len(out_labels) > N.PGM_MAX_DIMS or len(red) > N.PGM_MAX_DIMS:
+        raise ValueError("too many dimensions")
+    if out is None:
+        out = empty([card[l] for l in out_labels])
+    d = N.ContractNDesc()
+    d.n_ops = len(operands)
+    d.reduce = _REDUCE[reduce]
+    d.n_keep = len(out_labels)
+    d.n_red = len(red)
+
+    def st(t, ls, l):
+        return int(t.stride(list(ls).index(l))) if l in ls else 0
+
+    for i, l in enumerate(out_labels):
+        d.keep_card[i] = card[l]
+        d.keep_sc[i] = int(out.stride(i))
+        for j, (t, ls) in enumerate(operands):
+            d.keep_s[j][i] = st(t, ls, l)
+    for i, l in enumerate(red):
+        d.red_card[i] = card[l]
+        for j, (t, ls) in enumerate(operands):
+            d.red_s[j][i] = st(t, ls, l)
+    ptrs = (ctypes.c_void_p * len(operands))(*[t.data_ptr() for t, _ in operands])
+    return d, ptrs, out
+
+
 def product_n(operands, out_labels, out=None, kinds=None):
     L = N.lib()
     d, ptrs, out = prepare_product_n(operands, out_labels, out, kinds)

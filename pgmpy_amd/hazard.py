@@ -65,6 +65,20 @@ def contract_foot(d, pA, pB, pC, pws=None, ws_bytes=0):
     return out
 
 
+def contract_n_foot(d, ptrs, pC):
+    """pgm_batch_add_contract_n: every operand read over the kept and reduced index space, C written
+    over the kept space (pgm_contractn_desc)."""
+    nk, nr = int(d.n_keep), int(d.n_red)
+    kc = [int(d.keep_card[i]) for i in range(nk)]
+    rc = [int(d.red_card[i]) for i in range(nr)]
+    out = []
+    for t in range(int(d.n_ops)):
+        _add(out, span(_pv(ptrs[t]), kc + rc, [d.keep_s[t][i] for i in range(nk)] + [d.red_s[t][i] for i in range(nr)],
+                       8), READ)
+    _add(out, span(_pv(pC), kc, [d.keep_sc[i] for i in range(nk)], 8), WRITE)
+    return out
+
+
 def product_n_foot(d, ptrs, pout, store=True, marg=()):
     """pgm_product_n (+ _marginal / _marginals): operands read over the keep space, C written when
     stored, every marginal M (strides over the keep labels, 0 = reduced) written."""

@@ -24,6 +24,7 @@ side keeping >= 16 states) run on FP64 MFMA instead (pgm_gemm, engine.pair_gemm)
 and executor run single queries (C2) and row batches.
 """
 import heapq
+import os
 import threading
 from collections import OrderedDict
 from functools import partial
@@ -275,16 +276,11 @@ def path_cost(steps, operand_labels, dims):
     depth = {i: 0 for i in labels}
     nbytes = flops = maxd = 0
     for st in steps:
-        if st[0] == "reduce":
-            _, i, keep, nid = st
-            nbytes += 8 * (_size(labels[i], dims) + _size(keep, dims))
-            flops += _size(labels[i], dims)
-            d = depth[i] + 1
-        else:
-            _, i, j, keep, nid = st
-            nbytes += 8 * (_size(labels[i], dims) + _size(labels[j], dims) + _size(keep, dims))
-            flops += 2 * _size(list(dict.fromkeys(labels[i] + labels[j])), dims)
-            d = max(depth[i], depth[j]) + 1
+        ins, keep, nid = st[1:-2], st[-2], st[-1]
+        nbytes += 8 * (sum(_size(labels[i], dims) for i in ins) + _size(keep, dims))
+        space = list(dict.fromkeys(l for i in ins for l in labels[i]))
+        flops += (1 if st[0] == "reduce" else 2 if st[0] == "pair" else len(ins)) * _size(space, dims)
+        d = max(depth[i] for i in ins) + 1
         labels[nid], depth[nid] = keep, d
         maxd = max(maxd, d)
     return nbytes, flops, maxd
@@ -305,23 +301,91 @@ def choose_path(operand_labels, out_labels, dims):
     return best[1], best[2]
 
 
-def plan_stats(operand_labels, out_labels, dims):
-    """Algorithmic bytes / flops of the executed path (choose_path; SURVEY.md §8(d) C2 definition):
-    sum over pairwise steps of 8 (|A| + |B| + |C|) bytes and 2 |index space| flops."""
+# r06: the pairwise steps of a compiled single-row path fused into n-ary steps (fuse_path) of at most
+# FUSE_BUDGET index-space entries each: fewer dependency levels, i.e. fewer dependent launches per query
+FUSE = os.environ.get("PGM_FUSE", "1") != "0"
+FUSE_BUDGET = int(os.environ.get("PGM_FUSE_BUDGET", 1 << 16))
+# reduction entries per output of a fused step: each lane walks them one dependent round of loads after
+# another, so a long walk costs more than the launches it saves
+FUSE_MAX_RED = int(os.environ.get("PGM_FUSE_MAX_RED", 64))
+# absorb only the inputs on the step's critical path (the deepest): absorbing a shallower one saves no
+# level, it only lengthens the job's walk
+FUSE_CRITICAL_ONLY = os.environ.get("PGM_FUSE_CRIT", "1") != "0"
+FUSE_MAX_OPS = 8   # PGM_PRODN_MAX_OPS
+FUSE_MAX_DIMS = 12  # KMAX: kept / reduced dims of one job
+
+
+def fuse_path(steps, operand_labels, dims, budget=None, max_ops=FUSE_MAX_OPS, max_dims=FUSE_MAX_DIMS, fixed=(),
+              max_red=None):
+    """A path's pairwise / reduce steps grouped into n-ary steps ("nary", inputs..., keep, nid): walking
+    the steps in order, each step absorbs the steps that produced its inputs (deepest first) while the
+    group's index space (the union of its inputs' labels) stays within `budget` entries, its inputs
+    within `max_ops` and its kept / summed labels within `max_dims` — so C[keep] is the sum over the
+    group's other labels of the product of its inputs, the same value as the steps it replaces (every
+    intermediate of a path is consumed once).  A group of one step stays that step.  `fixed`: ids of
+    steps that keep their own kernel (dense GEMMs, packed reductions): they neither absorb nor are
+    absorbed."""
+    budget = FUSE_BUDGET if budget is None else budget
+    max_red = FUSE_MAX_RED if max_red is None else max_red
+    labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    depth = {i: 0 for i in labels}
+    groups = {}  # nid -> (original step, inputs)
+    kept_as_is = set()
+    for st in steps:
+        ins, keep, nid = list(st[1:-2]), st[-2], st[-1]
+        labels[nid] = keep
+        if nid in fixed:
+            kept_as_is.add(nid)
+            depth[nid] = 1 + max(depth[y] for y in ins)
+            continue
+        cur = list(ins)
+        while True:
+            done = True
+            top = max(depth[y] for y in cur)
+            for x in sorted((x for x in cur if x in groups), key=lambda x: -depth[x]):
+                if FUSE_CRITICAL_ONLY and depth[x] < top:
+                    break
+                trial = [y for y in cur if y != x] + groups[x][1]
+                space = list(dict.fromkeys(l for y in trial for l in labels[y]))
+                n_space = _size(space, dims)
+                if (len(trial) <= max_ops and n_space <= budget and len(keep) <= max_dims
+                        and len(space) - len(keep) <= max_dims and n_space <= max_red * _size(keep, dims)):
+                    cur = trial
+                    del groups[x]
+                    done = False
+                    break
+            if done:
+                break
+        groups[nid] = (st, cur)
+        depth[nid] = 1 + max(depth[y] for y in cur)
+    out = []
+    for st in steps:
+        if st[-1] in kept_as_is:
+            out.append(st)
+            continue
+        g = groups.get(st[-1])
+        if g is None:
+            continue
+        orig, cur = g
+        out.append(orig if list(cur) == list(orig[1:-2]) else ("nary",) + tuple(cur) + (orig[-2], orig[-1]))
+    return out
+
+
+def plan_stats(operand_labels, out_labels, dims, fuse=False):
+    """Algorithmic bytes / flops of the executed path (choose_path, fused as the compiled program runs it
+    when `fuse`; SURVEY.md §8(d) C2 definition): sum over steps of 8 (sum |inputs| + |C|) bytes and
+    (inputs) x |index space| flops."""
     steps, _ = choose_path(operand_labels, out_labels, dims)
+    if fuse:
+        steps = fuse_path(steps, operand_labels, dims)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     nbytes = flops = 0
     max_inter = sum_inter = 0
     for st in steps:
-        if st[0] == "reduce":
-            _, i, keep, nid = st
-            nbytes += 8 * (_size(labels[i], dims) + _size(keep, dims))
-            flops += _size(labels[i], dims)
-        else:
-            _, i, j, keep, nid = st
-            union = list(dict.fromkeys(labels[i] + labels[j]))
-            nbytes += 8 * (_size(labels[i], dims) + _size(labels[j], dims) + _size(keep, dims))
-            flops += 2 * _size(union, dims)
+        ins, keep, nid = st[1:-2], st[-2], st[-1]
+        space = list(dict.fromkeys(l for i in ins for l in labels[i]))
+        nbytes += 8 * (sum(_size(labels[i], dims) for i in ins) + _size(keep, dims))
+        flops += (1 if st[0] == "reduce" else 2 if st[0] == "pair" else len(ins)) * _size(space, dims)
         labels[nid] = keep
         max_inter = max(max_inter, _size(keep, dims))
         sum_inter += _size(keep, dims)
@@ -336,13 +400,13 @@ PACK_MIN_WORK = 1 << 20   # ... and at least this large an index space
 PATH_CACHE_SIZE = 256
 
 
-def compiled_path(operand_labels, out_labels, dims, order=None):
+def compiled_path(operand_labels, out_labels, dims, order=None, fuse=False):
     """choose_path (or, with `order`, order_path) plus, per pairwise step, the dense-GEMM
     classification (engine.gemm_shape), cached on the contraction's structure: repeated queries with
     the same query / evidence variables (C2's pattern; every row batch of a predict pattern) re-plan
-    nothing."""
+    nothing.  fuse: the steps that are neither GEMMs nor packed grouped into n-ary steps (fuse_path)."""
     key = (tuple(tuple((l, int(dims[l])) for l in ls) for ls in operand_labels), tuple(out_labels),
-           None if order is None else tuple(order))
+           None if order is None else tuple(order), bool(fuse))
     with _PATHS_LOCK:  # concurrent queries (engine.device_lock is shared) share this cache
         hit = _PATHS.get(key)
         if hit is not None:
@@ -352,11 +416,13 @@ def compiled_path(operand_labels, out_labels, dims, order=None):
         steps, final_id = choose_path(operand_labels, out_labels, dims)
     else:
         steps, final_id = order_path(operand_labels, out_labels, dims, order)
+    if fuse:
+        steps = _fuse_plain(steps, operand_labels, dims)
     labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
     plan = []
     for st in steps:
-        if st[0] == "reduce":
-            labels[st[3]] = st[2]
+        if st[0] in ("reduce", "nary"):
+            labels[st[-1]] = st[-2]
             plan.append((st, None))
             continue
         _, i, j, keep, nid = st
@@ -376,7 +442,7 @@ def compiled_path(operand_labels, out_labels, dims, order=None):
     depth = {i: 0 for i in range(len(operand_labels))}
     levels = []
     for k, (st, _) in enumerate(plan):
-        ins = (st[1],) if st[0] == "reduce" else (st[1], st[2])
+        ins = st[1:-2]
         d = 1 + max(depth[i] for i in ins)
         depth[st[-1]] = d
         while len(levels) < d:
@@ -388,6 +454,30 @@ def compiled_path(operand_labels, out_labels, dims, order=None):
         if len(_PATHS) > PATH_CACHE_SIZE:
             _PATHS.popitem(last=False)
     return hit
+
+
+def _specialising():
+    """Batches of compiled programs become plan-specialised kernels (hipRTC present, not disabled)."""
+    from .. import program as P
+
+    return bool(getattr(P, "BATCH_SPECIALISE", False)) and not os.environ.get("PGM_NO_JIT")
+
+
+def _fuse_plain(steps, operand_labels, dims):
+    """fuse_path over the steps that stay plain contractions: a pairwise step that is a dense GEMM
+    (engine.gemm_shape) or a packed long reduction keeps its own kernel, so it never joins a group
+    (its index space is beyond the budget anyway; checked here rather than assumed)."""
+    labels = {i: list(dict.fromkeys(ls)) for i, ls in enumerate(operand_labels)}
+    fixed = set()
+    for st in steps:
+        if st[0] == "pair":
+            _, i, j, keep, nid = st
+            if (E.gemm_shape(labels[i], labels[j], keep, dims) is not None or
+                    (_size(keep, dims) <= PACK_MAX_OUT and
+                     _size(list(dict.fromkeys(labels[i] + labels[j])), dims) >= PACK_MIN_WORK)):
+                fixed.add(nid)
+        labels[st[-1]] = st[-2]
+    return fuse_path(steps, operand_labels, dims, fixed=fixed)
 
 
 def contract_factors(operands, out_labels, reduce="sum", prog=None, order=None):
@@ -412,7 +502,10 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None, order=None):
     for l in out_labels:
         if l not in dims:
             raise ValueError(f"output label {l!r} not in any operand")
-    plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims, order=order)
+    # n-ary fusion for compiled plain programs whose batches become plan-specialised kernels (the only
+    # kernels that run n-ary jobs)
+    fuse = (FUSE and prog is not None and not getattr(prog, "_levels", True) and _specialising())
+    plan, final_id, levels = compiled_path([ls for _, ls in operands], out_labels, dims, order=order, fuse=fuse)
     live = {i: (t, list(ls)) for i, (t, ls) in enumerate(operands)}
 
     after = []  # contractions that read operands packed in the same level (recorded after its batch)
@@ -422,6 +515,9 @@ def contract_factors(operands, out_labels, reduce="sum", prog=None, order=None):
             _, i, keep, nid = st
             t, ls = live.pop(i)
             live[nid] = (run.contract(t, ls, None, None, keep, reduce=reduce, combine="copy"), keep)
+        elif st[0] == "nary":
+            ins, keep, nid = st[1:-2], st[-2], st[-1]
+            live[nid] = (prog.contract_n([live.pop(i) for i in ins], keep, reduce=reduce), keep)
         else:
             _, i, j, keep, nid = st
             ti, li = live.pop(i)

@@ -451,8 +451,9 @@ class PatternPlan:
         """SURVEY.md §8(d) C2 accounting of the steps path for n_rows rows: pairwise steps,
         algorithmic bytes (sum of 8 (|A| + |B| + |C|)), flops (2 |index space|), max intermediate;
         plus how many steps run as dense FP64 MFMA GEMMs."""
-        from .contraction import compiled_path
+        from .contraction import FUSE, _specialising, compiled_path
 
+        fuse = FUSE and _specialising()  # the compiled programs run the fused path (contract_factors)
         labels, dims = [], dict(self.card)
         dims[E.ROW] = n_rows
         for vars_, _ in self.factors:
@@ -460,8 +461,10 @@ class PatternPlan:
             if any(v in self.evidence_vars for v in vars_):
                 ls = ls + [E.ROW]
             labels.append(ls)
-        st = plan_stats(labels, self.variables + [E.ROW], dims)
-        plan, _, levels = compiled_path(labels, self.variables + [E.ROW], dims)
+        st = plan_stats(labels, self.variables + [E.ROW], dims, fuse=fuse)
+        plan, _, levels = compiled_path(labels, self.variables + [E.ROW], dims, fuse=fuse)
+        st["fused"] = fuse
+        st["nary_steps"] = sum(1 for p_, _ in plan if p_[0] == "nary")
         st["gemm_steps"] = sum(1 for _, shape in plan if shape is not None and shape != "pack")
         st["packed_steps"] = sum(1 for _, shape in plan if shape == "pack")
         st["levels"] = len(levels)

@@ -162,6 +162,8 @@ class Program:
         for kind, args, _ in jobs:
             if kind == "contract":
                 N.check(L.pgm_batch_add_contract(h, *args), "batch_add_contract")
+            elif kind == "contract_n":
+                N.check(L.pgm_batch_add_contract_n(h, *args), "batch_add_contract_n")
             else:
                 N.check(L.pgm_batch_add_gather(h, *args), "batch_add_gather")
 
@@ -200,7 +202,7 @@ class Program:
             return None
         chunks, cur, n = [], [], 0
         for j in jobs:
-            w = 4 if j[0] == "gather" else 3
+            w = 4 if j[0] == "gather" else (j[1][0]._obj.n_ops + 1) if j[0] == "contract_n" else 3
             if cur and n + w > 512:
                 chunks.append(cur)
                 cur, n = [], 0
@@ -232,6 +234,9 @@ class Program:
         parts = self._specialise_parts(b.jobs)
         if parts:
             return _PMStep(*parts), f"specialised batch of {len(b.jobs)} in {len(parts)} parts"
+        if any(kind == "contract_n" for kind, _, _ in b.jobs):
+            raise RuntimeError("a batch with n-ary contraction jobs was not specialised (hipRTC unavailable or "
+                               "PGM_NO_JIT set); contraction.FUSE plans them only when it is")
         if len(b.jobs) == 1:  # a job the generator does not take: its own planner's launch
             kind, _, args = b.jobs[0]
             if kind == "contract":
@@ -280,8 +285,8 @@ class Program:
             if WG_CHAIN_BLOCKS > 0 and len(group) >= 2:
                 # runs of consecutive tiny levels of contractions (each at most WG_CHAIN_BLOCKS blocks) ->
                 # one single-workgroup launch; the other levels keep one launch each
-                blocks = [self._batch_blocks(b) if all(kind == "contract" for kind, _, _ in b.jobs) else None
-                          for b in group]
+                blocks = [self._batch_blocks(b) if all(kind in ("contract", "contract_n") for kind, _, _ in b.jobs)
+                          else None for b in group]
                 k = 0
                 while k < len(group):
                     e = k
@@ -293,6 +298,9 @@ class Program:
                             sb = self._specialise(h)
                             if sb is not None:
                                 fn = _PMStep(sb)
+                            elif any(kind == "contract_n" for b in group[k:e] for kind, _, _ in b.jobs):
+                                raise RuntimeError("a single-workgroup chain with n-ary contraction jobs was not "
+                                                   "specialised")
                             else:
                                 fn = lambda s, hh=h: N.check(L.pgm_batch_run(hh, s), "batch_run")
                             steps.append(fn)
@@ -593,6 +601,19 @@ class Program:
         args = (ctypes.byref(d), N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb)
         self._emit(lambda s, a=args: N.check(L.pgm_contract(*a, s), "contract"), note, [A, B], [out, ws],
                    foot=H.contract_foot(d, N.ptr(A), N.ptr(B), N.ptr(out), N.ptr(ws), wsb))
+        return out
+
+    def contract_n(self, operands, out_labels, reduce="sum", out=None):
+        """C[out_labels] = REDUCE over the other labels of prod_i X_i (operands: (tensor, labels)) as ONE
+        job of the open batch (plain Program; pgm_batch_add_contract_n, specialised kernel only): a fused
+        group of a contraction path's pairwise steps (contraction.fuse_path)."""
+        if self._levels or self._batch is None:
+            raise RuntimeError("contract_n: a job of an open batch of a plain Program")
+        d, ptrs, out = E.prepare_contract_n(operands, out_labels, reduce, out)
+        self._keep.extend([d, ptrs, out] + [t for t, _ in operands])
+        self._batch.jobs.append(("contract_n", (ctypes.byref(d), ptrs, N.ptr(out)), None))
+        note = f"contract_n {reduce} {len(operands)} ops -> {list(out_labels)}"
+        self._batch_job(note, [t for t, _ in operands], [out], H.contract_n_foot(d, ptrs, N.ptr(out)))
         return out
 
     def _bind_marginal(self, A, la, out_labels, out, reduce):

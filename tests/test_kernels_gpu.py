@@ -1074,3 +1074,87 @@ def test_program_direct_chain_and_eligibility(gpu):
     assert not bad.bind_direct(dq)
     assert "not specialised" in bad.direct_note, bad.direct_note
     del y
+
+
+@pytest.mark.parametrize("chain", [False, True])
+def test_contract_n_jobs_match_numpy(gpu, chain):
+    """r06: n-ary contraction jobs (pgm_batch_add_contract_n, specialised kernel only): one level of a
+    plain Program with a 3-operand sum over two labels (nested literal loops), an 8-operand job, a long
+    reduction to few outputs (G lanes per output), a max-product, a broadcast product with no reduction
+    and a transposed output; chain=True records two dependent levels of them so they run as the
+    single-workgroup chain.  Each equals numpy's einsum (products as a left fold, rtol 1e-12)."""
+    import torch
+
+    from pgmpy_amd.program import Program
+
+    E = _e()
+    rng = np.random.default_rng(31)
+    X = [rng.random((3, 4)), rng.random((4, 5)), rng.random((5, 2))]
+    Y = [rng.random((2,)) + 0.1 for _ in range(7)] + [rng.random((2, 3))]
+    Z = [rng.random((2, 900)), rng.random((900, 4)), rng.random((4,))]
+    W = [rng.random((3, 6)), rng.random((6, 4)), rng.random((3,))]
+    V = [rng.random((5,)), rng.random((7,))]
+    T = [rng.random((4, 3, 2)), rng.random((2, 3))]
+    prog = Program()
+    prog.begin_batch()
+    o1 = prog.contract_n([(E.to_device(X[0]), ["a", "b"]), (E.to_device(X[1]), ["b", "c"]),
+                          (E.to_device(X[2]), ["c", "d"])], ["a", "d"])
+    o2 = prog.contract_n([(E.to_device(y), ["p"]) for y in Y[:7]] + [(E.to_device(Y[7]), ["p", "q"])], ["q"])
+    o3 = prog.contract_n([(E.to_device(Z[0]), ["a", "r"]), (E.to_device(Z[1]), ["r", "s"]),
+                          (E.to_device(Z[2]), ["s"])], ["a"])
+    o4 = prog.contract_n([(E.to_device(W[0]), ["a", "b"]), (E.to_device(W[1]), ["b", "c"]),
+                          (E.to_device(W[2]), ["a"])], ["c"], reduce="max")
+    o5 = prog.contract_n([(E.to_device(V[0]), ["i"]), (E.to_device(V[1]), ["j"])], ["j", "i"])
+    prog.end_batch()
+    if chain:
+        prog.begin_batch()
+        o6 = prog.contract_n([(o1, ["a", "d"]), (E.to_device(T[0]), ["x", "a", "d"]), (E.to_device(T[1]), ["d", "a"])],
+                             ["x"])
+        prog.end_batch()
+        prog.begin_batch()
+        o7 = prog.contract_n([(o6, ["x"]), (o3, ["a"])], ["a"])
+        prog.end_batch()
+    prog.run()
+    torch.cuda.synchronize()
+    assert all("specialised" in n or "levels in one workgroup" in n for n in prog.notes), prog.notes
+    r1 = np.einsum("ab,bc,cd->ad", *X)
+    r2 = np.einsum("p,p,p,p,p,p,p,pq->q", *Y)
+    r3 = np.einsum("ar,rs,s->a", *Z)
+    r4 = (W[0][:, :, None] * W[1][None, :, :] * W[2][:, None, None]).max(axis=(0, 1))
+    r5 = np.outer(V[1], V[0])
+    got = [(o1, r1), (o2, r2), (o3, r3), (o4, r4), (o5, r5)]
+    if chain:
+        r6 = np.einsum("ad,xad,da->x", r1, *T)
+        got += [(o6, r6), (o7, np.einsum("x,a->a", r6, r3))]
+    for o, r in got:
+        np.testing.assert_allclose(E.to_host(o), r, rtol=1e-12, atol=0)
+
+
+def test_fused_query_programs_match_unfused(gpu, monkeypatch):
+    """r06: compiled single queries with the path's pairwise steps fused into n-ary jobs
+    (contraction.fuse_path) — fewer dependency levels — equal the unfused programs (PGM_FUSE=0 path) on
+    the C2 munin rows and alarm's 50 C1 patterns, rtol 1e-10; the fused C2 program has fewer launches."""
+    import pgmpy_amd.inference.contraction as C
+    from pgmpy_amd.inference import VariableElimination
+    from pgmpy_amd.utils import get_example_model
+    from tests.goldens import load_json
+
+    c2 = load_json("munin_c2_rows.json")
+    c1 = load_json("alarm_queries.json")
+
+    def run(fuse):
+        monkeypatch.setattr(C, "FUSE", fuse)
+        C._PATHS.clear()
+        ve2 = VariableElimination(get_example_model("munin"))
+        ve1 = VariableElimination(get_example_model("alarm"))
+        out = [np.asarray(ve2.query_unnormalized(c2["variables"], r["evidence"]).values) for r in c2["rows"][:4]]
+        out += [np.asarray(ve1.query(p["variables"], p["evidence"], show_progress=False).values) for p in c1["patterns"]]
+        runner, = ve2._compiled.values()
+        prog = runner.plan.__dict__["_q1"]["joint"][0]
+        return out, len(prog._direct) if prog._direct else len(prog)
+
+    fused, n_fused = run(True)
+    plain, n_plain = run(False)
+    for a, b in zip(fused, plain):
+        np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-300)
+    assert n_fused < n_plain, (n_fused, n_plain)
