@@ -35,7 +35,7 @@
 #include "pgmhip.h"
 #include "pgm_internal.h"
 
-#define PGM_ABI_VERSION 22  // 22: pgm_dq_bind_pm / pgm_dq_run_chain / pgm_dq_profiling; 21: pgm_batch_specialise; 20: pgm_batch_info and the grid-barrier levelled batch removed (levels: single-workgroup mode only); 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
+#define PGM_ABI_VERSION 23  // 23: pgm_batch_add_contract_n (n-ary contraction jobs), pgm_dq_timer_dispatch_times, pgm_host_scan_* / pgm_host_lut_map_u8; 22: pgm_dq_bind_pm / pgm_dq_run_chain / pgm_dq_profiling; 21: pgm_batch_specialise; 20: pgm_batch_info and the grid-barrier levelled batch removed (levels: single-workgroup mode only); 19: pgm_stream_sync_spin; 18: pgm_batch_set_mode (single-workgroup levelled batch), pgm_batch_blocks; 17: pgm_rows_shard_run (rows sharded over several GPUs from host buffers); 16: pgm_rows_ring_start_ready; 15: pgm_batch_add_level / pgm_batch_info (levelled batch), pgm_memcpy_d2h_async; 14: pgm_rows_ring_* (resident ring of row batches); 13: pgm_dq_timer_dispatch_stats, pgm_rows_bound_kernel; 12: pgm_dq_launch_group, pgm_dq_timer_stop_ticks, PGM_ROWS_FLOOR; 11: pgm_product_n_marginal_bind / pgm_pm_bound_*; 10: pgm_dq_* direct AQL dispatch, pgm_codes_remap; 9: gemm lane_order, batch product_n / indicator
 
 // ----------------------------------------------------------------------------- errors
 static thread_local std::string g_err;

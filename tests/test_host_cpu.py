@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.pgm_version() == 22
+    assert lib.pgm_version() == 23
 
 
 def test_struct_layouts_match_header():
@@ -38,6 +38,7 @@ def test_struct_layouts_match_header():
     from pgmpy_amd import _native as N
 
     assert ctypes.sizeof(N.ContractDesc) == 16 + 7 * 8 * N.PGM_MAX_DIMS
+    assert ctypes.sizeof(N.ContractNDesc) == 16 + (3 + 2 * N.PRODN_MAX_OPS) * 8 * N.PGM_MAX_DIMS
     assert ctypes.sizeof(N.GatherDesc) == 16 + 16 + 6 * 8 * N.PGM_MAX_DIMS
     assert ctypes.sizeof(N.RowsPlan) == 4 * (8 + 3 * N.ROWS_MAX_LOOP + 5 * N.ROWS_MAX_COMP
                                              + N.ROWS_MAX_FAC * (3 + N.ROWS_MAX_LOOP) + 3 * N.ROWS_MAX_EV)
