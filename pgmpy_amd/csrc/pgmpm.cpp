@@ -995,12 +995,15 @@ int pgm_pm_bound_run(void *bound, void *stream) {
   return PGM_OK;
 }
 
-// a merged launch's kernel arguments stay within 4 KB (512 pointers)
+// a merged launch's kernel arguments stay within 4 KB (512 pointers); bodies per merged launch (a block finds
+// its body through a balanced tree of block-range compares, so the count costs log2 compares; r06: 64 -> 128,
+// C4's level 1 holds 74 specialised steps)
 static constexpr size_t kPmMaxArgPtrs = 512;
+static constexpr int kPmMaxBodies = 128;
 
 int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
   STALE_PROBE();
-  if (!bounds || !merged || n < 1 || n > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: 1..64 bound steps");
+  if (!bounds || !merged || n < 1 || n > kPmMaxBodies) return pgmi_failf(PGM_EINVAL, "pm_merge: 1..%d bound steps", kPmMaxBodies);
   *merged = nullptr;
   std::vector<PMSpec> specs;
   std::vector<const double *> ptrs;
@@ -1011,7 +1014,7 @@ int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
     specs.insert(specs.end(), b->specs.begin(), b->specs.end());
     ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
   }
-  if (specs.size() > 64) return pgmi_failf(PGM_EINVAL, "pm_merge: more than 64 bodies");
+  if (specs.size() > (size_t)kPmMaxBodies) return pgmi_failf(PGM_EINVAL, "pm_merge: more than %d bodies", kPmMaxBodies);
   if (ptrs.size() > kPmMaxArgPtrs) return PGM_OK;  // kernel arguments over 4 KB: keep the separate launches
   std::vector<uint64_t> starts;
   uint64_t blocks = 0;

@@ -32,6 +32,7 @@ PRODN_BATCH_MAX = 1 << 21
 # specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
 # take or that are below the engine's own threshold)
 PM_PREFER_MIN = 1 << 14  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
+X
 # plain programs: consecutive dependency levels of at most this many 256-thread blocks each, all of their
 # jobs contractions, run in ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP, k_batch_wg_c:
 # descriptors staged in LDS, a level's blocks four at a time in a 1,024-thread workgroup, a workgroup
@@ -307,7 +308,10 @@ class Program:
                             notes.append(f"{e - k} levels in one workgroup ({sum(blocks[k:e])} blocks, "
                                          f"{sum(len(b.jobs) for b in group[k:e])} jobs)")
                             # the same levels one launch each: _tune_chains keeps whichever form is faster
-                            self._chain_alts.append((fn, [self._batch_step(b) for b in group[k:e]]))
+                            # (built only when it will tune: each alternative is a specialised kernel that
+                            # _ready would otherwise compile and keep unused)
+                            if CHAIN_TUNE:
+                                self._chain_alts.append((fn, [self._batch_step(b) for b in group[k:e]]))
                             k = e
                             continue
                         e = k + 1  # tables over the LDS budget: one launch per level
@@ -531,9 +535,9 @@ class Program:
         L = N.lib()
         done = set()
         parts, cur, n_ptr = [], [], 0
-        for r in recs:  # <= 64 bodies and <= 512 kernel-argument pointers (operands + C + M each) per launch
+        for r in recs:  # <= PM_MERGE_BODIES bodies and <= 512 kernel-argument pointers (operands + C + M) per launch
             k = len(r.reads) + 2
-            if cur and (len(cur) == 64 or n_ptr + k > 512):
+            if cur and (len(cur) == PM_MERGE_BODIES or n_ptr + k > 512):
                 parts.append(cur)
                 cur, n_ptr = [], 0
             cur.append(r)
