@@ -520,6 +520,18 @@ int pgm_dq_launch_group(void *const *dbounds, int32_t n) {
   return PGM_OK;
 }
 
+uint16_t env_scope(const char *name) {
+  const char *v = getenv(name);
+  if (!v || !*v) return HSA_FENCE_SCOPE_AGENT;
+  return v[0] == '0' ? (uint16_t)HSA_FENCE_SCOPE_NONE : v[0] == '2' ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : (uint16_t)HSA_FENCE_SCOPE_AGENT;
+}
+
+// A/B knob (timing only): fence scope of a chain's inner packets (0 none, 1 agent = default)
+uint16_t chain_scope(const char *name) {
+  static const uint16_t acq = env_scope("PGM_DQ_CHAIN_ACQ"), rel = env_scope("PGM_DQ_CHAIN_REL");
+  return name[13] == 'A' ? acq : rel;
+}
+
 // a dependent chain (a compiled program's steps): every packet waits for the ones before it (barrier bit;
 // not on a packet flagged independent of its predecessor — the parts of one split level — except the
 // last, which always waits, so its completion signal and system-scope release cover the whole chain) and
@@ -592,8 +604,8 @@ int pgm_dq_run_chain(void *const *dbounds, const uint8_t *independent, int32_t n
       // in coherent (fine-grained) host memory the kernels read uncached, so no system-scope acquire (which
       // also dropped the CPT tables from L2 each query) is needed — C2 0.106 -> 0.103 ms, C1 0.043 -> 0.040
       // (profiles/r05an/); the last packet still releases at system scope for the host's reads
-      const uint16_t acq = (uint16_t)HSA_FENCE_SCOPE_AGENT;
-      const uint16_t rel = is_last ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : (uint16_t)HSA_FENCE_SCOPE_AGENT;
+      const uint16_t acq = i == 0 ? (uint16_t)HSA_FENCE_SCOPE_AGENT : chain_scope("PGM_DQ_CHAIN_ACQ");
+      const uint16_t rel = is_last ? (uint16_t)HSA_FENCE_SCOPE_SYSTEM : chain_scope("PGM_DQ_CHAIN_REL");
       const bool barrier = i == 0 || is_last || !independent || !independent[i];
       __atomic_store_n((uint32_t *)slot,
                        header_word(HSA_PACKET_TYPE_KERNEL_DISPATCH, acq, rel,

@@ -3427,15 +3427,19 @@ static void launch_batch_c(int spec, dim3 g, hipStream_t s, const BatchJob *jobs
 // a batch contraction job with a reduction takes G lanes per output (G a power of two up to the innermost
 // reduction extent) while its outputs x G stay under this many lanes (r04: 32 K / 128 K slower on C2,
 // profiles/r04p/)
-static constexpr uint64_t kBatchLanesCap = 4096;
+static uint64_t env_u64(const char *name, uint64_t dflt) {
+  const char *v = getenv(name);
+  return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
+static const uint64_t kBatchLanesCap = env_u64("PGM_BATCH_LANES_CAP", 4096);
 // workgroups one batch job may take (its lanes grid-stride over the job's outputs beyond that; r04:
 // 1,024 / 4,096 no faster on C1 / C2 / C4, profiles/r04j/)
-static constexpr uint64_t kBatchMaxBlocks = 256;
+static const uint64_t kBatchMaxBlocks = env_u64("PGM_BATCH_MAX_BLOCKS", 256);
 // a batch contraction without a reduction (a broadcast product or a copy: one load per operand per output)
 // may take more workgroups than one that reduces: its lanes otherwise walk several outputs one after
 // another, a full memory round trip each (C2's 448,000-output product level: 11.7 -> 8.9 us at 1,024
 // blocks, profiles/r04t/), while the reducing jobs of a level were measured slower with more
-static constexpr uint64_t kBatchMaxBlocksProduct = 1024;
+static const uint64_t kBatchMaxBlocksProduct = env_u64("PGM_BATCH_MAX_BLOCKS_PRODUCT", 1024);
 
 extern "C" {
 

@@ -1122,9 +1122,13 @@ static void cs_decode(std::string &o, const ContractK &k, int nk, bool use_b, co
 static void cs_red_loops_open(std::string &o, const ContractK &k, std::string &ind, uint64_t inner_trip) {
   uint64_t prod = inner_trip;
   int first_unrolled = k.nr - 1;
+  // the innermost reduction dims are unrolled while their trip product stays <= 64, so a 48-entry walk issues
+  // its loads together instead of in six dependent rounds (r06q/r06r: C2 91.4 -> 88.6 us; 16 before, 256 no
+  // better; PGM_CS_UNROLL_PROD is the A/B knob)
+  static const uint64_t unroll_prod = getenv("PGM_CS_UNROLL_PROD") ? strtoull(getenv("PGM_CS_UNROLL_PROD"), nullptr, 10) : 64;
   for (int r = k.nr - 2; r >= 0; --r) {
     prod *= k.rdiv[r].d;
-    if (prod > 16) break;
+    if (prod > unroll_prod) break;
     first_unrolled = r;
   }
   for (int r = 0; r < k.nr - 1; ++r) {
@@ -1298,11 +1302,12 @@ static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
     o += "      " + upd(prod(off)) + "\n    }\n";
   } else {
     std::string ind = "    ";
+    static const uint64_t unroll_prod = getenv("PGM_NARY_UNROLL_PROD") ? strtoull(getenv("PGM_NARY_UNROLL_PROD"), nullptr, 10) : 64;
     uint64_t inner = 1;
     int first_unrolled = k.nr;
     for (int r = k.nr - 1; r >= 0; --r) {
       inner *= k.rcard[r];
-      if (inner > 64) break;
+      if (inner > unroll_prod) break;
       first_unrolled = r;
     }
     for (int r = 0; r < k.nr; ++r) {
