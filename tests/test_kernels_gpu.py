@@ -1076,6 +1076,50 @@ def test_program_direct_chain_and_eligibility(gpu):
     del y
 
 
+def test_program_direct_chain_split_last_level(gpu):
+    """a chain whose LAST step is a level split into parts over the kernel-argument budget. The
+    parts after the first are independent packets, and only the chain's last packet carries the completion
+    signal and the system-scope release.  pgm_dq_run_chain gives that packet the barrier bit whatever its
+    flag, so run_direct returns only after every part has completed, and the host sees all of their
+    outputs, bit for bit as the graph replay writes them."""
+    import torch
+
+    from pgmpy_amd.inference.plan import DirectQueue
+    from pgmpy_amd.program import Program
+
+    E = _e()
+    rng = np.random.default_rng(23)
+    dq = DirectQueue()
+    prog = Program()
+    xs = [E.to_device(rng.random((8, 64))) for _ in range(200)]
+    W = [E.to_device(rng.random((8, 8)) / 4) for _ in range(200)]
+    prog.begin_batch()
+    mid = [prog.contract(W[i], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    prog.end_batch()
+    prog.begin_batch()  # the last level: 200 jobs x 3 pointers > 512, specialised in parts
+    out = [prog.contract(W[(i + 7) % 200], ["b", "a"], mid[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    prog.end_batch()
+    assert prog.bind_direct(dq), prog.direct_note
+    assert "parts" in prog.notes[-1], list(prog.notes)
+    want = [W[(i + 7) % 200] for i in range(200)]
+    for rep in range(3):
+        for t in out:
+            t.zero_()
+        torch.cuda.synchronize()
+        prog.run_direct()
+        got = [E.to_host(t).copy() for t in out]  # read right after the chain returned
+        for i, g in enumerate(got):
+            ref = E.to_host(want[i]) @ (E.to_host(W[i]) @ E.to_host(xs[i]))
+            np.testing.assert_allclose(g, ref, rtol=1e-12, err_msg=f"rep {rep} job {i}")
+    for t in out:
+        t.zero_()
+    torch.cuda.synchronize()
+    prog.run()
+    torch.cuda.synchronize()
+    for a, t in zip(got, out):
+        np.testing.assert_array_equal(a, E.to_host(t))
+
+
 @pytest.mark.parametrize("chain", [False, True])
 def test_contract_n_jobs_match_numpy(gpu, chain):
     """r06: n-ary contraction jobs (pgm_batch_add_contract_n, specialised kernel only): one level of a
