@@ -68,7 +68,7 @@ class _FastQuery:
     the full path) when the model or a CPD changed, or a value is not a state name of its table."""
 
     __slots__ = ("model", "epoch", "runner", "plan", "get_used", "tab_used", "get_rest", "tab_rest",
-                 "variables", "joint", "qtabs", "run_bytes")
+                 "variables", "joint", "qtabs", "run_bytes", "fast")
 
     def __init__(self, model, runner, ev_vars, tables, variables, joint, qtabs):
         plan = runner.plan
@@ -80,6 +80,7 @@ class _FastQuery:
         self.get_rest, self.tab_rest = (_tuple_getter(rest), [tab[v] for v in rest]) if rest else (None, None)
         self.variables, self.joint, self.qtabs = variables, joint, qtabs
         self.run_bytes = getattr(runner, "run_bytes", None)
+        self.fast = None  # runner.bytes_caller() once the program is on the query queue
 
     def __call__(self, evidence):
         if (self.run_bytes is None or getattr(self.model, "_epoch", None) != self.epoch
@@ -91,7 +92,13 @@ class _FastQuery:
                 bytes(map(dict.__getitem__, self.tab_rest, self.get_rest(evidence)))
         except (KeyError, TypeError, ValueError):
             return None
-        vals = self.run_bytes(codes)
+        fast = self.fast
+        if fast is None:
+            vals = self.run_bytes(codes)
+            getter = getattr(self.runner, "bytes_caller", None)
+            self.fast = (getter() if getter is not None else None) or False
+            return _query_result(self.plan, list(self.variables), self.joint, vals, self.qtabs)
+        vals = fast(codes) if fast else self.run_bytes(codes)
         return _query_result(self.plan, list(self.variables), self.joint, vals, self.qtabs)
 
 

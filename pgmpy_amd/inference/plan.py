@@ -34,6 +34,15 @@ from .contraction import contract_factors, plan_stats
 FUSED_MAX_SPACE = 4096  # query x hidden index space per row for the fused kernel
 
 
+def _values_epoch():
+    """factors.discrete.DiscreteFactor.values_epoch, imported once (is_current runs on every single query)."""
+    global _values_epoch
+    from ..factors.discrete.DiscreteFactor import values_epoch
+
+    _values_epoch = values_epoch
+    return values_epoch()
+
+
 class PatternPlan:
     """Compiled plan for (query variables, observed variables) on a DiscreteBayesianNetwork."""
 
@@ -101,11 +110,9 @@ class PatternPlan:
     def is_current(self):
         """True while the model structure and the values of every CPD this plan read are unchanged
         (the reference recomputes from the current CPDs on every call)."""
-        from ..factors.discrete.DiscreteFactor import values_epoch
-
         if getattr(self.model, "_epoch", None) != self._epoch:
             return False
-        ve = values_epoch()
+        ve = _values_epoch()
         if ve == self.__dict__.get("_vepoch"):
             # no factor's values were replaced or newly handed out since the last full check: only
             # the exposed sources (host arrays a caller may edit in place) need their CRC compared
@@ -716,6 +723,34 @@ class QueryRunner:
             self._prepared = True
         with self.lock:
             return self.plan.query_one(None, self.key, codes_bytes=codes)
+
+    def bytes_caller(self):
+        """run_bytes once the one-row program is bound to the query queue, as a closure with every lookup
+        made once: copy the codes into the mapped host buffer, run the AQL chain, copy the result out
+        (r06, _FastQuery's repeat calls).  None while the program is not built or not on the queue."""
+        plan = self.plan
+        hit = (plan.__dict__.get("_q1") or {}).get(self.key)
+        if hit is None or not hit[0]._direct:
+            return None
+        prog, host = hit
+        run = N.lib().pgm_dq_run_chain
+        arr, ind, cnt = prog._direct_arr, prog._direct_indep, len(prog._direct)
+        dst, n = host["codes"].array.ctypes.data, len(plan.ev_used)
+        out = host[self.key].array.reshape(-1)
+        memmove, lock, plock = ctypes.memmove, self.lock, plan._lock
+
+        def call(codes):
+            if len(codes) != n:
+                raise ValueError("query_one: one code per evidence column the plan reads")
+            with lock, plock:
+                if n:
+                    memmove(dst, codes, n)
+                if run(arr, ind, cnt):
+                    N.check(1, "dq_run_chain")
+                return out.copy()
+
+        call.keep = (prog, host)  # the chain's launches and buffers live as long as the closure
+        return call
 
     def run(self, codes, unnorm=False):
         """codes: state numbers of plan.evidence_vars (in that order). Returns a new fp64 ndarray:

@@ -45,7 +45,15 @@ def split(name, ve, calls, n):
             p.run_direct()
         ts.append((time.perf_counter() - t0) / len(progs))
     out["chains_us"] = statistics.median(ts) * 1e6
+    # the Python part alone: every chain made a no-op (the programs' run_direct, and the bound fast
+    # callers of repeat calls, QueryRunner.bytes_caller, which run the chain themselves)
     real = [p.run_direct for p in progs]
+    fast = ve.__dict__.get("_fast", {})
+    real_fast = {k: f.fast for k, f in fast.items()}
+    for f in fast.values():
+        if f.fast:
+            res = f.fast.keep[1][f.runner.key].array.reshape(-1)
+            f.fast = lambda codes, r=res: r.copy()
     for p in progs:
         p.run_direct = lambda: None
     try:
@@ -59,6 +67,8 @@ def split(name, ve, calls, n):
     finally:
         for p, r in zip(progs, real):
             p.run_direct = r
+        for k, f in fast.items():
+            f.fast = real_fast[k]
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(22)
     print(json.dumps(out, indent=1))
