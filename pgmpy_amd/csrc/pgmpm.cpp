@@ -1286,9 +1286,65 @@ static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
     for (int t = 0; t < n; ++t) off.push_back("o" + std::to_string(t));
     o += "    acc = " + prod(off) + ";\n";
   } else if (G > 1) {
-    pgmi_appendf(o, "    #pragma unroll 4\n    for (unsigned r = lane_g; r < %uu; r += %uu) {\n      unsigned ri = r;", k.n_red, G);
+    // the G lanes of an output stride over the flattened index of the OUTER reduction dims [0, s) only — the
+    // fewest outer dims whose product reaches G — and walk the inner dims [s, nr) as literal nested loops:
+    // digits are decoded once per outer index instead of once per summed entry (r06; PGM_NARY_SPLIT=0: the
+    // whole reduction index flattened and decoded per entry, as before)
+    static const bool split = !getenv("PGM_NARY_SPLIT") || getenv("PGM_NARY_SPLIT")[0] != '0';
+    int sd = k.nr;
+    uint64_t pout = 1;
+    for (int i = 0; i < k.nr; ++i) {
+      pout *= k.rcard[i];
+      if (pout >= G) {
+        sd = i + 1;
+        break;
+      }
+    }
+    if (!split || sd >= k.nr) {
+      sd = k.nr;
+      pout = k.n_red;
+    }
+    pgmi_appendf(o, "    #pragma unroll %d\n    for (unsigned r = lane_g; r < %lluu; r += %uu) {\n      unsigned ri = r;",
+                 sd == k.nr ? 4 : 1, (unsigned long long)pout, G);
     for (int t = 0; t < n; ++t) pgmi_appendf(o, " long long p%d = o%d;", t, t);
     o += "\n";
+    if (sd < k.nr) {
+      for (int i = sd - 1; i >= 0; --i) {
+        const unsigned d = k.rcard[i];
+        if (i == 0) o += "      { const unsigned g_ = ri;";
+        else pgmi_appendf(o, "      { const unsigned q_ = ri / %uu, g_ = ri - q_ * %uu; ri = q_;", d, d);
+        for (int t = 0; t < n; ++t)
+          if (k.rs[t][i]) pgmi_appendf(o, " p%d += (long long)g_ * %lldLL;", t, (long long)k.rs[t][i]);
+        o += " }\n";
+      }
+      static const uint64_t unroll_in = getenv("PGM_NARY_UNROLL_PROD") ? strtoull(getenv("PGM_NARY_UNROLL_PROD"), nullptr, 10) : 64;
+      uint64_t inner = 1;
+      int first_unrolled = k.nr;
+      for (int r = k.nr - 1; r >= sd; --r) {
+        inner *= k.rcard[r];
+        if (inner > unroll_in) break;
+        first_unrolled = r;
+      }
+      std::string ind = "      ";
+      for (int r = sd; r < k.nr; ++r) {
+        pgmi_appendf(o, "%s#pragma unroll%s\n", ind.c_str(), r >= first_unrolled ? "" : " 2");
+        pgmi_appendf(o, "%sfor (unsigned r%d = 0; r%d < %uu; ++r%d) {\n", ind.c_str(), r, r, k.rcard[r], r);
+        ind += "  ";
+      }
+      std::vector<std::string> off;
+      for (int t = 0; t < n; ++t) {
+        std::string e = "p" + std::to_string(t);
+        for (int r = sd; r < k.nr; ++r)
+          if (k.rs[t][r]) e += " + (long long)r" + std::to_string(r) + " * " + std::to_string((long long)k.rs[t][r]) + "LL";
+        off.push_back(e);
+      }
+      o += ind + upd(prod(off)) + "\n";
+      for (int r = sd; r < k.nr; ++r) {
+        ind.resize(ind.size() - 2);
+        o += ind + "}\n";
+      }
+      o += "    }\n";
+    } else {
     for (int i = k.nr - 1; i >= 0; --i) {
       const unsigned d = k.rcard[i];
       if (i == 0) o += "      { const unsigned g_ = ri;";
@@ -1300,6 +1356,7 @@ static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
     std::vector<std::string> off;
     for (int t = 0; t < n; ++t) off.push_back("p" + std::to_string(t));
     o += "      " + upd(prod(off)) + "\n    }\n";
+    }
   } else {
     std::string ind = "    ";
     static const uint64_t unroll_prod = getenv("PGM_NARY_UNROLL_PROD") ? strtoull(getenv("PGM_NARY_UNROLL_PROD"), nullptr, 10) : 64;

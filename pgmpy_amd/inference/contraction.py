@@ -303,11 +303,14 @@ def choose_path(operand_labels, out_labels, dims):
 
 # r06: the pairwise steps of a compiled single-row path fused into n-ary steps (fuse_path) of at most
 # FUSE_BUDGET index-space entries each: fewer dependency levels, i.e. fewer dependent launches per query
+# (512 Ki / 512 since the n-ary kernels' lanes stride over the outer reduction dims only and walk the inner
+# ones as literal loops: C2 16 -> 11 launches, 85-86.5 -> 78.8 us per query; 1 Mi entries: slower again,
+# profiles/r06ab/, r06ad/.  64 Ki / 64 before: with a per-entry index decode longer walks cost more than the
+# launches they saved, r06g-r06i)
 FUSE = os.environ.get("PGM_FUSE", "1") != "0"
-FUSE_BUDGET = int(os.environ.get("PGM_FUSE_BUDGET", 1 << 16))
-# reduction entries per output of a fused step: each lane walks them one dependent round of loads after
-# another, so a long walk costs more than the launches it saves
-FUSE_MAX_RED = int(os.environ.get("PGM_FUSE_MAX_RED", 64))
+FUSE_BUDGET = int(os.environ.get("PGM_FUSE_BUDGET", 1 << 19))
+# reduction entries per output of a fused step
+FUSE_MAX_RED = int(os.environ.get("PGM_FUSE_MAX_RED", 512))
 # absorb only the inputs on the step's critical path (the deepest): absorbing a shallower one saves no
 # level, it only lengthens the job's walk
 FUSE_CRITICAL_ONLY = os.environ.get("PGM_FUSE_CRIT", "1") != "0"

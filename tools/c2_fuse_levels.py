@@ -3,7 +3,7 @@
 the jobs (kind, outputs, reduction entries per output, inputs), and each lowered step's time replayed
 alone (Program.time_steps).
 
-    python3 tools/c2_fuse_levels.py [budget]"""
+    python3 tools/c2_fuse_levels.py [budget [max_red]]"""
 import json
 import os
 import sys
@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(budget=None):
+def main(budget=None, max_red=None):
     import torch
 
     import pgmpy_amd.inference.contraction as C
@@ -22,9 +22,11 @@ def main(budget=None):
 
     if budget:
         C.FUSE_BUDGET = int(budget)
+    if max_red:
+        C.FUSE_MAX_RED = int(max_red)
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "munin_c2_rows.json")))
     q = g["variables"]
-    for fuse in (True, False):
+    for fuse in ((True,) if os.environ.get("FUSED_ONLY") else (True, False)):
         C.FUSE = fuse
         C._PATHS.clear()
         ve = VariableElimination(get_example_model("munin"))
