@@ -3643,9 +3643,10 @@ static int plan_contract_n(const pgm_contractn_desc *d, const double *const *ops
   k.n_red = (uint32_t)n_red;
   // lanes per output: up to 64 while the job's lanes stay under 4x a batch contraction's cap (a fused
   // step's reduction is a walk of dependent load rounds; more lanes, fewer rounds each)
+  static const uint64_t nary_lanes = env_u64("PGM_NARY_LANES", 4 * kBatchLanesCap);
   int g = 0;
   if (k.nr > 0)
-    while (g < 6 && ((uint64_t)k.n_out << g) < 4 * kBatchLanesCap && (1ull << (g + 1)) <= n_red) ++g;
+    while (g < 6 && ((uint64_t)k.n_out << g) < nary_lanes && (1ull << (g + 1)) <= n_red) ++g;
   k.g_log2 = g;
   return PGM_OK;
 }
