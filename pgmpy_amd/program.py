@@ -79,10 +79,11 @@ class _PMStep:
     a specialised contraction batch), or of several independent ones (a level batch over the kernel-argument
     budget, in parts); `bounds` are their handles, which a direct AQL chain re-binds (Program.bind_direct)."""
 
-    __slots__ = ("bounds",)
+    __slots__ = ("bounds", "batch")
 
     def __init__(self, *bounds):
         self.bounds = bounds
+        self.batch = None  # the level batch it runs, when it runs one (profiling: Program.time_step_jobs)
 
     def __call__(self, s):
         L = N.lib()
@@ -231,10 +232,14 @@ class Program:
         N.check(L.pgm_batch_finalize(h), "batch_finalize")
         sb = self._specialise(h)
         if sb is not None:
-            return _PMStep(sb), f"specialised batch of {len(b.jobs)}"
+            st = _PMStep(sb)
+            st.batch = b
+            return st, f"specialised batch of {len(b.jobs)}"
         parts = self._specialise_parts(b.jobs)
         if parts:
-            return _PMStep(*parts), f"specialised batch of {len(b.jobs)} in {len(parts)} parts"
+            st = _PMStep(*parts)
+            st.batch = b
+            return st, f"specialised batch of {len(b.jobs)} in {len(parts)} parts"
         if any(kind == "contract_n" for kind, _, _ in b.jobs):
             raise RuntimeError("a batch with n-ary contraction jobs was not specialised (hipRTC unavailable or "
                                "PGM_NO_JIT set); contraction.FUSE plans them only when it is")
@@ -823,6 +828,51 @@ class Program:
             out.append((ms.value * 1e3 / reps, note))
         L.pgm_event_destroy(a)
         L.pgm_event_destroy(b)
+        return out
+
+    def time_step_jobs(self, i, reps=20):
+        """[(us, kind, descriptor summary)] for each job of step i (a specialised level batch), each job
+        specialised and replayed alone (profiling aid: which job of a level sets its time)."""
+        import ctypes as C
+
+        self._ready()
+        st = self._steps[i]
+        b = getattr(st, "batch", None)
+        if b is None:
+            return []
+        L = N.lib()
+        s = N.stream_handle()
+        ev0, ev1 = C.c_void_p(), C.c_void_p()
+        N.check(L.pgm_event_create(C.byref(ev0)))
+        N.check(L.pgm_event_create(C.byref(ev1)))
+        out = []
+        for job in b.jobs:
+            h = self._new_batch()
+            self._add_batch_jobs(h, [job])
+            N.check(L.pgm_batch_finalize(h), "batch_finalize")
+            sb = self._specialise(h)
+            if sb is None:
+                continue
+            N.check(L.pgm_pm_bound_run(sb, s))
+            N.check(L.pgm_event_record(ev0, s))
+            for _ in range(reps):
+                N.check(L.pgm_pm_bound_run(sb, s))
+            N.check(L.pgm_event_record(ev1, s))
+            ms = C.c_float()
+            N.check(L.pgm_event_elapsed_ms(ev0, ev1, C.byref(ms)))
+            d = job[1][0]
+            d = getattr(d, "_obj", d)
+            if job[0] == "contract_n":
+                desc = {"n_ops": int(d.n_ops), "keep": [int(d.keep_card[q]) for q in range(d.n_keep)],
+                        "red": [int(d.red_card[q]) for q in range(d.n_red)]}
+            elif job[0] == "contract":
+                desc = {"keep": [int(d.keep_card[q]) for q in range(d.n_keep)],
+                        "red": [int(d.red_card[q]) for q in range(d.n_red)]}
+            else:
+                desc = {}
+            out.append((ms.value * 1e3 / reps, job[0], desc))
+        L.pgm_event_destroy(ev0)
+        L.pgm_event_destroy(ev1)
         return out
 
     # ------------------------------------------------------------------ execution

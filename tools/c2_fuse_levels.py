@@ -59,9 +59,12 @@ def main(budget=None, max_red=None):
             print(f"  level {li:2d}: {len(jobs):3d} jobs, work {work:9d}, heaviest {big}")
         prog = plan.__dict__["_q1"]["joint"][0]
         tot = 0.0
-        for us, note in prog.time_steps(reps=20):
+        for i, (us, note) in enumerate(prog.time_steps(reps=20)):
             tot += us
             print(f"  {us:7.2f} us  {note[:100]}")
+            if us > 4.5 and os.environ.get("JOB_TIMES"):  # the slowest jobs of a slow launch, each alone
+                for t, kind, desc in sorted(prog.time_step_jobs(i), key=lambda r: -r[0])[:4]:
+                    print(f"      {t:6.2f} us  {kind} {desc}")
         print(f"  {tot:.1f} us summed; {prog.direct_note}")
 
 
