@@ -195,6 +195,14 @@ struct PMBound {
   std::vector<PMSpec> specs;
   std::vector<const double *> ptrs;  // per body: its n_ops operands, then C, M
   unsigned threads = 256;  // workitems per workgroup (a specialised contraction chain: 1,024)
+  // a contraction batch over the kernel-argument budget: its pointers in device memory, ptrs = {table}
+  void *table = nullptr;
+  PMBound() = default;
+  PMBound(const PMBound &) = delete;
+  PMBound &operator=(const PMBound &) = delete;
+  ~PMBound() {
+    if (table) (void)hipFree(table);
+  }
 };
 
 static int pm_knob(const char *name, int dflt) {
@@ -999,6 +1007,7 @@ int pgm_pm_bound_run(void *bound, void *stream) {
 // its body through a balanced tree of block-range compares, so the count costs log2 compares; r06: 64 -> 128,
 // C4's level 1 holds 74 specialised steps)
 static constexpr size_t kPmMaxArgPtrs = 512;
+static constexpr size_t kPmMaxTablePtrs = 8192;  // a specialised contraction batch's pointers through a table
 static constexpr int kPmMaxBodies = 128;
 
 int pgm_pm_merge(void *const *bounds, int32_t n, void **merged) {
@@ -1403,7 +1412,10 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
   // no limit but the kernel-argument budget of 170 jobs)
   std::vector<int> base(n + 1, 0);
   for (int j = 0; j < n; ++j) base[j + 1] = base[j] + cs_nptrs(jobs[j]);
-  if (no_jit || n < 1 || base[n] > (int)kPmMaxArgPtrs) return PGM_OK;
+  // over 512 pointers (4 KB of kernel arguments) the kernel reads them from a table in device memory instead
+  // (r06: C2's first path level is 106 jobs / ~600 pointers; as two kernels its second packet cost ~2.5 us)
+  const bool table = base[n] > (int)kPmMaxArgPtrs;
+  if (no_jit || n < 1 || base[n] > (int)kPmMaxTablePtrs) return PGM_OK;
   for (int j = 0; j < n; ++j) {
     if (jobs[j].kind == 1) {
       const GatherK &g = jobs[j].g;
@@ -1430,7 +1442,10 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
     o += jobs[j].kind == 1   ? cs_gather_body(jobs[j], "cj" + std::to_string(j))
          : jobs[j].kind == 2 ? cs_nary_body(jobs[j], "cj" + std::to_string(j))
                              : cs_job_body(jobs[j], "cj" + std::to_string(j));
-  pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", base[n]);
+  if (table)
+    o += "struct pgm_pm_args { const double *const *__restrict__ p; };\n";
+  else
+    pgmi_appendf(o, "struct pgm_pm_args { const double *p[%d]; };\n", base[n]);
   // jobs [j0, j1) by block b: a balanced tree of literal comparisons (the jobs' block ranges ascend)
   std::function<void(std::string &, int, int, std::string)> dispatch = [&](std::string &s, int j0, int j1,
                                                                             std::string ind) {
@@ -1506,6 +1521,18 @@ int pgmi_cs_bind(const pgmi_cs_job *jobs, int n, const uint32_t *level_off, int 
       b->ptrs.push_back(jobs[q].B);
       b->ptrs.push_back(jobs[q].C);
     }
+  }
+  if (table) {
+    const size_t bytes = b->ptrs.size() * sizeof(void *);
+    hipError_t e = hipMalloc(&b->table, bytes);
+    if (e == hipSuccess) e = hipMemcpy(b->table, b->ptrs.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      delete b;
+      return pgmi_failf(e == hipErrorOutOfMemory ? PGM_ENOMEM : PGM_EDEVICE, "batch_specialise: pointer table: %s",
+                        hipGetErrorString(e));
+    }
+    b->ptrs.assign(1, (const double *)b->table);
   }
   *bound = b;
   return PGM_OK;

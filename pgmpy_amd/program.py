@@ -51,6 +51,9 @@ CHAIN_TUNE = False
 # plan-specialised kernel (pgm_batch_specialise) instead of the descriptor-driven k_batch_c /
 # k_batch_wg_c (r05).  A/B knob PGM_BATCH_RTC=0
 BATCH_SPECIALISE = os.environ.get("PGM_BATCH_RTC", "1") != "0"
+# A/B knob: a level batch of more jobs than this as that many jobs per kernel, the parts independent packets
+# (0: one kernel per level unless over the kernel-argument budget)
+PART_JOBS = int(os.environ.get("PGM_PART_JOBS", 0))
 
 
 def _key(t):
@@ -196,7 +199,7 @@ class Program:
         self._pm_bound.append(b)
         return b
 
-    def _specialise_parts(self, jobs):
+    def _specialise_parts(self, jobs, max_jobs=0):
         """A level batch whose kernel arguments exceed one specialised kernel's budget (512 pointers: a
         contraction takes 3, a gather 4; C2's 205-gather level) as consecutive parts that each fit, every
         part specialised; None when there is nothing to split or a part is not taken."""
@@ -205,7 +208,7 @@ class Program:
         chunks, cur, n = [], [], 0
         for j in jobs:
             w = 4 if j[0] == "gather" else (j[1][0]._obj.n_ops + 1) if j[0] == "contract_n" else 3
-            if cur and n + w > 512:
+            if cur and (n + w > 512 or (max_jobs and len(cur) >= max_jobs)):
                 chunks.append(cur)
                 cur, n = [], 0
             cur.append(j)
@@ -227,6 +230,12 @@ class Program:
 
     def _batch_step(self, b):
         L = N.lib()
+        if PART_JOBS and len(b.jobs) > PART_JOBS:
+            parts = self._specialise_parts(b.jobs, PART_JOBS)
+            if parts:
+                st = _PMStep(*parts)
+                st.batch = b
+                return st, f"specialised batch of {len(b.jobs)} in {len(parts)} parts"
         h = self._new_batch()
         self._add_batch_jobs(h, b.jobs)
         N.check(L.pgm_batch_finalize(h), "batch_finalize")

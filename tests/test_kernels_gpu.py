@@ -1044,10 +1044,11 @@ def test_program_direct_chain_and_eligibility(gpu):
     rng = np.random.default_rng(21)
     dq = DirectQueue()
     prog = Program()
-    xs = [E.to_device(rng.random((8, 4))) for _ in range(200)]
+    NJ = 3000  # independent jobs x 3 pointers > 8,192 (the pointer table's limit): specialised in parts
+    xs = [E.to_device(rng.random((8, 4))) for _ in range(NJ)]
     W = [E.to_device(rng.random((8, 8)) / 4) for _ in range(200)]
-    prog.begin_batch()  # 200 independent jobs x 3 pointers > 512: specialised in parts
-    cur = [prog.contract(W[i], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    prog.begin_batch()
+    cur = [prog.contract(W[i % 200], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(NJ)]
     prog.end_batch()
     for lv in range(5):
         prog.begin_batch()
@@ -1091,17 +1092,18 @@ def test_program_direct_chain_split_last_level(gpu):
     rng = np.random.default_rng(23)
     dq = DirectQueue()
     prog = Program()
-    xs = [E.to_device(rng.random((8, 64))) for _ in range(200)]
+    NJ = 3000
+    xs = [E.to_device(rng.random((8, 64))) for _ in range(NJ)]
     W = [E.to_device(rng.random((8, 8)) / 4) for _ in range(200)]
     prog.begin_batch()
-    mid = [prog.contract(W[i], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    mid = [prog.contract(W[i % 200], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(NJ)]
     prog.end_batch()
-    prog.begin_batch()  # the last level: 200 jobs x 3 pointers > 512, specialised in parts
-    out = [prog.contract(W[(i + 7) % 200], ["b", "a"], mid[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(200)]
+    prog.begin_batch()  # the last level: 3,000 jobs x 3 pointers > 8,192, specialised in parts
+    out = [prog.contract(W[(i + 7) % 200], ["b", "a"], mid[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(NJ)]
     prog.end_batch()
     assert prog.bind_direct(dq), prog.direct_note
     assert "parts" in prog.notes[-1], list(prog.notes)
-    want = [W[(i + 7) % 200] for i in range(200)]
+    want = [W[(i + 7) % 200] for i in range(NJ)]
     for rep in range(3):
         for t in out:
             t.zero_()
@@ -1109,7 +1111,7 @@ def test_program_direct_chain_split_last_level(gpu):
         prog.run_direct()
         got = [E.to_host(t).copy() for t in out]  # read right after the chain returned
         for i, g in enumerate(got):
-            ref = E.to_host(want[i]) @ (E.to_host(W[i]) @ E.to_host(xs[i]))
+            ref = E.to_host(want[i]) @ (E.to_host(W[i % 200]) @ E.to_host(xs[i]))
             np.testing.assert_allclose(g, ref, rtol=1e-12, err_msg=f"rep {rep} job {i}")
     for t in out:
         t.zero_()
@@ -1118,6 +1120,40 @@ def test_program_direct_chain_split_last_level(gpu):
     torch.cuda.synchronize()
     for a, t in zip(got, out):
         np.testing.assert_array_equal(a, E.to_host(t))
+
+
+def test_specialised_batch_pointer_table(gpu):
+    """r06: a level batch over 512 pointers (4 KB of kernel arguments) is ONE specialised kernel that reads its
+    pointers from a table in device memory (instead of parts, one packet each); graph replay and the direct
+    chain give numpy's values."""
+    import torch
+
+    from pgmpy_amd.inference.plan import DirectQueue
+    from pgmpy_amd.program import Program
+
+    E = _e()
+    rng = np.random.default_rng(29)
+    prog = Program()
+    xs = [E.to_device(rng.random((6, 10))) for _ in range(400)]
+    W = [E.to_device(rng.random((5, 6))) for _ in range(400)]
+    prog.begin_batch()  # 400 jobs x 3 pointers = 1,200
+    out = [prog.contract(W[i], ["b", "a"], xs[i], ["a", "r"], ["b", "r"], reduce="sum") for i in range(400)]
+    prog.end_batch()
+    prog.begin_batch()
+    tot = [prog.contract(out[i], ["b", "r"], None, None, ["r"], reduce="sum", combine="copy") for i in range(0, 400, 7)]
+    prog.end_batch()
+    assert prog.bind_direct(DirectQueue()), prog.direct_note
+    assert prog.notes[0] == "specialised batch of 400", list(prog.notes)
+    for run in ("direct", "graph"):
+        for t in out + tot:
+            t.zero_()
+        torch.cuda.synchronize()
+        prog.run_direct() if run == "direct" else prog.run()
+        torch.cuda.synchronize()
+        for i in range(400):
+            np.testing.assert_allclose(E.to_host(out[i]), E.to_host(W[i]) @ E.to_host(xs[i]), rtol=1e-12)
+        for k, i in enumerate(range(0, 400, 7)):
+            np.testing.assert_allclose(E.to_host(tot[k]), (E.to_host(W[i]) @ E.to_host(xs[i])).sum(0), rtol=1e-12)
 
 
 @pytest.mark.parametrize("chain", [False, True])
