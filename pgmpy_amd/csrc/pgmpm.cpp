@@ -1200,8 +1200,18 @@ static std::string cs_job_body(const pgmi_cs_job &J, const std::string &name) {
     return o;
   }
   const unsigned G = 1u << k.g_log2;
-  if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
-  pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  // G lanes of an output at stride 64/G within a wave, as the n-ary jobs (cs_nary_body; PGM_NARY_LANEMAP)
+  static const bool lanemap = !getenv("PGM_NARY_LANEMAP") || getenv("PGM_NARY_LANEMAP")[0] != '0';
+  const bool lm = G > 1 && G < 64 && lanemap;
+  if (lm) {
+    const unsigned P = 64u / G;
+    pgmi_appendf(o, "  const unsigned lane_g = (tid & 63u) / %uu;\n", P);
+    pgmi_appendf(o, "  for (unsigned out = (tid >> 6) * %uu + (tid & %uu); out < %uu; out += (nth >> 6) * %uu) {\n", P, P - 1,
+                 k.n_out, P);
+  } else {
+    if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
+    pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  }
   o += "    unsigned idx = out;\n    long long oa = 0, ob = 0, oc = 0; (void)ob;\n";
   cs_decode(o, k, k.nk, use_b, "    ");
   pgmi_appendf(o, "    double acc = %s;\n", init);
@@ -1220,7 +1230,7 @@ static std::string cs_job_body(const pgmi_cs_job &J, const std::string &name) {
   pgmi_appendf(o, "%s}\n", ind.c_str());
   cs_red_loops_close(o, k, ind);
   if (G > 1 && J.red != PGM_RED_NONE)
-    for (unsigned off = G >> 1; off > 0; off >>= 1)
+    for (unsigned off = lm ? 32u : G >> 1; off > 0 && off >= (lm ? 64u / G : 1u); off >>= 1)
       pgmi_appendf(o, "    %s\n", cs_red(J.red, "acc", "__shfl_xor(acc, " + std::to_string(off) + ", 64)").c_str());
   pgmi_appendf(o, "    %sC[oc] = acc;\n  }\n}\n", G > 1 ? "if (lane_g == 0) " : "");
   return o;
@@ -1267,8 +1277,20 @@ static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
   for (int t = 0; t < n; ++t) pgmi_appendf(o, ", const double *__restrict__ X%d", t);
   o += ", double *__restrict__ C) {\n";
   const unsigned G = 1u << k.g_log2;
-  if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
-  pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  // lanes of an output: G > 1 takes the G lanes of an output at stride 64/G within a wave (lane_g = the high
+  // lane bits), so a wave's consecutive lanes hold consecutive outputs and an operand that is unit-stride
+  // along the output's fastest dim is read in runs instead of one line per lane (PGM_NARY_LANEMAP=0: the G
+  // lanes of an output adjacent, as before)
+  static const bool lanemap = !getenv("PGM_NARY_LANEMAP") || getenv("PGM_NARY_LANEMAP")[0] != '0';
+  if (G > 1 && G < 64 && lanemap) {
+    const unsigned P = 64u / G;
+    pgmi_appendf(o, "  const unsigned lane_g = (tid & 63u) / %uu;\n", P);
+    pgmi_appendf(o, "  for (unsigned out = (tid >> 6) * %uu + (tid & %uu); out < %uu; out += (nth >> 6) * %uu) {\n", P, P - 1,
+                 k.n_out, P);
+  } else {
+    if (G > 1) pgmi_appendf(o, "  const unsigned lane_g = tid & %uu;\n", G - 1);
+    pgmi_appendf(o, "  for (unsigned out = tid >> %d; out < %uu; out += nth >> %d) {\n", k.g_log2, k.n_out, k.g_log2);
+  }
   o += "    unsigned idx = out; long long oc = 0;";
   for (int t = 0; t < n; ++t) pgmi_appendf(o, " long long o%d = 0;", t);
   o += "\n";
@@ -1394,7 +1416,10 @@ static std::string cs_nary_body(const pgmi_cs_job &J, const std::string &name) {
       o += ind + "}\n";
     }
   }
-  if (G > 1)
+  if (G > 1 && G < 64 && lanemap)
+    for (unsigned off = 32; off >= 64u / G; off >>= 1)
+      pgmi_appendf(o, "    %s\n", upd("__shfl_xor(acc, " + std::to_string(off) + ", 64)").c_str());
+  else if (G > 1)
     for (unsigned off = G >> 1; off > 0; off >>= 1)
       pgmi_appendf(o, "    %s\n", upd("__shfl_xor(acc, " + std::to_string(off) + ", 64)").c_str());
   pgmi_appendf(o, "    %sC[oc] = acc;\n  }\n}\n", G > 1 ? "if (lane_g == 0) " : "");

@@ -66,6 +66,20 @@ def main(budget=None, max_red=None):
                 for t, kind, desc in sorted(prog.time_step_jobs(i), key=lambda r: -r[0])[:4]:
                     print(f"      {t:6.2f} us  {kind} {desc}")
         print(f"  {tot:.1f} us summed; {prog.direct_note}")
+        dump = os.environ.get("DUMP_SRC")
+        if dump and fuse:  # each launch's generated source (compile it with hipcc to read its resources)
+            import ctypes
+
+            from pgmpy_amd import _native as N
+
+            os.makedirs(dump, exist_ok=True)
+            L, buf = N.lib(), ctypes.create_string_buffer(1 << 22)
+            for i, st in enumerate(prog._steps):
+                for j, b in enumerate(getattr(st, "bounds", ())):
+                    n = L.pgm_pm_bound_source(b, buf, len(buf))
+                    if n > 0:
+                        with open(os.path.join(dump, f"step_{i}_{j}.hip"), "w") as f:
+                            f.write(buf.value.decode())
 
 
 if __name__ == "__main__":
