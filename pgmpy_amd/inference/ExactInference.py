@@ -67,8 +67,8 @@ class _FastQuery:
     name anywhere still takes the full path and its reference error.  Returns None (the caller takes
     the full path) when the model or a CPD changed, or a value is not a state name of its table."""
 
-    __slots__ = ("model", "epoch", "runner", "plan", "get_used", "tab_used", "get_rest", "tab_rest",
-                 "variables", "joint", "qtabs", "run_bytes", "fast")
+    __slots__ = ("model", "epoch", "runner", "plan", "get_all", "tab_all", "n_used", "variables", "joint", "qtabs",
+                 "run_bytes", "fast")
 
     def __init__(self, model, runner, ev_vars, tables, variables, joint, qtabs):
         plan = runner.plan
@@ -76,8 +76,8 @@ class _FastQuery:
         tab = dict(zip(ev_vars, tables))
         used = list(plan.ev_used)
         rest = [v for v in ev_vars if v not in set(used)]
-        self.get_used, self.tab_used = _tuple_getter(used), [tab[v] for v in used]
-        self.get_rest, self.tab_rest = (_tuple_getter(rest), [tab[v] for v in rest]) if rest else (None, None)
+        # one pass over every evidence value, the plan's columns first: bytes(...)[:n_used] are its codes
+        self.get_all, self.tab_all, self.n_used = _tuple_getter(used + rest), [tab[v] for v in used + rest], len(used)
         self.variables, self.joint, self.qtabs = variables, joint, qtabs
         self.run_bytes = getattr(runner, "run_bytes", None)
         self.fast = None  # runner.bytes_caller() once the program is on the query queue
@@ -87,11 +87,11 @@ class _FastQuery:
                 or not self.plan.is_current()):
             return None
         try:
-            codes = bytes(map(dict.__getitem__, self.tab_used, self.get_used(evidence)))
-            if self.get_rest is not None:
-                bytes(map(dict.__getitem__, self.tab_rest, self.get_rest(evidence)))
+            codes = bytes(map(dict.__getitem__, self.tab_all, self.get_all(evidence)))
         except (KeyError, TypeError, ValueError):
             return None
+        if len(codes) != self.n_used:
+            codes = codes[:self.n_used]
         fast = self.fast
         if fast is None:
             vals = self.run_bytes(codes)

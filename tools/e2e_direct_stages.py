@@ -86,6 +86,18 @@ def main(n_calls=30):
         out["d2h_%d_MB_us" % (marg.nbytes >> 20)] = med(lambda: N.check(L.pgm_memcpy_d2h_async(
             marg.ctypes.data_as(ctypes.c_void_p), N.ptr(dev), marg.nbytes, s)))
     print(json.dumps(out, indent=1))
+    import cProfile
+    import io
+    import pstats
+
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(20):
+        B._direct_categorical(model, df, order, True)
+    pr.disable()
+    sio = io.StringIO()
+    pstats.Stats(pr, stream=sio).sort_stats("tottime").print_stats(25)
+    print(sio.getvalue())
 
 
 if __name__ == "__main__":
