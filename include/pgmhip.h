@@ -364,7 +364,10 @@ int pgm_batch_run(void *handle, void *stream);
  * or descriptor is read (C1 / C2's path levels).  *bound = NULL when a job is not a contraction the
  * generator takes (the generic pgm_batch_run stays); else prepare / run / destroy it with
  * pgm_pm_prepare, pgm_pm_bound_run, pgm_pm_bound_destroy (not pgm_pm_merge).  The batch's pointers
- * must stay valid; the batch handle itself may be destroyed. */
+ * must stay valid; the batch handle itself may be destroyed.  Up to 512 job pointers travel as the
+ * kernel's arguments; a batch of more (up to 8,192) gets its pointer array copied into device memory
+ * here and the kernel reads them from that table (freed with the bound launch); *bound = NULL above
+ * 8,192 (split the batch). */
 int pgm_batch_specialise(void *handle, void **bound);
 int pgm_batch_destroy(void *handle);
 
