@@ -771,7 +771,9 @@ static int pm_bind(const pgm_productn_desc *d, const double *const *ops, double 
   // r03ag, after the schedule changes (direct collect operands, 128-block fused floor): 2^18 / 2^16 / 2^14
   // -> 0.96-0.97 / 1.024-1.026 / 1.026-1.028 M calibrations/s at 1,000 rows, 1.27-1.28 / 1.28-1.29 /
   // 1.29 M at 4,000 (small steps specialised join their level's merged launch instead of launching alone)
-  static const int64_t min_entries = getenv("PGM_PM_MIN_ENTRIES") ? atoll(getenv("PGM_PM_MIN_ENTRIES")) : (1ll << 14);
+  // r06at: 2^12 (was 2^14) — C4's smallest steps (the 4-state F29/F92 clique) join their level's merged launch
+  // instead of running as generic kernels: +0.5-0.7 % at 4,000 / 1,000 rows (PGM_PM_MIN_ENTRIES A/B knob)
+  static const int64_t min_entries = getenv("PGM_PM_MIN_ENTRIES") ? atoll(getenv("PGM_PM_MIN_ENTRIES")) : (1ll << 12);
   // per step, at least this many row pairs per lane when the rows fill them: 2 measured (MI355X, C4
   // 4,000 rows: 1.146 -> 1.18 M calibrations/s; 1,000 rows unchanged, too few rows; forced 2 / 4 for
   // every step, or a minimum of 4: slower, profiles/r02bw_c4_xi.txt)

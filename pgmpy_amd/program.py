@@ -31,7 +31,8 @@ PRODN_BATCH_MAX = 1 << 21
 # levelled programs: n-ary products / separator marginals at least this large (entries) become
 # specialised steps merged per level instead of level-batch jobs (the bind declines shapes it cannot
 # take or that are below the engine's own threshold)
-PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 14))  # C4 1,000 rows: 0.97 -> 1.03M (r03ag)
+# C4 1,000 rows: 0.97 -> 1.03M (r03ag, 2^14); r06at: 2^12 with the generator's own threshold, +0.5-0.7 %
+PM_PREFER_MIN = int(os.environ.get("PGM_PM_PREFER_MIN", 1 << 12))
 PM_MERGE_BODIES = int(os.environ.get("PGM_PM_MERGE_BODIES", 64))  # pgm_pm_merge takes up to 128; 128 measured neutral on C4 (r06n)
 # plain programs: consecutive dependency levels of at most this many 256-thread blocks each, all of their
 # jobs contractions, run in ONE single-workgroup launch (pgm_batch_set_mode ONE_WORKGROUP, k_batch_wg_c:
